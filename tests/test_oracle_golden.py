@@ -1,0 +1,114 @@
+"""CPU: pin the oracle (oracle/dstagnn_ref.py) against the reference's own outputs.
+
+The fixtures in tests/golden/ were produced by importing /root/reference
+(tests/golden/gen_golden.py).  These tests never touch the reference itself.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dstagnn_ref as ref
+
+TOL = dict(rtol=1e-4, atol=1e-4)
+
+
+def load(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name), allow_pickle=False))
+
+
+def T(a):
+    return torch.from_numpy(np.asarray(a))
+
+
+def close(a, b, **kw):
+    a = a.detach().numpy() if torch.is_tensor(a) else np.asarray(a)
+    np.testing.assert_allclose(a, np.asarray(b), **(kw or TOL))
+
+
+def test_laplacian_cheb_pems04(golden_dir):
+    g = load(golden_dir, "g6_laplacian_pems04.npz")
+    Lt = ref.scaled_laplacian(T(g["adj_tmd"]))
+    close(Lt, g["L_tilde"], rtol=1e-5, atol=1e-6)
+    cps = ref.cheb_polynomials(Lt.numpy(), 3)
+    for k in range(3):
+        close(cps[k].astype(np.float32), g[f"cheb_{k}"], rtol=1e-5, atol=1e-6)
+    # quirk 4: elementwise recurrence keeps the support of L~ u I
+    supp = (g["L_tilde"] != 0) | np.eye(307, dtype=bool)
+    assert np.all((g["cheb_2"] != 0) <= supp)
+
+
+@pytest.mark.parametrize("name", ["g1_cheb_pems04.npz", "g5_cheb_dense.npz"])
+@pytest.mark.parametrize("hoist", [False, True])
+def test_cheb_conv_sat(golden_dir, name, hoist):
+    g = load(golden_dir, name)
+    m = json.loads(str(g["meta"]))
+    K = m["K"]
+    x = T(g["x"]).requires_grad_(True)
+    sat = T(g["spatial_attention"]).requires_grad_(True)
+    th = [T(g[f"Theta_{k}"]).requires_grad_(True) for k in range(K)]
+    mk = [T(g[f"mask_{k}"]).requires_grad_(True) for k in range(K)]
+    cheb = [T(g[f"cheb_{k}"]) for k in range(K)]
+    out = ref.cheb_conv_sat(x, sat, T(g["adj_pa"]), th, mk, cheb, hoist=hoist)
+    close(out, g["out"])
+    (out * T(g["g_out"])).sum().backward()
+    close(x.grad, g["grad_x"])
+    close(sat.grad, g["grad_spatial_attention"], rtol=1e-4, atol=1e-5)
+    for k in range(K):
+        close(th[k].grad, g[f"grad_Theta_{k}"], rtol=1e-4, atol=1e-4)
+        close(mk[k].grad, g[f"grad_mask_{k}"], rtol=1e-4, atol=1e-5)
+
+
+def block_case(golden_dir, name):
+    g = load(golden_dir, name)
+    m = json.loads(str(g["meta"]))
+    p = {k[6:]: T(v) for k, v in g.items() if k.startswith("param/")}
+    cheb = [T(g[f"cheb_{k}"]) for k in range(m["K"])]
+    dims = dict(n_heads=m["n_heads"], d_k=m["d_k"], d_v=m["d_v"], K=m["K"])
+    res = T(g["res_att"]) if "res_att" in g else 0
+    return g, m, p, cheb, dims, res
+
+
+@pytest.mark.parametrize("name", ["g2_block_first.npz", "g3_block_inner.npz", "g3b_block_inner_full.npz"])
+def test_block(golden_dir, name):
+    g, m, p, cheb, dims, res = block_case(golden_dir, name)
+    out, re_at, gx, gra, grads = ref.block_forward_backward(p, T(g["x"]), res, cheb, T(g["adj_pa"]), dims,
+                                                            T(g["g_out"]), T(g["g_re"]))
+    close(out, g["out"])
+    close(re_at, g["re_at"])
+    close(gx, g["grad_x"])
+    if "grad_res_att" in g:
+        close(gra, g["grad_res_att"])
+    for k, v in grads.items():
+        if "grad/" + k in g:
+            close(v, g["grad/" + k], rtol=2e-4, atol=2e-4)
+        else:
+            # quirk 11: params unused by this block kind keep grad None
+            assert v is None, k
+
+
+def test_model(golden_dir):
+    g = load(golden_dir, "g4_model.npz")
+    m = json.loads(str(g["meta"]))
+    sd = {k[6:]: T(v).clone().requires_grad_(True) for k, v in g.items() if k.startswith("param/")}
+    blocks, final = ref.split_state_dict(sd, m["nb_block"])
+    cheb = [T(g[f"cheb_{k}"]) for k in range(m["K"])]
+    dims = dict(n_heads=m["n_heads"], d_k=m["d_k"], d_v=m["d_v"], K=m["K"])
+    out = ref.model_forward(blocks, final, T(g["x"]), cheb, T(g["adj_pa"]), dims)
+    close(out, g["out"])
+    loss = torch.nn.SmoothL1Loss()(out, T(g["target"]))
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    loss.backward()
+    for k, v in sd.items():
+        if bool(g["hasgrad/" + k]):
+            close(v.grad, g["grad/" + k], rtol=2e-4, atol=2e-4)
+        else:
+            assert v.grad is None, k
+
+
+def test_gambia_failure_recorded(golden_dir):
+    with open(os.path.join(golden_dir, "g9_gambia_error.json")) as f:
+        err = json.load(f)
+    assert err["type"] == "RuntimeError" and "must match" in err["message"]
