@@ -1,0 +1,21 @@
+# Builds the in-tree C-ABI library dstagnn_drought_amd/libdstagnn.so for gfx950 (MI355X).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CXXFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+SRC := $(wildcard dstagnn_drought_amd/csrc/*.hip)
+OBJ := $(patsubst dstagnn_drought_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB := dstagnn_drought_amd/libdstagnn.so
+
+all: $(LIB)
+
+build/%.o: dstagnn_drought_amd/csrc/%.hip dstagnn_drought_amd/csrc/*.hpp include/dstagnn.h
+	@mkdir -p build
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

@@ -1,0 +1,233 @@
+#!/usr/bin/env python
+"""Benchmark: DSTAGNN_block forward+backward samples/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): one INNER DSTAGNN_block of the
+PEMS08 geometry — B=32 per GPU, N=170, F=C=32, T=12, K=3, n_heads=3, d_model=512,
+d_k=d_v=32, res_att (B,1,h,T,T) — train mode (both Dropout(0.05) on), random
+make_model-style init, synthetic x ~ N(0,1), seeded d_out / d_re_At.
+A step = forward + backward of one batch through the HIP library (+ the RCCL
+all-reduce of the parameter gradients when --gpus > 1: data parallel, weak scaling).
+
+Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel
+(gemm_f32_hot_kernel = the pre_conv forward GEMM, M=B*N, N=d_model, K=F*T), timed
+live with HIP events on the stream it runs on; `cpu_baseline` is the CPU oracle
+(a literal restatement of the reference's loops, oracle/dstagnn_ref.py) timed on
+this host's cores on a bounded sample.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CFG = dict(B=32, N=170, T=12, K=3, n_heads=3, d_model=512, d_k=32, C=32)
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (vector == f32 MFMA), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def synth_graph(N, seed=0):
+    rs = np.random.RandomState(seed)
+    tmd = np.eye(N)
+    pa = np.zeros((N, N))
+    for i in range(N):
+        tmd[i, rs.choice([j for j in range(N) if j != i], 2, replace=False)] = 1.0
+        pa[i, rs.choice(N, 4, replace=False)] = 1.0
+    return tmd, pa
+
+
+def build_block(device):
+    import dstagnn_drought_amd as D
+    c = CFG
+    tmd, pa = synth_graph(c["N"])
+    Lt = D.scaled_Laplacian(torch.FloatTensor(tmd))
+    cheb = [torch.from_numpy(p).float() for p in D.cheb_polynomial(Lt.numpy(), c["K"])]
+    torch.manual_seed(1)
+    blk = D.DSTAGNN_block("cpu", c["C"], c["C"], c["K"], c["C"], c["C"], 1, cheb, pa, tmd, c["N"], c["T"],
+                          c["d_model"], c["d_k"], c["d_k"], c["n_heads"])
+    for p in blk.parameters():  # make_model init (model/DSTAGNN_my.py:292-296)
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+        else:
+            torch.nn.init.uniform_(p)
+    return blk.to(device).train(), cheb, torch.FloatTensor(pa)
+
+
+def algorithmic_flops_per_sample(c=CFG):
+    """SURVEY.md §8(d) formula (sparse-T_k count, fwd; fwd+bwd = 3x)."""
+    B, N, F, T, h, dk, D, K, C = 1, c["N"], c["C"], c["T"], c["n_heads"], c["d_k"], c["d_model"], c["K"], c["C"]
+    nnzT = 4 * N
+    fwd = 2 * (3 * F * T * N * h * dk + 2 * F * h * T * T * dk + F * T * h * dk * N + N * D * T * F
+               + 2 * N * D * K * dk + K * N * N * dk + K * nnzT * F * T + K * N * T * F * C
+               + sum(N * (T - k + 1) * 2 * C * C * k for k in (3, 5, 7)) + C * N * (3 * T - 12) * T)
+    return 3 * fwd
+
+
+def cpu_baseline(budget_s=12.0):
+    """Oracle (literal restatement of the reference loops) on this host's cores."""
+    from oracle import dstagnn_ref as ref
+    c = CFG
+    torch.set_num_threads(os.cpu_count() or 1)
+    threads = torch.get_num_threads()
+    gen = torch.Generator().manual_seed(0)
+    tmd, pa = synth_graph(c["N"])
+    Lt = ref.scaled_laplacian(tmd)
+    cheb = [torch.from_numpy(p).float() for p in ref.cheb_polynomials(Lt, c["K"])][:c["K"]]
+    p = ref.random_block_params(gen, c["C"], c["C"], c["K"], c["C"], c["N"], c["T"], c["d_model"], c["d_k"], c["d_k"],
+                                c["n_heads"])
+    B = c["B"]
+    x = torch.randn(B, c["N"], c["C"], c["T"], generator=gen)
+    res = torch.randn(B, 1, c["n_heads"], c["T"], c["T"], generator=gen)
+    g_out = torch.randn(B, c["N"], c["C"], c["T"], generator=gen)
+    g_re = torch.randn(B, c["C"], c["n_heads"], c["T"], c["T"], generator=gen)
+    dims = dict(n_heads=c["n_heads"], d_k=c["d_k"], d_v=c["d_k"], K=c["K"])
+    apa = torch.from_numpy(pa).float()
+    ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, hoist=False)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, hoist=False)
+        n += 1
+        if time.perf_counter() - t0 > budget_s or n >= 20:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} fwd+bwd iterations of the PEMS08 inner block at B={B} (oracle, literal T x K loop), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hot-iters", type=int, default=50)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from dstagnn_drought_amd import _lib
+    from dstagnn_drought_amd.block_fn import make_dims, workspace_sizes, _fill
+    import dstagnn_drought_amd.block_fn as bf
+
+    blk, cheb, apa = build_block(dev)
+    c = CFG
+    B = c["B"]
+    gen = torch.Generator(device=dev).manual_seed(100 + rank)
+    x = torch.randn(B, c["N"], c["C"], c["T"], device=dev, generator=gen)
+    res = torch.randn(B, 1, c["n_heads"], c["T"], c["T"], device=dev, generator=gen)
+    g_out = torch.randn(B, c["N"], c["C"], c["T"], device=dev, generator=gen)
+    g_re = torch.randn(B, c["C"], c["n_heads"], c["T"], c["T"], device=dev, generator=gen)
+    params = [p for p in blk.parameters()]
+
+    def step():
+        for p in params:
+            p.grad = None
+        out, re_at = blk(x, res)
+        torch.autograd.backward([out, re_at], [g_out, g_re])
+        if world > 1:
+            grads = [p.grad for p in params if p.grad is not None]
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            dist.all_reduce(flat)
+            flat.div_(world)
+            off = 0
+            for g in grads:
+                n = g.numel()
+                g.copy_(flat[off:off + n].view_as(g))
+                off += n
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+
+    # ---- dominant kernel: the pre_conv fwd GEMM (gemm_f32_hot_kernel), HIP events on its stream
+    meta = dict(blk.meta, train=True, seed=1)
+    dims = make_dims(x, meta, _lib.RES_BCAST, True, 1)
+    sv, sc = workspace_sizes(dims)
+    save = torch.empty(sv, dtype=torch.uint8, device=dev)
+    scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
+    names, ps = zip(*blk.named_parameters())
+    pstruct = _fill(_lib.BlockParams(), names, ps)
+    gstruct = _lib.Graph(blk.cheb_conv_SAt.cheb_stack.data_ptr(), blk.adj_pa.data_ptr())
+    out = torch.empty(B, c["N"], c["C"], c["T"], device=dev)
+    re_at = torch.empty(B, c["C"], c["n_heads"], c["T"], c["T"], device=dev)
+    lib = _lib.load()
+    st = _lib.stream_handle(dev)
+    args_common = (ctypes.byref(dims), ctypes.byref(pstruct), ctypes.byref(gstruct), _lib.ptr(x), _lib.ptr(res),
+                   _lib.ptr(out), _lib.ptr(re_at), _lib.ptr(save), sv, _lib.ptr(scratch), sc)
+    _lib.check(lib.dstagnn_block_forward(*args_common, st), "forward")
+    ms = ctypes.c_float(0)
+    _lib.check(lib.dstagnn_block_time_stage(*args_common, 10, 3, ctypes.byref(ms), st), "hot warmup")
+    _lib.check(lib.dstagnn_block_time_stage(*args_common, 10, args.hot_iters, ctypes.byref(ms), st), "hot timing")
+    hot_ms = ms.value
+    M, Nn, Kk = B * c["N"], c["d_model"], c["C"] * c["T"]
+    hot_flops = 2.0 * M * Nn * Kk
+    achieved = hot_flops / (hot_ms * 1e-3) / 1e12
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "hot_kernel_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get("bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+    roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+            "kernel": "gemm_f32_hot_kernel (pre_conv fwd GEMM %dx%dx%d)" % (M, Nn, Kk),
+            "avg_launch_us": round(hot_ms * 1e3, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        line = {
+            "metric": "DSTAGNN_block fwd+bwd samples/sec (B,N=170,T=12) @1/2/4/8 GPU; %HBM roofline",
+            "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "PEMS08 inner DSTAGNN_block fwd+bwd (train mode, dropout 0.05)",
+                       "global_batch": B * world, "per_gpu_batch": B, "N": c["N"], "T": c["T"], "F": c["C"],
+                       "K": c["K"], "n_heads": c["n_heads"], "d_model": c["d_model"], "d_k": c["d_k"],
+                       "parallelism": f"dp{world}"},
+            "algorithmic_tflops": round(algorithmic_flops_per_sample() * value / 1e12, 3),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

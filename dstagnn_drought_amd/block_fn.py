@@ -1,0 +1,153 @@
+"""torch.autograd.Function over the HIP block (libdstagnn.so).
+
+One forward call and one backward call per DSTAGNN_block: every stage of
+model/DSTAGNN_my.py:225-253 and its gradient runs in our own gfx950 kernels,
+launched on torch's current HIP stream.  PyTorch only provides the device
+memory (caching allocator) and the stream.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+# block-local state_dict name -> (struct field, index or None)
+PARAM_MAP = {
+    "pre_conv.weight": ("pre_conv_w", None), "pre_conv.bias": ("pre_conv_b", None),
+    "EmbedT.pos_embed.weight": ("embT_pos", None), "EmbedT.norm.weight": ("embT_g", None),
+    "EmbedT.norm.bias": ("embT_b", None),
+    "EmbedS.pos_embed.weight": ("embS_pos", None), "EmbedS.norm.weight": ("embS_g", None),
+    "EmbedS.norm.bias": ("embS_b", None),
+    "TAt.W_Q.weight": ("tat_wq", None), "TAt.W_K.weight": ("tat_wk", None), "TAt.W_V.weight": ("tat_wv", None),
+    "TAt.fc.weight": ("tat_fc", None), "TAt.layer_norm.weight": ("tat_ln_g", None),
+    "TAt.layer_norm.bias": ("tat_ln_b", None),
+    "SAt.W_Q.weight": ("sat_wq", None), "SAt.W_K.weight": ("sat_wk", None),
+    "gtu3.con2out.weight": ("gtu_w", 0), "gtu3.con2out.bias": ("gtu_b", 0),
+    "gtu5.con2out.weight": ("gtu_w", 1), "gtu5.con2out.bias": ("gtu_b", 1),
+    "gtu7.con2out.weight": ("gtu_w", 2), "gtu7.con2out.bias": ("gtu_b", 2),
+    "residual_conv.weight": ("res_w", None), "residual_conv.bias": ("res_b", None),
+    "fcmy.0.weight": ("fcmy_w", None), "fcmy.0.bias": ("fcmy_b", None),
+    "ln.weight": ("ln_g", None), "ln.bias": ("ln_b", None),
+}
+for _k in range(_lib.MAX_K):
+    PARAM_MAP[f"cheb_conv_SAt.Theta.{_k}"] = ("theta", _k)
+    PARAM_MAP[f"cheb_conv_SAt.mask.{_k}"] = ("mask", _k)
+
+# parameters a block of each kind never touches (quirk 11: their .grad stays None)
+UNUSED_INNER = ("EmbedT.", "residual_conv.")
+
+
+def _fill(struct, names, tensors):
+    for n, t in zip(names, tensors):
+        if t is None:
+            continue
+        field, i = PARAM_MAP[n]
+        if i is None:
+            setattr(struct, field, t.data_ptr())
+        else:
+            getattr(struct, field)[i] = t.data_ptr()
+    return struct
+
+
+def res_mode_of(res_att, F):
+    if not torch.is_tensor(res_att):
+        if res_att != 0:
+            raise RuntimeError("res_att must be 0 or a tensor (model/DSTAGNN_my.py:37)")
+        return _lib.RES_NONE
+    if res_att.dim() != 5:
+        raise RuntimeError(f"res_att must be 5-D (B,F|1,h,T,T), got {tuple(res_att.shape)}")
+    if res_att.shape[1] == F:
+        return _lib.RES_FULL
+    if res_att.shape[1] == 1:
+        return _lib.RES_BCAST
+    raise RuntimeError(f"The size of tensor a ({F}) must match the size of tensor b ({res_att.shape[1]}) "
+                       "at non-singleton dimension 1")
+
+
+def make_dims(x, meta, res_mode, train, seed):
+    B, N, F, T = x.shape
+    return _lib.BlockDims(B, N, F, T, meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"],
+                          meta["C"], res_mode, 1 if train else 0, float(meta.get("drop_p", 0.05)), seed)
+
+
+def workspace_sizes(dims):
+    lib = _lib.load()
+    sv, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _lib.check(lib.dstagnn_block_sizes(ctypes.byref(dims), ctypes.byref(sv), ctypes.byref(sc)), "dstagnn_block_sizes")
+    return sv.value, sc.value
+
+
+class DSTAGNNBlockFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, names, x, res_att, cheb, adj_pa, *params):
+        lib = _lib.load()
+        ctx.set_materialize_grads(False)
+        dev = x.device
+        x = x.contiguous()
+        B, N, F, T = x.shape
+        mode = res_mode_of(res_att if res_att is not None else 0, F)
+        ra = res_att.contiguous() if mode != _lib.RES_NONE else None
+        train = bool(meta.get("train", False))
+        seed = int(meta.get("seed", 0))
+        dims = make_dims(x, meta, mode, train, seed)
+        sv, sc = workspace_sizes(dims)
+        save = torch.empty(sv, dtype=torch.uint8, device=dev)
+        scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
+        out = torch.empty(B, N, meta["C"], T, dtype=torch.float32, device=dev)
+        re_at = torch.empty(B, F, meta["n_heads"], T, T, dtype=torch.float32, device=dev)
+        p = _fill(_lib.BlockParams(), names, params)
+        g = _lib.Graph(cheb.data_ptr(), adj_pa.data_ptr())
+        rc = lib.dstagnn_block_forward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
+                                       _lib.ptr(ra), _lib.ptr(out), _lib.ptr(re_at), _lib.ptr(save), sv,
+                                       _lib.ptr(scratch), sc, _lib.stream_handle(dev))
+        _lib.check(rc, "dstagnn_block_forward")
+        del scratch
+        ctx.meta, ctx.names, ctx.mode, ctx.dims = meta, names, mode, dims
+        ctx.save_buf, ctx.sizes = save, (sv, sc)
+        ctx.save_for_backward(x, ra if ra is not None else torch.empty(0, device=dev), cheb, adj_pa, *params)
+        return out, re_at
+
+    @staticmethod
+    def backward(ctx, d_out, d_re_at):
+        lib = _lib.load()
+        x, ra, cheb, adj_pa, *params = ctx.saved_tensors
+        dev = x.device
+        names, mode, dims = ctx.names, ctx.mode, ctx.dims
+        if d_out is None:
+            d_out = torch.zeros(dims.B, dims.N, dims.C, dims.T, device=dev)
+        d_out = d_out.contiguous()
+        d_re_at = d_re_at.contiguous() if d_re_at is not None else None
+        first = dims.F == 1
+        grads = []
+        for n, t in zip(names, params):
+            used = first or not n.startswith(UNUSED_INNER)
+            grads.append(torch.empty_like(t) if used else None)
+        gs = _fill(_lib.BlockGrads(), names, grads)
+        p = _fill(_lib.BlockParams(), names, params)
+        g = _lib.Graph(cheb.data_ptr(), adj_pa.data_ptr())
+        d_x = torch.empty_like(x)
+        d_ra = torch.empty_like(ra) if mode != _lib.RES_NONE else None
+        sv, sc = ctx.sizes
+        scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
+        rc = lib.dstagnn_block_backward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
+                                        _lib.ptr(ra if mode != _lib.RES_NONE else None), _lib.ptr(d_out),
+                                        _lib.ptr(d_re_at), _lib.ptr(d_x), _lib.ptr(d_ra), ctypes.byref(gs),
+                                        _lib.ptr(ctx.save_buf), sv, _lib.ptr(scratch), sc,
+                                        _lib.stream_handle(dev))
+        _lib.check(rc, "dstagnn_block_backward")
+        ctx.save_buf = None
+        return (None, None, d_x, d_ra, None, None, *grads)
+
+
+def dropout_masks(meta, x_shape, seed):
+    """The exact keep-masks (scaled by 1/(1-p)) the HIP forward draws for `seed`:
+    (mask after EmbedS (B,N,D), mask after fcmy (B,N,C,T)) — for parity tests."""
+    lib = _lib.load()
+    B, N, F, T = x_shape
+    dims = _lib.BlockDims(B, N, F, T, meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"],
+                          meta["C"], 0, 1, float(meta.get("drop_p", 0.05)), seed)
+    m0 = torch.empty(B, N, meta["d_model"], device="cuda")
+    m1 = torch.empty(B, N, meta["C"], T, device="cuda")
+    _lib.check(lib.dstagnn_dropout_mask(ctypes.byref(dims), 0, _lib.ptr(m0), _lib.stream_handle()), "mask0")
+    _lib.check(lib.dstagnn_dropout_mask(ctypes.byref(dims), 1, _lib.ptr(m1), _lib.stream_handle()), "mask1")
+    return m0, m1

@@ -1,0 +1,887 @@
+// block.hip — DSTAGNN_block forward / backward orchestration and the C-ABI (include/dstagnn.h).
+//
+// Mirrors DSTAGNN_block.forward (model/DSTAGNN_my.py:225-253) stage by stage; every
+// stage is one of our own HIP kernels (gemm.hip, ops.hip) launched asynchronously on
+// the caller's stream.  Layouts in HBM (fp32, row-major):
+//   x (B,N,F,T)           E (B,F,T,N)          qkv (B*F*T, 2h*dk+h*dv)
+//   O (B,F,T,N)           Zd (B*N, D)          qk  (B*N, 2K*dk)  [Q' | K']
+//   P, W (B,K,N,N)        xth (B,N,K,C,T) = x Theta_k (the Theta-first order of the
+//                         Chebyshev product, so the aggregation writes (B,N,C,T) directly)
+//   X (B,N,C,T)           conv_g (B*N, 2C, T-k+1)   G (B*N, C, 3T-12)   out (B,N,C,T)
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "common.hpp"
+#include "ops.hpp"
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& s) { g_last_error = s; }
+
+namespace {
+
+// ------------------------------------------------------------------------------
+// buffer plan: carving of the save / scratch buffers (identical in sizes/fwd/bwd)
+// ------------------------------------------------------------------------------
+struct Arena {
+  char* base;
+  size_t off = 0;
+  explicit Arena(void* b) : base((char*)b) {}
+  float* take(size_t floats) {
+    off = (off + 255) & ~size_t(255);
+    float* p = base ? (float*)(base + off) : nullptr;
+    off += floats * sizeof(float);
+    return p;
+  }
+};
+
+struct Dims {
+  int B, N, F, T, h, dk, dv, D, K, C;
+  int64_t FT, BFT, BN, NN, HQ, HV, QW, KD, KC, CT, KCT, S;
+  int Tg[3], Lp[3], ks[3];
+  bool first;
+};
+
+Dims mkdims(const dstagnn_block_dims& d) {
+  Dims m;
+  m.B = d.B; m.N = d.N; m.F = d.F; m.T = d.T; m.h = d.n_heads; m.dk = d.d_k; m.dv = d.d_v;
+  m.D = d.d_model; m.K = d.K; m.C = d.C;
+  m.FT = (int64_t)m.F * m.T; m.BFT = (int64_t)m.B * m.FT; m.BN = (int64_t)m.B * m.N; m.NN = (int64_t)m.N * m.N;
+  m.HQ = (int64_t)m.h * m.dk; m.HV = (int64_t)m.h * m.dv; m.QW = 2 * m.HQ + m.HV; m.KD = (int64_t)m.K * m.dk;
+  m.KC = (int64_t)m.K * m.C; m.CT = (int64_t)m.C * m.T; m.KCT = m.KC * m.T; m.S = 3 * (int64_t)m.T - 12;
+  for (int g = 0; g < 3; ++g) { m.ks[g] = 3 + 2 * g; m.Tg[g] = m.T - m.ks[g] + 1; m.Lp[g] = m.T + m.ks[g] - 1; }
+  m.first = (m.F == 1);
+  return m;
+}
+
+struct SaveBufs {
+  float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
+  float* conv[3];
+  float *G, *tco, *r, *mu_c, *rs_c, *u_et, *mu_et, *rs_et;
+};
+
+SaveBufs plan_save(const Dims& m, Arena& a) {
+  SaveBufs s;
+  s.E = a.take(m.BFT * m.N);
+  s.qkv = a.take(m.BFT * m.QW);
+  s.att = a.take(m.BFT * m.h * m.T);
+  s.ctx = a.take(m.BFT * m.HV);
+  s.u_tat = a.take(m.BFT * m.N);
+  s.mu_tat = a.take(m.BFT);
+  s.rs_tat = a.take(m.BFT);
+  s.O = a.take(m.BFT * m.N);
+  s.u_s = a.take(m.BN * m.D);
+  s.mu_s = a.take(m.BN);
+  s.rs_s = a.take(m.BN);
+  s.Zd = a.take(m.BN * m.D);
+  s.qk = a.take(m.BN * 2 * m.KD);
+  s.P = a.take((int64_t)m.B * m.K * m.NN);
+  s.W = a.take((int64_t)m.B * m.K * m.NN);
+  s.xth = a.take(m.BN * m.KCT);
+  s.X = a.take(m.BN * m.CT);
+  for (int g = 0; g < 3; ++g) s.conv[g] = a.take(m.BN * 2 * m.C * std::max(m.Tg[g], 0));
+  s.G = a.take(m.BN * m.C * m.S);
+  s.tco = a.take(m.BN * m.CT);
+  s.r = a.take(m.BN * m.CT);
+  s.mu_c = a.take(m.BN * m.T);
+  s.rs_c = a.take(m.BN * m.T);
+  if (m.first) {
+    s.u_et = a.take((int64_t)m.B * m.T * m.N);
+    s.mu_et = a.take((int64_t)m.B * m.T);
+    s.rs_et = a.take((int64_t)m.B * m.T);
+  } else {
+    s.u_et = s.mu_et = s.rs_et = nullptr;
+  }
+  return s;
+}
+
+constexpr size_t kGemmWs = size_t(8) << 20;   // floats (32 MB) for split-K partial slabs
+constexpr size_t kPart = size_t(2) << 20;      // floats (8 MB) for column-sum partials
+
+struct Scratch {
+  float *Wp, *thcat, *tc, *gemm_ws, *part;
+  // bwd
+  float *dtc, *dX, *gpre, *gcon, *bcon, *dG, *dconv[3], *dW, *dxth, *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dctx,
+      *dqkv, *dscore, *du_et;
+};
+
+Scratch plan_scratch(const Dims& m, Arena& a) {
+  Scratch s;
+  s.gemm_ws = a.take(kGemmWs);
+  s.part = a.take(kPart);
+  s.Wp = a.take((int64_t)m.D * m.FT);
+  s.thcat = a.take((int64_t)m.F * m.KC);
+  s.tc = a.take(m.BN * m.CT);
+  s.dtc = a.take(m.BN * m.CT);
+  s.dX = a.take(m.BN * m.CT);
+  s.gpre = a.take(m.BN * m.CT);
+  // LN / tail gamma & beta contributions: largest of (B*N*C*T, B*N*D, B*F*T*N)
+  int64_t con = std::max(m.BN * m.CT, std::max(m.BN * m.D, m.BFT * m.N));
+  s.gcon = a.take(con);
+  s.bcon = a.take(con);
+  s.dG = a.take(m.BN * m.C * m.S);
+  for (int g = 0; g < 3; ++g) s.dconv[g] = a.take(m.BN * 2 * m.C * m.Lp[g]);
+  s.dW = a.take((int64_t)m.B * m.K * m.NN);
+  s.dxth = a.take(m.BN * m.KCT);
+  s.dthcat = a.take((int64_t)m.F * m.KC);
+  s.dqk = a.take(m.BN * 2 * m.KD);
+  s.dZd = a.take(m.BN * m.D);
+  s.dY = a.take(m.BN * m.D);
+  s.dWp = a.take((int64_t)m.D * m.FT);
+  s.dO = a.take(m.BFT * m.N);
+  s.dU = a.take(m.BFT * m.N);
+  s.dctx = a.take(m.BFT * m.HV);
+  s.dqkv = a.take(m.BFT * m.QW);
+  s.dscore = a.take(m.BFT * m.h * m.T);
+  s.du_et = m.first ? a.take((int64_t)m.B * m.T * m.N) : nullptr;
+  return s;
+}
+
+void plan_sizes(const Dims& m, size_t* save, size_t* scratch) {
+  Arena a(nullptr);
+  plan_save(m, a);
+  *save = a.off + 256;
+  Arena b(nullptr);
+  plan_scratch(m, b);
+  *scratch = b.off + 256;
+}
+
+int check_dims(const dstagnn_block_dims* d) {
+  if (!d) { set_last_error("null dims"); return DSTAGNN_E_ARG; }
+  if (d->B <= 0 || d->N <= 0 || d->F <= 0 || d->T <= 0 || d->n_heads <= 0 || d->d_k <= 0 || d->d_v <= 0 ||
+      d->d_model <= 0 || d->K <= 0 || d->C <= 0) {
+    set_last_error("non-positive dimension");
+    return DSTAGNN_E_SHAPE;
+  }
+  if (d->K > DSTAGNN_MAX_K) { set_last_error("K > DSTAGNN_MAX_K"); return DSTAGNN_E_SHAPE; }
+  if (d->T < 7) { set_last_error("T must be >= 7 (GTU kernel 7, fcmy 3T-12)"); return DSTAGNN_E_SHAPE; }
+  if (d->F != 1 && d->F != d->C) {
+    // the reference fails at model/DSTAGNN_my.py:252 (x.permute + time_conv_output)
+    set_last_error("The size of tensor a (" + std::to_string(d->F) + ") must match the size of tensor b (" +
+                   std::to_string(d->C) + ") at non-singleton dimension 1");
+    return DSTAGNN_E_SHAPE;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------
+// Chebyshev graph convolution with spatial attention (cheb_conv_withSAt :117-133)
+// ------------------------------------------------------------------------------
+struct ChebIO {
+  int B, N, F, T, K, C;
+  const float* x;
+  const float* S;          // scores (B,K,N,N) (may alias P)
+  const float* const* mask;
+  const float* cheb;
+  const float* apa;
+  const float* thcat;      // (F, K*C)
+  float *P, *W, *xth, *X;
+};
+
+int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
+  const int64_t NN = (int64_t)c.N * c.N, KC = (int64_t)c.K * c.C, T = c.T, CT = (int64_t)c.C * T,
+                KCT = KC * T, FT = (int64_t)c.F * T;
+  ChebSm sm;
+  sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.S = c.S; sm.apa = c.apa; sm.cheb = c.cheb; sm.P = c.P; sm.W = c.W;
+  for (int k = 0; k < c.K; ++k) sm.mask[k] = c.mask[k];
+  DS_TRY(op_cheb_softmax_fwd(sm, st));
+  // xth[(b,i,t),(k,c)] = sum_f x[b,i,f,t] Theta_k[f,c]
+  {
+    Gemm g;
+    g.M = c.B * c.N * c.T; g.N = (int)KC; g.K = c.F;
+    g.A = c.x; g.am = idx2(T, 1, FT); g.ak = idx1(T);
+    g.B = c.thcat; g.bk = idx1(KC); g.bn = idx1(1);
+    g.C = c.xth; g.cm = idx2(T, 1, KCT); g.cn = idx1(T);
+    DS_TRY(run_gemm(g, ws, kGemmWs, st));
+  }
+  // X[b,j,(c,t)] = relu( sum_{k,i} W[b,k,i,j] xth[b,i,k,(c,t)] )
+  {
+    Gemm g;
+    g.M = c.N; g.N = (int)CT; g.K = c.K * c.N; g.batch = c.B;
+    g.A = c.W; g.am = idx1(1); g.ak = idx2(c.N, c.N, NN); g.az = idx1(c.K * NN);
+    g.B = c.xth; g.bk = idx2(c.N, KCT, CT); g.bn = idx1(1); g.bz = idx1(c.N * KCT);
+    g.C = c.X; g.cm = idx1(CT); g.cn = idx1(1); g.cz = idx1(c.N * CT);
+    g.relu = 1;
+    DS_TRY(run_gemm(g, ws, kGemmWs, st));
+  }
+  return 0;
+}
+
+struct ChebGradIO {
+  int B, N, F, T, K, C;
+  const float* x;
+  const float* thcat;
+  const float* cheb;
+  const float* apa;
+  const float *P, *W, *xth;
+  const float* gpre;       // d(pre-ReLU out) (B,N,C,T)
+  float* dx;               // accumulated (beta = dx_beta)
+  float dx_beta;
+  float* dz;               // (B,K,N,N) d scores
+  float* dthcat;           // (F, K*C)
+  float* const* dmask;     // K pointers (N,N)
+  float* dxth;             // scratch (B,N,K,C,T)
+};
+
+int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
+  const int64_t NN = (int64_t)c.N * c.N, KC = (int64_t)c.K * c.C, T = c.T, CT = (int64_t)c.C * T,
+                KCT = KC * T, FT = (int64_t)c.F * T;
+  // dW[b,k,i,j] = sum_ct xth[b,i,k,ct] g[b,j,ct]
+  {
+    Gemm g;
+    g.M = c.N; g.N = c.N; g.K = (int)CT; g.batch = c.B * c.K;
+    g.A = c.xth; g.am = idx1(KCT); g.ak = idx1(1); g.az = idx2(c.K, CT, c.N * KCT);
+    g.B = c.gpre; g.bk = idx1(1); g.bn = idx1(CT); g.bz = idx2(c.K, 0, c.N * CT);
+    g.C = c.dz; g.cm = idx1(c.N); g.cn = idx1(1); g.cz = idx1(NN);
+    DS_TRY(run_gemm(g, ws, kGemmWs, st));
+  }
+  // dxth[b,i,k,ct] = sum_j W[b,k,i,j] g[b,j,ct]
+  {
+    Gemm g;
+    g.M = c.N; g.N = (int)CT; g.K = c.N; g.batch = c.B * c.K;
+    g.A = c.W; g.am = idx1(c.N); g.ak = idx1(1); g.az = idx1(NN);
+    g.B = c.gpre; g.bk = idx1(CT); g.bn = idx1(1); g.bz = idx2(c.K, 0, c.N * CT);
+    g.C = c.dxth; g.cm = idx1(KCT); g.cn = idx1(1); g.cz = idx2(c.K, CT, c.N * KCT);
+    DS_TRY(run_gemm(g, ws, kGemmWs, st));
+  }
+  // softmax backward in place: dz = P * (T o dW - colsum(P T o dW))
+  ChebSm sm;
+  sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.apa = c.apa; sm.cheb = c.cheb; sm.P = const_cast<float*>(c.P);
+  sm.dW = c.dz; sm.dz = c.dz;
+  for (int k = 0; k < c.K; ++k) sm.dmask[k] = c.dmask[k];
+  DS_TRY(op_cheb_softmax_bwd(sm, st));
+  DS_TRY(op_cheb_mask_grad(sm, st));
+  // dTheta_cat[f,(k,c)] = sum_{b,i,t} x[b,i,f,t] dxth[b,i,k,c,t]
+  {
+    Gemm g;
+    g.M = c.F; g.N = (int)KC; g.K = c.B * c.N * c.T;
+    g.A = c.x; g.am = idx1(T); g.ak = idx2(T, 1, FT);
+    g.B = c.dxth; g.bk = idx2(T, 1, KCT); g.bn = idx1(T);
+    g.C = c.dthcat; g.cm = idx1(KC); g.cn = idx1(1);
+    DS_TRY(run_gemm(g, ws, kGemmWs, st));
+  }
+  // dx[b,i,f,t] += sum_{k,c} Theta_k[f,c] dxth[b,i,k,c,t]
+  {
+    Gemm g;
+    g.M = c.B * c.N * c.T; g.N = c.F; g.K = (int)KC;
+    g.A = c.dxth; g.am = idx2(T, 1, KCT); g.ak = idx1(T);
+    g.B = c.thcat; g.bk = idx1(1); g.bn = idx1(KC);
+    g.C = c.dx; g.cm = idx2(T, 1, FT); g.cn = idx1(T);
+    g.beta = c.dx_beta;
+    DS_TRY(run_gemm(g, ws, kGemmWs, st));
+  }
+  return 0;
+}
+
+int pack_theta(const float* const* theta, int K, int F, int C, float* thcat, hipStream_t st) {
+  for (int k = 0; k < K; ++k) {
+    hipError_t e = hipMemcpy2DAsync(thcat + (int64_t)k * C, sizeof(float) * K * C, theta[k], sizeof(float) * C,
+                                    sizeof(float) * C, F, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) { set_last_error(std::string("pack_theta: ") + hipGetErrorString(e)); return (int)e; }
+  }
+  return 0;
+}
+int unpack_theta(const float* thcat, int K, int F, int C, float* const* dtheta, hipStream_t st) {
+  for (int k = 0; k < K; ++k) {
+    if (!dtheta[k]) continue;
+    hipError_t e = hipMemcpy2DAsync(dtheta[k], sizeof(float) * C, thcat + (int64_t)k * C, sizeof(float) * K * C,
+                                    sizeof(float) * C, F, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) { set_last_error(std::string("unpack_theta: ") + hipGetErrorString(e)); return (int)e; }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------
+struct Fwd {
+  const Dims& m;
+  const dstagnn_block_dims& d;
+  const dstagnn_block_params& p;
+  const dstagnn_graph& gr;
+  const float* x;
+  const float* res;
+  float* out;
+  float* re_at;
+  SaveBufs& s;
+  Scratch& w;
+  hipStream_t st;
+
+  int stage_tat() {
+    const int64_t N = m.N;
+    // E: TAt input (B,F,T,N)
+    if (m.first) {
+      LnFwd a;
+      a.R = m.B * m.T; a.L = m.N;
+      a.src[0].p = x; a.src[0].row = idx2(m.T, 1, (int64_t)m.N * m.T); a.src[0].es = m.T;
+      a.src[1].p = p.embT_pos; a.src[1].row = idx2(m.T, m.N, 0); a.src[1].es = 1;
+      a.nsrc = 2;
+      a.g = p.embT_g; a.b = p.embT_b;
+      a.y = s.E; a.yrow = idx1(N); a.yes = 1;
+      a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et;
+      DS_TRY(op_ln_fwd(a, st));
+    } else {
+      DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, N * m.FT, m.FT * N, 0.f, st));
+    }
+    // Q | K | V projections  (MultiHeadAttention :92-94)
+    const float* wts[3] = {p.tat_wq, p.tat_wk, p.tat_wv};
+    const int64_t cols[3] = {m.HQ, m.HQ, m.HV};
+    const int64_t offs[3] = {0, m.HQ, 2 * m.HQ};
+    for (int q = 0; q < 3; ++q) {
+      Gemm g;
+      g.M = (int)m.BFT; g.N = (int)cols[q]; g.K = m.N;
+      g.A = s.E; g.am = idx1(N); g.ak = idx1(1);
+      g.B = wts[q]; g.bk = idx1(1); g.bn = idx1(N);
+      g.C = s.qkv; g.c_off = offs[q]; g.cm = idx1(m.QW); g.cn = idx1(1);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    DS_TRY(op_tat_fwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, res, d.res_mode, re_at, s.att, s.ctx, st));
+    // fc (:99)
+    {
+      Gemm g;
+      g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.HV;
+      g.A = s.ctx; g.am = idx1(m.HV); g.ak = idx1(1);
+      g.B = p.tat_fc; g.bk = idx1(1); g.bn = idx1(m.HV);
+      g.C = s.u_tat; g.cm = idx1(N); g.cn = idx1(1);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    // LN_N(fc + E) (:100)
+    {
+      LnFwd a;
+      a.R = (int)m.BFT; a.L = m.N;
+      a.src[0].p = s.u_tat; a.src[0].row = idx1(N);
+      a.src[1].p = s.E; a.src[1].row = idx1(N);
+      a.nsrc = 2;
+      a.g = p.tat_ln_g; a.b = p.tat_ln_b;
+      a.y = s.O; a.yrow = idx1(N);
+      a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat;
+      DS_TRY(op_ln_fwd(a, st));
+    }
+    return 0;
+  }
+
+  Gemm preconv_gemm() {
+    Gemm g;  // u_s[(b,n), d] = bias[d] + sum_{(f,t)} O[b,f,t,n] Wp[d,(f,t)]
+    g.M = (int)m.BN; g.N = m.D; g.K = (int)m.FT;
+    g.A = s.O; g.am = idx2(m.N, 1, m.FT * m.N); g.ak = idx1(m.N);
+    g.B = w.Wp; g.bk = idx1(1); g.bn = idx1(m.FT);
+    g.C = s.u_s; g.cm = idx1(m.D); g.cn = idx1(1);
+    g.bias = p.pre_conv_b;
+    g.hot = 1;
+    return g;
+  }
+
+  int stage_preconv() {
+    // Wp[d][f][t] = pre_conv.weight[d][t][0][f]
+    DS_TRY(op_transpose(p.pre_conv_w, w.Wp, m.T, m.F, m.D, m.FT, m.FT, 0.f, st));
+    return run_gemm(preconv_gemm(), w.gemm_ws, kGemmWs, st);
+  }
+
+  int stage_sat() {
+    {  // EmbedS LN_D(y + pos) + dropout (:233-234)
+      LnFwd a;
+      a.R = (int)m.BN; a.L = m.D;
+      a.src[0].p = s.u_s; a.src[0].row = idx1(m.D);
+      a.src[1].p = p.embS_pos; a.src[1].row = idx2(m.N, m.D, 0);
+      a.nsrc = 2;
+      a.g = p.embS_g; a.b = p.embS_b;
+      a.y = s.Zd; a.yrow = idx1(m.D);
+      a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s;
+      if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
+      DS_TRY(op_ln_fwd(a, st));
+    }
+    const float* wts[2] = {p.sat_wq, p.sat_wk};
+    for (int q = 0; q < 2; ++q) {  // SMultiHeadAttention W_Q / W_K (:62-63)
+      Gemm g;
+      g.M = (int)m.BN; g.N = (int)m.KD; g.K = m.D;
+      g.A = s.Zd; g.am = idx1(m.D); g.ak = idx1(1);
+      g.B = wts[q]; g.bk = idx1(1); g.bn = idx1(m.D);
+      g.C = s.qk; g.c_off = q * m.KD; g.cm = idx1(2 * m.KD); g.cn = idx1(1);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    {  // S'[b,k] = Q'_k K'_k^T / sqrt(dk)  (:19) -> written into P (softmaxed in place)
+      Gemm g;
+      g.M = m.N; g.N = m.N; g.K = m.dk; g.batch = m.B * m.K;
+      g.A = s.qk; g.am = idx1(2 * m.KD); g.ak = idx1(1); g.az = idx2(m.K, m.dk, m.N * 2 * m.KD);
+      g.B = s.qk; g.b_off = m.KD; g.bk = idx1(1); g.bn = idx1(2 * m.KD); g.bz = idx2(m.K, m.dk, m.N * 2 * m.KD);
+      g.C = s.P; g.cm = idx1(m.N); g.cn = idx1(1); g.cz = idx1(m.NN);
+      g.alpha = 1.f / sqrtf((float)m.dk);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    return 0;
+  }
+
+  int stage_cheb() {
+    DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, w.thcat, st));
+    ChebIO c;
+    c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
+    c.x = x; c.S = s.P; c.mask = p.mask; c.cheb = gr.cheb; c.apa = gr.adj_pa; c.thcat = w.thcat;
+    c.P = s.P; c.W = s.W; c.xth = s.xth; c.X = s.X;
+    return cheb_forward(c, w.gemm_ws, st);
+  }
+
+  int stage_tail() {
+    for (int q = 0; q < 3; ++q) {  // GTU convs (:190) as implicit-im2col GEMMs
+      const int ks = m.ks[q], Tg = m.Tg[q];
+      Gemm g;
+      g.M = (int)(m.BN * Tg); g.N = 2 * m.C; g.K = m.C * ks;
+      g.A = s.X; g.am = idx2(Tg, 1, m.CT); g.ak = idx2(ks, 1, m.T);
+      g.B = p.gtu_w[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);
+      g.C = s.conv[q]; g.cm = idx2(Tg, 1, 2 * m.C * Tg); g.cn = idx1(Tg);
+      g.bias = p.gtu_b[q];
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    GateArgs ga;
+    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
+    for (int q = 0; q < 3; ++q) ga.conv[q] = s.conv[q];
+    ga.G = s.G;
+    DS_TRY(op_gate_fwd(ga, st));
+    {  // fcmy (:243)
+      Gemm g;
+      g.M = (int)(m.BN * m.C); g.N = m.T; g.K = (int)m.S;
+      g.A = s.G; g.am = idx1(m.S); g.ak = idx1(1);
+      g.B = p.fcmy_w; g.bk = idx1(1); g.bn = idx1(m.S);
+      g.C = w.tc; g.cm = idx1(m.T); g.cn = idx1(1);
+      g.bias = p.fcmy_b;
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    TailArgs t;
+    t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
+    t.X = s.X; t.tc = w.tc; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
+    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
+    t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c; t.out = out;
+    return op_tail_fwd(t, st);
+  }
+
+  int run() {
+    DS_TRY(stage_tat());
+    DS_TRY(stage_preconv());
+    DS_TRY(stage_sat());
+    DS_TRY(stage_cheb());
+    DS_TRY(stage_tail());
+    return 0;
+  }
+};
+
+// ------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------
+struct Bwd {
+  const Dims& m;
+  const dstagnn_block_dims& d;
+  const dstagnn_block_params& p;
+  const dstagnn_graph& gr;
+  const dstagnn_block_grads& gd;
+  const float* x;
+  const float* dout;
+  const float* dre;
+  float* dx;
+  float* dres;
+  SaveBufs& s;
+  Scratch& w;
+  hipStream_t st;
+
+  int colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out) {
+    if (!out) return 0;
+    return op_colsum(in, in2, A, O, I, out, 1, 0.f, w.part, kPart, st);
+  }
+  int gemm(const Gemm& g) { return run_gemm(g, w.gemm_ws, kGemmWs, st); }
+
+  int stage_tail() {
+    TailArgs t;
+    t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
+    t.X = s.X; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
+    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
+    t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c;
+    t.dout = dout; t.gcontrib = w.gcon; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
+    t.rcontrib = w.bcon; t.dres = w.gpre;  // gpre reused as scratch until the cheb stage
+    DS_TRY(op_tail_bwd(t, st));
+    DS_TRY(colsum(w.gcon, nullptr, m.BN, m.C, m.T, gd.ln_g));
+    DS_TRY(colsum(dout, nullptr, m.BN, m.C, m.T, gd.ln_b));
+    if (m.first) {
+      DS_TRY(colsum(w.bcon, nullptr, m.BN, m.C, m.T, gd.res_w));
+      DS_TRY(colsum(w.gpre, nullptr, m.BN, m.C, m.T, gd.res_b));
+    }
+    // fcmy backward
+    {
+      Gemm g;  // dG = dtc @ W
+      g.M = (int)(m.BN * m.C); g.N = (int)m.S; g.K = m.T;
+      g.A = w.dtc; g.am = idx1(m.T); g.ak = idx1(1);
+      g.B = p.fcmy_w; g.bk = idx1(m.S); g.bn = idx1(1);
+      g.C = w.dG; g.cm = idx1(m.S); g.cn = idx1(1);
+      DS_TRY(gemm(g));
+    }
+    if (gd.fcmy_w) {
+      Gemm g;  // dW[t,s] = sum_r dtc[r,t] G[r,s]
+      g.M = m.T; g.N = (int)m.S; g.K = (int)(m.BN * m.C);
+      g.A = w.dtc; g.am = idx1(1); g.ak = idx1(m.T);
+      g.B = s.G; g.bk = idx1(m.S); g.bn = idx1(1);
+      g.C = gd.fcmy_w; g.cm = idx1(m.S); g.cn = idx1(1);
+      DS_TRY(gemm(g));
+    }
+    DS_TRY(colsum(w.dtc, nullptr, m.BN * m.C, m.T, 1, gd.fcmy_b));
+    // gates
+    GateArgs ga;
+    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
+    for (int q = 0; q < 3; ++q) { ga.conv[q] = s.conv[q]; ga.dconv_pad[q] = w.dconv[q]; }
+    ga.dG = w.dG;
+    DS_TRY(op_gate_bwd(ga, st));
+    for (int q = 0; q < 3; ++q) {
+      const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
+      const int64_t cs = 2 * (int64_t)m.C * Lp;  // per-(b,n) stride of the padded dconv
+      if (gd.gtu_w[q]) {
+        Gemm g;  // dW[o,(c,tau)] = sum_{(bn,t')} dconv[bn,o,t'] X[bn,c,t'+tau]
+        g.M = 2 * m.C; g.N = m.C * ks; g.K = (int)(m.BN * Tg);
+        g.A = w.dconv[q]; g.a_off = ks - 1; g.am = idx1(Lp); g.ak = idx2(Tg, 1, cs);
+        g.B = s.X; g.bk = idx2(Tg, 1, m.CT); g.bn = idx2(ks, 1, m.T);
+        g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx1(1);
+        DS_TRY(gemm(g));
+      }
+      DS_TRY(colsum(w.dconv[q], nullptr, m.BN, 2 * m.C, Lp, gd.gtu_b[q]));
+      {
+        Gemm g;  // dX[bn,c,t] += sum_{o,tau} W[o,c,tau] dconv[bn,o,t-tau]
+        g.M = (int)(m.BN * m.T); g.N = m.C; g.K = 2 * m.C * ks;
+        g.A = w.dconv[q]; g.a_off = ks - 1; g.am = idx2(m.T, 1, cs); g.ak = idx2(ks, -1, Lp);
+        g.B = p.gtu_w[q]; g.bk = idx2(ks, 1, (int64_t)m.C * ks); g.bn = idx1(ks);
+        g.C = w.dX; g.cm = idx2(m.T, 1, m.CT); g.cn = idx1(m.T);
+        g.beta = 1.f;
+        DS_TRY(gemm(g));
+      }
+    }
+    return 0;
+  }
+
+  int stage_cheb() {
+    DS_TRY(op_relu_mask(w.dX, s.X, w.gpre, m.BN * m.CT, st));
+    DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, w.thcat, st));
+    ChebGradIO c;
+    c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
+    c.x = x; c.thcat = w.thcat; c.cheb = gr.cheb; c.apa = gr.adj_pa; c.P = s.P; c.W = s.W; c.xth = s.xth;
+    c.gpre = w.gpre; c.dx = dx; c.dx_beta = 1.f; c.dz = w.dW; c.dthcat = w.dthcat; c.dmask = gd.mask;
+    c.dxth = w.dxth;
+    DS_TRY(cheb_backward(c, w.gemm_ws, st));
+    DS_TRY(unpack_theta(w.dthcat, m.K, m.F, m.C, gd.theta, st));
+    return 0;
+  }
+
+  int stage_sat() {
+    const float sc = 1.f / sqrtf((float)m.dk);
+    const int64_t ld = 2 * m.KD;
+    {  // dQ'[b,i,k,:] = sum_j dz[b,k,i,j] K'[b,j,k,:] / sqrt(dk)
+      Gemm g;
+      g.M = m.N; g.N = m.dk; g.K = m.N; g.batch = m.B * m.K;
+      g.A = w.dW; g.am = idx1(m.N); g.ak = idx1(1); g.az = idx1(m.NN);
+      g.B = s.qk; g.b_off = m.KD; g.bk = idx1(ld); g.bn = idx1(1); g.bz = idx2(m.K, m.dk, m.N * ld);
+      g.C = w.dqk; g.cm = idx1(ld); g.cn = idx1(1); g.cz = idx2(m.K, m.dk, m.N * ld);
+      g.alpha = sc;
+      DS_TRY(gemm(g));
+    }
+    {  // dK'[b,j,k,:] = sum_i dz[b,k,i,j] Q'[b,i,k,:] / sqrt(dk)
+      Gemm g;
+      g.M = m.N; g.N = m.dk; g.K = m.N; g.batch = m.B * m.K;
+      g.A = w.dW; g.am = idx1(1); g.ak = idx1(m.N); g.az = idx1(m.NN);
+      g.B = s.qk; g.bk = idx1(ld); g.bn = idx1(1); g.bz = idx2(m.K, m.dk, m.N * ld);
+      g.C = w.dqk; g.c_off = m.KD; g.cm = idx1(ld); g.cn = idx1(1); g.cz = idx2(m.K, m.dk, m.N * ld);
+      g.alpha = sc;
+      DS_TRY(gemm(g));
+    }
+    float* wg[2] = {gd.sat_wq, gd.sat_wk};
+    const float* wts[2] = {p.sat_wq, p.sat_wk};
+    for (int q = 0; q < 2; ++q) {
+      if (wg[q]) {  // dW'[n,d] = sum_r dqk[r, q*KD + n] Zd[r,d]
+        Gemm g;
+        g.M = (int)m.KD; g.N = m.D; g.K = (int)m.BN;
+        g.A = w.dqk; g.a_off = q * m.KD; g.am = idx1(1); g.ak = idx1(ld);
+        g.B = s.Zd; g.bk = idx1(m.D); g.bn = idx1(1);
+        g.C = wg[q]; g.cm = idx1(m.D); g.cn = idx1(1);
+        DS_TRY(gemm(g));
+      }
+      Gemm g;  // dZd += dqk[:, q] W'
+      g.M = (int)m.BN; g.N = m.D; g.K = (int)m.KD;
+      g.A = w.dqk; g.a_off = q * m.KD; g.am = idx1(ld); g.ak = idx1(1);
+      g.B = wts[q]; g.bk = idx1(m.D); g.bn = idx1(1);
+      g.C = w.dZd; g.cm = idx1(m.D); g.cn = idx1(1);
+      g.beta = q ? 1.f : 0.f;
+      DS_TRY(gemm(g));
+    }
+    {  // EmbedS LN_D backward (dropout mask re-derived from the seed)
+      LnBwd a;
+      a.R = (int)m.BN; a.L = m.D;
+      a.dy = w.dZd; a.dyrow = idx1(m.D);
+      a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s; a.g = p.embS_g;
+      if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
+      a.dx = w.dY; a.dxrow = idx1(m.D);
+      a.gcontrib = w.gcon; a.bcontrib = w.bcon;
+      DS_TRY(op_ln_bwd(a, st));
+      DS_TRY(colsum(w.gcon, nullptr, m.BN, m.D, 1, gd.embS_g));
+      DS_TRY(colsum(w.bcon, nullptr, m.BN, m.D, 1, gd.embS_b));
+      if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, st));
+    }
+    return 0;
+  }
+
+  int stage_preconv() {
+    DS_TRY(colsum(w.dY, nullptr, m.BN, m.D, 1, gd.pre_conv_b));
+    if (gd.pre_conv_w) {
+      Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
+      g.M = m.D; g.N = (int)m.FT; g.K = (int)m.BN;
+      g.A = w.dY; g.am = idx1(1); g.ak = idx1(m.D);
+      g.B = s.O; g.bk = idx2(m.N, 1, m.FT * m.N); g.bn = idx1(m.N);
+      g.C = w.dWp; g.cm = idx1(m.FT); g.cn = idx1(1);
+      DS_TRY(gemm(g));
+      // pre_conv.weight[d][t][0][f] = dWp[d][f][t]
+      DS_TRY(op_transpose(w.dWp, gd.pre_conv_w, m.F, m.T, m.D, m.FT, m.FT, 0.f, st));
+    }
+    DS_TRY(op_transpose(p.pre_conv_w, w.Wp, m.T, m.F, m.D, m.FT, m.FT, 0.f, st));
+    Gemm g;  // dO[b,(f,t),n] = sum_d Wp[d,(f,t)] dY[(b,n),d]
+    g.M = (int)m.FT; g.N = (int)m.BN; g.K = m.D;
+    g.A = w.Wp; g.am = idx1(1); g.ak = idx1(m.FT);
+    g.B = w.dY; g.bk = idx1(1); g.bn = idx1(m.D);
+    g.C = w.dO; g.cm = idx1(m.N); g.cn = idx2(m.N, 1, m.FT * m.N);
+    return gemm(g);
+  }
+
+  int stage_tat() {
+    const int64_t N = m.N;
+    {  // LN_N backward (:100); dU = d(fc + E)
+      LnBwd a;
+      a.R = (int)m.BFT; a.L = m.N;
+      a.dy = w.dO; a.dyrow = idx1(N);
+      a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat; a.g = p.tat_ln_g;
+      a.dx = w.dU; a.dxrow = idx1(N);
+      a.gcontrib = w.gcon; a.bcontrib = nullptr;
+      DS_TRY(op_ln_bwd(a, st));
+      DS_TRY(colsum(w.gcon, nullptr, m.BFT, m.N, 1, gd.tat_ln_g));
+      DS_TRY(colsum(w.dO, nullptr, m.BFT, m.N, 1, gd.tat_ln_b));
+    }
+    {  // dctx = dU Wfc
+      Gemm g;
+      g.M = (int)m.BFT; g.N = (int)m.HV; g.K = m.N;
+      g.A = w.dU; g.am = idx1(N); g.ak = idx1(1);
+      g.B = p.tat_fc; g.bk = idx1(m.HV); g.bn = idx1(1);
+      g.C = w.dctx; g.cm = idx1(m.HV); g.cn = idx1(1);
+      DS_TRY(gemm(g));
+    }
+    if (gd.tat_fc) {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
+      Gemm g;
+      g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
+      g.A = w.dU; g.am = idx1(1); g.ak = idx1(N);
+      g.B = s.ctx; g.bk = idx1(m.HV); g.bn = idx1(1);
+      g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
+      DS_TRY(gemm(g));
+    }
+    float* dsc = (d.res_mode == DSTAGNN_RES_FULL && dres) ? dres : w.dscore;
+    DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, st));
+    if (d.res_mode == DSTAGNN_RES_BCAST && dres)
+      DS_TRY(op_sum_middle(w.dscore, m.B, m.F, (int64_t)m.h * m.T * m.T, dres, 0.f, st));
+    // dE = dU + sum_q dqkv_q W_q ;  dW_q = dqkv_q^T E
+    const float* wts[3] = {p.tat_wq, p.tat_wk, p.tat_wv};
+    float* wg[3] = {gd.tat_wq, gd.tat_wk, gd.tat_wv};
+    const int64_t cols[3] = {m.HQ, m.HQ, m.HV};
+    const int64_t offs[3] = {0, m.HQ, 2 * m.HQ};
+    for (int q = 0; q < 3; ++q) {
+      if (wg[q]) {
+        Gemm g;
+        g.M = (int)cols[q]; g.N = m.N; g.K = (int)m.BFT;
+        g.A = w.dqkv; g.a_off = offs[q]; g.am = idx1(1); g.ak = idx1(m.QW);
+        g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
+        g.C = wg[q]; g.cm = idx1(N); g.cn = idx1(1);
+        DS_TRY(gemm(g));
+      }
+      Gemm g;
+      g.M = (int)m.BFT; g.N = m.N; g.K = (int)cols[q];
+      g.A = w.dqkv; g.a_off = offs[q]; g.am = idx1(m.QW); g.ak = idx1(1);
+      g.B = wts[q]; g.bk = idx1(N); g.bn = idx1(1);
+      g.C = w.dU; g.cm = idx1(N); g.cn = idx1(1);
+      g.beta = 1.f;
+      DS_TRY(gemm(g));
+    }
+    // dE -> dx
+    if (m.first) {
+      LnBwd a;
+      a.R = m.B * m.T; a.L = m.N;
+      a.dy = w.dU; a.dyrow = idx1(N);
+      a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et; a.g = p.embT_g;
+      a.dx = w.du_et; a.dxrow = idx1(N);
+      a.gcontrib = w.gcon; a.bcontrib = nullptr;
+      DS_TRY(op_ln_bwd(a, st));
+      DS_TRY(colsum(w.gcon, nullptr, (int64_t)m.B * m.T, m.N, 1, gd.embT_g));
+      DS_TRY(colsum(w.dU, nullptr, (int64_t)m.B * m.T, m.N, 1, gd.embT_b));
+      if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, st));
+      DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
+    } else {
+      DS_TRY(op_transpose(w.dU, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
+    }
+    return 0;
+  }
+
+  int run() {
+    DS_TRY(stage_tail());
+    DS_TRY(stage_cheb());
+    DS_TRY(stage_sat());
+    DS_TRY(stage_preconv());
+    DS_TRY(stage_tat());
+    return 0;
+  }
+};
+
+int check_space(const Dims& m, size_t save_bytes, size_t scratch_bytes) {
+  size_t sv, sc;
+  plan_sizes(m, &sv, &sc);
+  if (save_bytes < sv || scratch_bytes < sc) {
+    set_last_error("save/scratch smaller than dstagnn_block_sizes()");
+    return DSTAGNN_E_SPACE;
+  }
+  return 0;
+}
+
+void* align256(void* p) { return (void*)(((uintptr_t)p + 255) & ~uintptr_t(255)); }
+
+}  // namespace
+
+// ==================================================================================
+// C-ABI
+// ==================================================================================
+extern "C" {
+
+const char* dstagnn_last_error(void) { return g_last_error.c_str(); }
+int dstagnn_version(void) { return 1; }
+
+int dstagnn_block_sizes(const dstagnn_block_dims* d, size_t* save_bytes, size_t* scratch_bytes) {
+  DS_TRY(check_dims(d));
+  if (!save_bytes || !scratch_bytes) return DSTAGNN_E_ARG;
+  plan_sizes(mkdims(*d), save_bytes, scratch_bytes);
+  return 0;
+}
+
+int dstagnn_block_forward(const dstagnn_block_dims* d, const dstagnn_block_params* p, const dstagnn_graph* g,
+                          const float* x, const float* res_att, float* out, float* re_at, void* save,
+                          size_t save_bytes, void* scratch, size_t scratch_bytes, dstagnn_stream_t stream) {
+  DS_TRY(check_dims(d));
+  if (!p || !g || !x || !out || !re_at || !save || !scratch) { set_last_error("null argument"); return DSTAGNN_E_ARG; }
+  if (d->res_mode != DSTAGNN_RES_NONE && !res_att) { set_last_error("res_att missing"); return DSTAGNN_E_ARG; }
+  Dims m = mkdims(*d);
+  DS_TRY(check_space(m, save_bytes, scratch_bytes));
+  Arena a(align256(save)), b(align256(scratch));
+  SaveBufs s = plan_save(m, a);
+  Scratch w = plan_scratch(m, b);
+  Fwd f{m, *d, *p, *g, x, d->res_mode ? res_att : nullptr, out, re_at, s, w, (hipStream_t)stream};
+  return f.run();
+}
+
+int dstagnn_block_backward(const dstagnn_block_dims* d, const dstagnn_block_params* p, const dstagnn_graph* g,
+                           const float* x, const float* res_att, const float* d_out, const float* d_re_at, float* d_x,
+                           float* d_res_att, const dstagnn_block_grads* grads, void* save, size_t save_bytes,
+                           void* scratch, size_t scratch_bytes, dstagnn_stream_t stream) {
+  (void)res_att;
+  DS_TRY(check_dims(d));
+  if (!p || !g || !x || !d_out || !d_x || !grads || !save || !scratch) {
+    set_last_error("null argument");
+    return DSTAGNN_E_ARG;
+  }
+  Dims m = mkdims(*d);
+  DS_TRY(check_space(m, save_bytes, scratch_bytes));
+  Arena a(align256(save)), b(align256(scratch));
+  SaveBufs s = plan_save(m, a);
+  Scratch w = plan_scratch(m, b);
+  Bwd bw{m, *d, *p, *g, *grads, x, d_out, d_re_at, d_x, d->res_mode ? d_res_att : nullptr, s, w, (hipStream_t)stream};
+  return bw.run();
+}
+
+int dstagnn_cheb_sat_forward(int B, int N, int F, int T, int K, int C, const float* x, const float* sat,
+                             const float* theta_cat, const float* mask_cat, const float* cheb, const float* adj_pa,
+                             float* out, float* P, float* W, float* xth, void* scratch, size_t scratch_bytes,
+                             dstagnn_stream_t stream) {
+  if (K > DSTAGNN_MAX_K || K <= 0) return DSTAGNN_E_SHAPE;
+  if (scratch_bytes < kGemmWs * sizeof(float) + 256) { set_last_error("scratch too small"); return DSTAGNN_E_SPACE; }
+  const float* masks[DSTAGNN_MAX_K];
+  for (int k = 0; k < K; ++k) masks[k] = mask_cat + (int64_t)k * N * N;
+  ChebIO c;
+  c.B = B; c.N = N; c.F = F; c.T = T; c.K = K; c.C = C;
+  c.x = x; c.S = sat; c.mask = masks; c.cheb = cheb; c.apa = adj_pa; c.thcat = theta_cat;
+  c.P = P; c.W = W; c.xth = xth; c.X = out;
+  return cheb_forward(c, (float*)align256(scratch), (hipStream_t)stream);
+}
+
+int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C, const float* x, const float* theta_cat,
+                              const float* cheb, const float* adj_pa, const float* out, const float* P, const float* W,
+                              const float* xth, const float* d_out, float* d_x, float* d_sat, float* d_theta_cat,
+                              float* d_mask_cat, void* scratch, size_t scratch_bytes, dstagnn_stream_t stream) {
+  if (K > DSTAGNN_MAX_K || K <= 0) return DSTAGNN_E_SHAPE;
+  const int64_t nbig = (int64_t)B * N * C * T;
+  const int64_t nxth = (int64_t)B * N * K * C * T;
+  size_t need = (kGemmWs + nbig + nxth) * sizeof(float) + 3 * 256;
+  if (scratch_bytes < need) { set_last_error("scratch too small"); return DSTAGNN_E_SPACE; }
+  Arena a(align256(scratch));
+  float* ws = a.take(kGemmWs);
+  float* gpre = a.take(nbig);
+  float* dxth = a.take(nxth);
+  hipStream_t st = (hipStream_t)stream;
+  DS_TRY(op_relu_mask(d_out, out, gpre, nbig, st));
+  float* dmask[DSTAGNN_MAX_K];
+  for (int k = 0; k < K; ++k) dmask[k] = d_mask_cat + (int64_t)k * N * N;
+  ChebGradIO c;
+  c.B = B; c.N = N; c.F = F; c.T = T; c.K = K; c.C = C;
+  c.x = x; c.thcat = theta_cat; c.cheb = cheb; c.apa = adj_pa; c.P = P; c.W = W; c.xth = xth;
+  c.gpre = gpre; c.dx = d_x; c.dx_beta = 0.f; c.dz = d_sat; c.dthcat = d_theta_cat; c.dmask = dmask; c.dxth = dxth;
+  return cheb_backward(c, ws, st);
+}
+
+int dstagnn_gemm_f32(const dstagnn_gemm_desc* d, void* scratch, size_t scratch_bytes, dstagnn_stream_t stream) {
+  if (!d) return DSTAGNN_E_ARG;
+  Gemm g;
+  g.M = d->M; g.N = d->N; g.K = d->K; g.batch = d->batch > 0 ? d->batch : 1;
+  g.A = d->A; g.am = make_idx(d->a_m); g.ak = make_idx(d->a_k); g.az = make_idx(d->a_z); g.a_off = d->a_off;
+  g.B = d->B; g.bk = make_idx(d->b_k); g.bn = make_idx(d->b_n); g.bz = make_idx(d->b_z); g.b_off = d->b_off;
+  g.C = d->C; g.cm = make_idx(d->c_m); g.cn = make_idx(d->c_n); g.cz = make_idx(d->c_z); g.c_off = d->c_off;
+  g.alpha = d->alpha; g.beta = d->beta; g.bias = d->bias; g.bias_stride = d->bias_stride; g.relu = d->relu;
+  float* ws = scratch ? (float*)align256(scratch) : nullptr;
+  size_t wsf = scratch ? (scratch_bytes > 256 ? (scratch_bytes - 256) / sizeof(float) : 0) : 0;
+  return run_gemm(g, ws, wsf, (hipStream_t)stream);
+}
+
+int dstagnn_dropout_mask(const dstagnn_block_dims* d, int which, float* mask, dstagnn_stream_t stream) {
+  if (!d || !mask) return DSTAGNN_E_ARG;
+  int64_t n = which == 0 ? (int64_t)d->B * d->N * d->d_model : (int64_t)d->B * d->N * d->C * d->T;
+  return op_dropout_mask(mask, n, d->seed, (uint32_t)which, d->drop_p, (hipStream_t)stream);
+}
+
+int dstagnn_block_time_stage(const dstagnn_block_dims* d, const dstagnn_block_params* p, const dstagnn_graph* g,
+                             const float* x, const float* res_att, float* out, float* re_at, void* save,
+                             size_t save_bytes, void* scratch, size_t scratch_bytes, int stage, int iters,
+                             float* ms_per_launch, dstagnn_stream_t stream) {
+  DS_TRY(check_dims(d));
+  if (!ms_per_launch || iters <= 0) return DSTAGNN_E_ARG;
+  Dims m = mkdims(*d);
+  DS_TRY(check_space(m, save_bytes, scratch_bytes));
+  Arena a(align256(save)), b(align256(scratch));
+  SaveBufs s = plan_save(m, a);
+  Scratch w = plan_scratch(m, b);
+  hipStream_t st = (hipStream_t)stream;
+  Fwd f{m, *d, *p, *g, x, d->res_mode ? res_att : nullptr, out, re_at, s, w, st};
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  int rc = 0;
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < iters && rc == 0; ++i) {
+    switch (stage) {
+      case 0: rc = f.run(); break;
+      case 2: rc = f.stage_cheb(); break;
+      case 3: rc = f.stage_preconv(); break;
+      case 10: rc = run_gemm(f.preconv_gemm(), w.gemm_ws, kGemmWs, st); break;  // the hot GEMM alone
+      default: rc = DSTAGNN_E_ARG;
+    }
+  }
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  *ms_per_launch = ms / iters;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,132 @@
+// common.hpp — shared device/host helpers for the gfx950 (CDNA4) DSTAGNN kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+#include <string>
+
+#include "../../include/dstagnn.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------
+// Unsigned fast division by a runtime constant (round-up magic, valid for n < 2^31).
+// q = (umulhi(n, m) + n) >> s   with s = ceil(log2 d), m = 2^32 (2^s - d) / d + 1.
+// ---------------------------------------------------------------------------------
+struct FastDiv {
+  uint32_t d = 1, m = 1, s = 0;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d ? d : 1;
+  uint32_t s = 0;
+  while ((1ull << s) < f.d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - f.d)) / f.d + 1);
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+// Two-level affine index map:  off(i) = (i % d) * s0 + (i / d) * s1   (d == 0: i * s0)
+struct Idx2 {
+  FastDiv f;
+  int32_t two = 0;  // 0: single level
+  int64_t s0 = 0, s1 = 0;
+};
+
+inline Idx2 make_idx(const dstagnn_idx& x) {
+  Idx2 r;
+  r.two = x.div > 0 ? 1 : 0;
+  r.f = make_fastdiv(x.div > 0 ? (uint32_t)x.div : 1u);
+  r.s0 = x.s0;
+  r.s1 = x.s1;
+  return r;
+}
+inline Idx2 idx1(int64_t s0) {
+  dstagnn_idx x{0, s0, 0};
+  return make_idx(x);
+}
+inline Idx2 idx2(int64_t div, int64_t s0, int64_t s1) {
+  dstagnn_idx x{div, s0, s1};
+  return make_idx(x);
+}
+
+__device__ __forceinline__ int64_t ioff(const Idx2& m, uint32_t i) {
+  if (!m.two) return (int64_t)i * m.s0;
+  uint32_t q = fdiv(i, m.f);
+  uint32_t r = i - q * m.f.d;
+  return (int64_t)r * m.s0 + (int64_t)q * m.s1;
+}
+
+// ---------------------------------------------------------------------------------
+// Wave64 reductions (CDNA: 64 lanes; __shfl_xor spans the whole wave).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------
+// Counter-based dropout RNG (splitmix64 finaliser of seed ^ stream ^ index).
+// ---------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+// scale = 1/(1-p) when kept, 0 when dropped
+__device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t which, uint64_t idx, float p) {
+  uint64_t z = mix64(seed * 0x9E3779B97F4A7C15ull + ((uint64_t)which << 56) + idx * 0xD1B54A32D192ED03ull + 1);
+  float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  return u >= p ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+// ---------------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------------
+void set_last_error(const std::string& s);
+
+#define DS_CHECK_LAUNCH()                                            \
+  do {                                                               \
+    hipError_t _e = hipGetLastError();                               \
+    if (_e != hipSuccess) {                                          \
+      set_last_error(std::string("launch: ") + hipGetErrorString(_e)); \
+      return (int)_e;                                                \
+    }                                                                \
+  } while (0)
+
+#define DS_TRY(x)                 \
+  do {                            \
+    int _r = (x);                 \
+    if (_r != 0) return _r;       \
+  } while (0)
+
+static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------------
+// internal GEMM entry (gemm.hip)
+// ---------------------------------------------------------------------------------
+struct Gemm {
+  int M = 0, N = 0, K = 0, batch = 1;
+  const float* A = nullptr; Idx2 am, ak, az; int64_t a_off = 0;
+  const float* B = nullptr; Idx2 bk, bn, bz; int64_t b_off = 0;
+  float* C = nullptr;       Idx2 cm, cn, cz; int64_t c_off = 0;
+  float alpha = 1.f, beta = 0.f;
+  const float* bias = nullptr; int64_t bias_stride = 1;
+  int relu = 0;
+  int hot = 0;  // 1: launch under the separately named gemm_f32_hot_kernel (profiling tag)
+  Gemm() { am = ak = az = bk = bn = bz = cm = cn = cz = idx1(0); }
+};
+// ws: split-K partial slab scratch (may be null -> no split)
+int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st);

@@ -1,0 +1,255 @@
+// gemm.hip — generic strided fp32 contraction on the CDNA4 f32 matrix cores.
+//
+// Every dense contraction of the DSTAGNN block (TAt / SAt projections, pre_conv,
+// SAt scores, Chebyshev aggregation, GTU temporal convolutions as implicit im2col,
+// and all their weight / input gradients) is one call of this kernel with a
+// different set of two-level affine index maps — no permute / im2col copies in HBM.
+//
+// Math: v_mfma_f32_32x32x2_f32 (exact fp32 FMA chain, 64 FLOP/clk/SIMD = the fp32
+// peak; gfx950 has no xf32).  Block tile (64*WM) x (64*WN) x 16, 4 waves in 2x2,
+// each wave owns WM x WN 32x32 accumulators.  Global -> register prefetch of the
+// next k-tile overlaps the MFMAs on the current LDS buffer (2 LDS buffers, one
+// barrier per k-tile).  Split-K for long reductions writes fp32 partial slabs that a
+// deterministic second pass sums (no float atomics: bitwise reproducible).
+#include "common.hpp"
+
+namespace {
+
+constexpr int BK = 16;
+
+struct GemmK {
+  int M, N, K, batch, splitk, kchunk;
+  const float* A; Idx2 am, ak, az;
+  const float* B; Idx2 bk, bn, bz;
+  float* C; Idx2 cm, cn, cz;
+  float alpha, beta;
+  const float* bias; int64_t bias_stride;
+  int relu;
+  float* ws;  // split partials [batch][splitk][M][N]
+};
+
+__device__ __forceinline__ void epilogue_store(const GemmK& g, int zb, int m, int n, float v) {
+  float* C = g.C + ioff(g.cz, zb);
+  int64_t o = ioff(g.cm, m) + ioff(g.cn, n);
+  v *= g.alpha;
+  if (g.beta != 0.f) v += g.beta * C[o];
+  if (g.bias) v += g.bias[(int64_t)n * g.bias_stride];
+  if (g.relu) v = fmaxf(v, 0.f);
+  C[o] = v;
+}
+
+// A_KC: A is contiguous along k (thread mapping reads rows of 16 k).  Otherwise lanes
+// run along m.  B_NC: B contiguous along n (lanes along n), otherwise lanes along k.
+template <int WM, int WN, bool A_KC, bool B_NC>
+__device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // elements per thread
+  __shared__ float As[2][BK][BM + 1];
+  __shared__ float Bs[2][BK][BN + 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int zb = blockIdx.z / g.splitk, sp = blockIdx.z % g.splitk;
+  const int kbeg = sp * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  if (kbeg >= kend && g.splitk > 1) {
+    // empty split: contribute zeros
+  }
+
+  const float* A = g.A + ioff(g.az, zb);
+  const float* Bp = g.B + ioff(g.bz, zb);
+
+  // --- per-thread element coordinates inside a tile
+  int a_ml[LA], a_kl[LA], b_kl[LB], b_nl[LB];
+#pragma unroll
+  for (int j = 0; j < LA; ++j) {
+    int e = tid + 256 * j;
+    if (A_KC) { a_kl[j] = e % BK; a_ml[j] = e / BK; }
+    else      { a_ml[j] = e % BM; a_kl[j] = e / BM; }
+  }
+#pragma unroll
+  for (int j = 0; j < LB; ++j) {
+    int e = tid + 256 * j;
+    if (B_NC) { b_nl[j] = e % BN; b_kl[j] = e / BN; }
+    else      { b_kl[j] = e % BK; b_nl[j] = e / BK; }
+  }
+  int64_t a_mo[LA], b_no[LB];
+  bool a_mv[LA], b_nv[LB];
+#pragma unroll
+  for (int j = 0; j < LA; ++j) {
+    int m = m0 + a_ml[j];
+    a_mv[j] = m < g.M;
+    a_mo[j] = a_mv[j] ? ioff(g.am, m) : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < LB; ++j) {
+    int n = n0 + b_nl[j];
+    b_nv[j] = n < g.N;
+    b_no[j] = b_nv[j] ? ioff(g.bn, n) : 0;
+  }
+
+  float ra[LA], rb[LB];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < LA; ++j) {
+      int k = k0 + a_kl[j];
+      ra[j] = (a_mv[j] && k < kend) ? A[a_mo[j] + ioff(g.ak, k)] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      int k = k0 + b_kl[j];
+      rb[j] = (b_nv[j] && k < kend) ? Bp[ioff(g.bk, k) + b_no[j]] : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < LA; ++j) As[buf][a_kl[j]][a_ml[j]] = ra[j];
+#pragma unroll
+    for (int j = 0; j < LB; ++j) Bs[buf][b_kl[j]][b_nl[j]] = rb[j];
+  };
+
+  floatx16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (ntiles > 0) {
+    load_tile(kbeg);
+    store_tile(0);
+    __syncthreads();
+  }
+  const int lr = lane & 31, lk = lane >> 5;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BK);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      float a[WM], b[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) a[i] = As[cur][kk + lk][wr * 32 * WM + i * 32 + lr];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) b[j] = Bs[cur][kk + lk][wc * 32 * WN + j * 32 + lr];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < ntiles) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // --- epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = n0 + wc * 32 * WN + j * 32 + lr;
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wr * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (m >= g.M) continue;
+        if (g.splitk > 1) {
+          g.ws[(((int64_t)zb * g.splitk + sp) * g.M + m) * g.N + n] = acc[i][j][r];
+        } else {
+          epilogue_store(g, zb, m, n, acc[i][j][r]);
+        }
+      }
+    }
+}
+
+template <int WM, int WN, bool A_KC, bool B_NC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmK g) {
+  gemm_f32_body<WM, WN, A_KC, B_NC>(g);
+}
+// identical body under its own symbol: the call site the benchmark reports as the
+// dominant kernel (rocprofv3 then lists exactly that call site's launches)
+template <int WM, int WN, bool A_KC, bool B_NC>
+__global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmK g) {
+  gemm_f32_body<WM, WN, A_KC, B_NC>(g);
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmK g) {
+  const int64_t total = (int64_t)g.batch * g.M * g.N;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int n = (int)(idx % g.N);
+    int64_t t = idx / g.N;
+    int m = (int)(t % g.M);
+    int zb = (int)(t / g.M);
+    const float* p = g.ws + ((int64_t)zb * g.splitk * g.M + m) * g.N + n;
+    float s = 0.f;
+    for (int q = 0; q < g.splitk; ++q) s += p[(int64_t)q * g.M * g.N];
+    epilogue_store(g, zb, m, n, s);
+  }
+}
+
+template <int WM, int WN>
+void launch_cfg(const GemmK& k, bool akc, bool bnc, bool hot, hipStream_t st) {
+  dim3 grid((unsigned)cdiv64(k.M, 64 * WM), (unsigned)cdiv64(k.N, 64 * WN), (unsigned)(k.batch * k.splitk));
+#define DS_GEMM_LAUNCH(KER)                                                                     \
+  if (akc && bnc) hipLaunchKernelGGL((KER<WM, WN, true, true>), grid, dim3(256), 0, st, k);     \
+  else if (akc)   hipLaunchKernelGGL((KER<WM, WN, true, false>), grid, dim3(256), 0, st, k);    \
+  else if (bnc)   hipLaunchKernelGGL((KER<WM, WN, false, true>), grid, dim3(256), 0, st, k);    \
+  else            hipLaunchKernelGGL((KER<WM, WN, false, false>), grid, dim3(256), 0, st, k);
+  if (hot) { DS_GEMM_LAUNCH(gemm_f32_hot_kernel) } else { DS_GEMM_LAUNCH(gemm_f32_kernel) }
+#undef DS_GEMM_LAUNCH
+}
+
+}  // namespace
+
+int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return 0;
+  if (!g.A || !g.B || !g.C) { set_last_error("gemm: null operand"); return DSTAGNN_E_ARG; }
+  GemmK k;
+  k.M = g.M; k.N = g.N; k.K = g.K; k.batch = g.batch;
+  k.A = g.A + g.a_off; k.am = g.am; k.ak = g.ak; k.az = g.az;
+  k.B = g.B + g.b_off; k.bk = g.bk; k.bn = g.bn; k.bz = g.bz;
+  k.C = g.C + g.c_off; k.cm = g.cm; k.cn = g.cn; k.cz = g.cz;
+  k.alpha = g.alpha; k.beta = g.beta; k.bias = g.bias; k.bias_stride = g.bias_stride; k.relu = g.relu;
+  k.ws = ws;
+
+  // tile choice: the largest tile that still gives >= 256 workgroups (one per CU)
+  int WM = 1, WN = 1;
+  auto ntile = [&](int wm, int wn) { return cdiv64(g.M, 64 * wm) * cdiv64(g.N, 64 * wn) * g.batch; };
+  if (ntile(2, 2) >= 256) { WM = 2; WN = 2; }
+  else if (ntile(2, 1) >= 256) { WM = 2; WN = 1; }
+  const int64_t tiles = ntile(WM, WN);
+
+  // split-K when even 64x64 tiles leave most CUs idle and the reduction is long
+  int splitk = 1;
+  if (g.K > 0 && tiles < 128 && g.K >= 512 && ws) {
+    int want = (int)std::min<int64_t>(64, cdiv64(512, tiles));
+    int maxk = g.K / 128;  // keep >= 128 k per split
+    splitk = std::max(1, std::min(want, maxk));
+    while (splitk > 1 && (size_t)g.batch * splitk * g.M * g.N > ws_floats) --splitk;
+  }
+  int kchunk = g.K;
+  if (splitk > 1) {
+    kchunk = (int)cdiv64(cdiv64(g.K, splitk), BK) * BK;
+    splitk = (int)cdiv64(g.K, kchunk);
+  }
+  if (g.K <= 0) { splitk = 1; kchunk = 0; }
+  k.splitk = splitk; k.kchunk = kchunk;
+
+  const bool akc = !g.ak.two && g.ak.s0 == 1;
+  const bool bnc = !g.bn.two && g.bn.s0 == 1;
+  const bool hot = g.hot != 0;
+  if (WM == 2 && WN == 2) launch_cfg<2, 2>(k, akc, bnc, hot, st);
+  else if (WM == 2) launch_cfg<2, 1>(k, akc, bnc, hot, st);
+  else launch_cfg<1, 1>(k, akc, bnc, hot, st);
+  DS_CHECK_LAUNCH();
+  if (splitk > 1) {
+    int64_t total = (int64_t)g.batch * g.M * g.N;
+    unsigned blocks = (unsigned)std::min<int64_t>(4096, cdiv64(total, 256));
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, k);
+    DS_CHECK_LAUNCH();
+  }
+  return 0;
+}

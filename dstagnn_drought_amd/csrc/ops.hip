@@ -1,0 +1,708 @@
+// ops.hip — the non-GEMM kernels of the DSTAGNN block (gfx950, wave64).
+//
+//   tat_fwd / tat_bwd     temporal attention core per (b,f,head): T x T scores,
+//                         softmax over the QUERY axis (model/DSTAGNN_my.py:37-41)
+//   ln_fwd / ln_bwd       row LayerNorm over strided multi-source sums (TAt LN_N :100,
+//                         EmbedT LN_N :176-181, EmbedS LN_D :180-181) + fused dropout
+//   cheb_softmax_fwd/bwd  column softmax over source node i of S'+A_pa*M_k, times T_k
+//                         (cheb_conv_withSAt :126-128), and its backward
+//   gate_fwd / gate_bwd   GTU gates tanh(p)*sigmoid(q) + concat (:192-197, :242)
+//   tail_fwd / tail_bwd   fcmy dropout + residual + ReLU + LN_C (:243-252)
+//   reductions            deterministic two-stage column sums (bias / gamma / beta grads)
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace {
+
+// =====================================================================================
+// generic batched transpose  out[b][c][r] = in[b][r][c] (+ beta * out)
+// =====================================================================================
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                        int R, int Cc, int64_t in_bs, int64_t out_bs, float beta) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const float* ip = in + (int64_t)b * in_bs;
+  float* op = out + (int64_t)b * out_bs;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int y = ty; y < 32; y += 8) {
+    int r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < R && c < Cc) ? ip[(int64_t)r * Cc + c] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    int c = c0 + y, r = r0 + tx;
+    if (r < R && c < Cc) {
+      int64_t o = (int64_t)c * R + r;
+      float v = tile[tx][y];
+      if (beta != 0.f) v += beta * op[o];
+      op[o] = v;
+    }
+  }
+}
+
+// =====================================================================================
+// temporal attention core (one workgroup per (b, f, head))
+// =====================================================================================
+struct TatArgs {
+  int B, F, T, h, dk, dv;
+  const float* qkv;      // (B*F*T, 2*h*dk + h*dv): [Q | K | V]
+  const float* res;      // res_att or null
+  int res_mode;
+  float scale;
+  float* re_at;          // (B,F,h,T,T) scores
+  float* att;            // (B,F,h,T,T) softmax (saved)
+  float* ctx;            // (B*F*T, h*dv)
+  // bwd
+  const float* dctx;     // (B*F*T, h*dv)
+  const float* dre;      // (B,F,h,T,T) or null
+  float* dqkv;           // (B*F*T, 3 cols blocks)
+  float* dscore;         // (B,F,h,T,T) dS (== d res_att before f-reduction)
+};
+
+__global__ __launch_bounds__(256) void tat_fwd_kernel(TatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int T = a.T, dk = a.dk, dv = a.dv;
+  const int dkp = dk + 1, dvp = dv + 1;
+  float* Qs = sm;
+  float* Ks = Qs + T * dkp;
+  float* Vs = Ks + T * dkp;
+  float* Ss = Vs + T * dvp;  // T*T
+  const int id = blockIdx.x;  // ((b*F + f)*h + hd)
+  const int hd = id % a.h;
+  const int bf = id / a.h;
+  const int b = bf / a.F;
+  const int ld = 2 * a.h * dk + a.h * dv;
+  const float* base = a.qkv + (int64_t)bf * T * ld;
+  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+    int i = e / dk, d = e % dk;
+    Qs[i * dkp + d] = base[(int64_t)i * ld + hd * dk + d];
+    Ks[i * dkp + d] = base[(int64_t)i * ld + a.h * dk + hd * dk + d];
+  }
+  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {
+    int i = e / dv, d = e % dv;
+    Vs[i * dvp + d] = base[(int64_t)i * ld + 2 * a.h * dk + hd * dv + d];
+  }
+  __syncthreads();
+  const int64_t sbase = (int64_t)id * T * T;
+  const float* rp = nullptr;
+  if (a.res_mode == DSTAGNN_RES_BCAST) rp = a.res + ((int64_t)b * a.h + hd) * T * T;
+  else if (a.res_mode == DSTAGNN_RES_FULL) rp = a.res + sbase;
+  for (int e = threadIdx.x; e < T * T; e += blockDim.x) {
+    int i = e / T, j = e % T;
+    float s = 0.f;
+    for (int d = 0; d < dk; ++d) s = fmaf(Qs[i * dkp + d], Ks[j * dkp + d], s);
+    s = s * a.scale;
+    if (rp) s += rp[e];
+    Ss[e] = s;
+    a.re_at[sbase + e] = s;
+  }
+  __syncthreads();
+  // softmax over i (query axis) for each column j
+  for (int j = threadIdx.x; j < T; j += blockDim.x) {
+    float m = -INFINITY;
+    for (int i = 0; i < T; ++i) m = fmaxf(m, Ss[i * T + j]);
+    float l = 0.f;
+    for (int i = 0; i < T; ++i) l += expf(Ss[i * T + j] - m);
+    float inv = 1.f / l;
+    for (int i = 0; i < T; ++i) Ss[i * T + j] = expf(Ss[i * T + j] - m) * inv;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * T; e += blockDim.x) a.att[sbase + e] = Ss[e];
+  const int ldc = a.h * dv;
+  float* cbase = a.ctx + (int64_t)bf * T * ldc;
+  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {
+    int i = e / dv, d = e % dv;
+    float s = 0.f;
+    for (int j = 0; j < T; ++j) s = fmaf(Ss[i * T + j], Vs[j * dvp + d], s);
+    cbase[(int64_t)i * ldc + hd * dv + d] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void tat_bwd_kernel(TatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int T = a.T, dk = a.dk, dv = a.dv;
+  const int dkp = dk + 1, dvp = dv + 1;
+  float* Qs = sm;
+  float* Ks = Qs + T * dkp;
+  float* Vs = Ks + T * dkp;
+  float* dCs = Vs + T * dvp;    // T*dvp
+  float* As = dCs + T * dvp;    // T*T
+  float* dAs = As + T * T;      // T*T  (becomes dS)
+  const int id = blockIdx.x;
+  const int hd = id % a.h;
+  const int bf = id / a.h;
+  const int ld = 2 * a.h * dk + a.h * dv;
+  const int ldc = a.h * dv;
+  const float* base = a.qkv + (int64_t)bf * T * ld;
+  const float* cb = a.dctx + (int64_t)bf * T * ldc;
+  const int64_t sbase = (int64_t)id * T * T;
+  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+    int i = e / dk, d = e % dk;
+    Qs[i * dkp + d] = base[(int64_t)i * ld + hd * dk + d];
+    Ks[i * dkp + d] = base[(int64_t)i * ld + a.h * dk + hd * dk + d];
+  }
+  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {
+    int i = e / dv, d = e % dv;
+    Vs[i * dvp + d] = base[(int64_t)i * ld + 2 * a.h * dk + hd * dv + d];
+    dCs[i * dvp + d] = cb[(int64_t)i * ldc + hd * dv + d];
+  }
+  for (int e = threadIdx.x; e < T * T; e += blockDim.x) As[e] = a.att[sbase + e];
+  __syncthreads();
+  // dA[i][j] = sum_d dctx[i][d] V[j][d]
+  for (int e = threadIdx.x; e < T * T; e += blockDim.x) {
+    int i = e / T, j = e % T;
+    float s = 0.f;
+    for (int d = 0; d < dv; ++d) s = fmaf(dCs[i * dvp + d], Vs[j * dvp + d], s);
+    dAs[e] = s;
+  }
+  // dV[j][d] = sum_i A[i][j] dctx[i][d]
+  float* dbase = a.dqkv + (int64_t)bf * T * ld;
+  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {
+    int j = e / dv, d = e % dv;
+    float s = 0.f;
+    for (int i = 0; i < T; ++i) s = fmaf(As[i * T + j], dCs[i * dvp + d], s);
+    dbase[(int64_t)j * ld + 2 * a.h * dk + hd * dv + d] = s;
+  }
+  __syncthreads();
+  // column softmax backward: dS = A * (dA - sum_i A dA) + d re_At
+  for (int j = threadIdx.x; j < T; j += blockDim.x) {
+    float c = 0.f;
+    for (int i = 0; i < T; ++i) c = fmaf(As[i * T + j], dAs[i * T + j], c);
+    for (int i = 0; i < T; ++i) {
+      float v = As[i * T + j] * (dAs[i * T + j] - c);
+      if (a.dre) v += a.dre[sbase + i * T + j];
+      dAs[i * T + j] = v;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * T; e += blockDim.x) a.dscore[sbase + e] = dAs[e];
+  // dQ[i][d] = scale * sum_j dS[i][j] K[j][d];  dK[j][d] = scale * sum_i dS[i][j] Q[i][d]
+  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+    int i = e / dk, d = e % dk;
+    float sq = 0.f, sk = 0.f;
+    for (int j = 0; j < T; ++j) {
+      sq = fmaf(dAs[i * T + j], Ks[j * dkp + d], sq);
+      sk = fmaf(dAs[j * T + i], Qs[j * dkp + d], sk);
+    }
+    dbase[(int64_t)i * ld + hd * dk + d] = sq * a.scale;
+    dbase[(int64_t)i * ld + a.h * dk + hd * dk + d] = sk * a.scale;
+  }
+}
+
+// =====================================================================================
+// LayerNorm over rows of length L; one wave per row, values kept in registers.
+// =====================================================================================
+template <int VPT>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.R) return;
+  float v[VPT];
+  int64_t o[3];
+  for (int s = 0; s < a.nsrc; ++s) o[s] = ioff(a.src[s].row, row);
+  float sum = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    int e = lane + 64 * q;
+    float u = 0.f;
+    if (e < a.L) {
+      for (int s = 0; s < a.nsrc; ++s) u += a.src[s].p[o[s] + (int64_t)e * a.src[s].es];
+    }
+    v[q] = u;
+    sum += u;
+  }
+  const float mean = wave_sum(sum) / a.L;
+  float var = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    int e = lane + 64 * q;
+    if (e < a.L) { float d = v[q] - mean; var += d * d; }
+  }
+  var = wave_sum(var) / a.L;
+  const float rs = rsqrtf(var + a.eps);
+  if (lane == 0) { a.mu[row] = mean; a.rs[row] = rs; }
+  const int64_t yo = ioff(a.yrow, row);
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    int e = lane + 64 * q;
+    if (e < a.L) {
+      if (a.u) a.u[(int64_t)row * a.L + e] = v[q];
+      float y = (v[q] - mean) * rs * a.g[e] + a.b[e];
+      if (a.drop_p > 0.f) y *= drop_scale(a.seed, a.which, (uint64_t)row * a.L + e, a.drop_p);
+      a.y[yo + (int64_t)e * a.yes] = y;
+    }
+  }
+}
+
+template <int VPT>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.R) return;
+  const float mean = a.mu[row], rs = a.rs[row];
+  const int64_t yo = ioff(a.dyrow, row);
+  float dyv[VPT], xh[VPT];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    int e = lane + 64 * q;
+    dyv[q] = 0.f; xh[q] = 0.f;
+    if (e < a.L) {
+      float dy = a.dy[yo + (int64_t)e * a.dyes];
+      if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * a.L + e, a.drop_p);
+      float x = (a.u[(int64_t)row * a.L + e] - mean) * rs;
+      dyv[q] = dy; xh[q] = x;
+      float dxh = dy * a.g[e];
+      s1 += dxh; s2 += dxh * x;
+      if (a.gcontrib) a.gcontrib[(int64_t)row * a.L + e] = dy * x;
+      if (a.bcontrib) a.bcontrib[(int64_t)row * a.L + e] = dy;
+    }
+  }
+  s1 = wave_sum(s1) / a.L;
+  s2 = wave_sum(s2) / a.L;
+  const int64_t xo = ioff(a.dxrow, row);
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    int e = lane + 64 * q;
+    if (e < a.L) {
+      float dx = rs * (dyv[q] * a.g[e] - s1 - xh[q] * s2);
+      int64_t oo = xo + (int64_t)e * a.dxes;
+      if (a.beta != 0.f) dx += a.beta * a.dx[oo];
+      a.dx[oo] = dx;
+    }
+  }
+}
+
+// =====================================================================================
+// reductions
+// =====================================================================================
+// stage 1: in viewed as (A, E) (E = O*I contiguous per a).  part[p][e] = sum over the
+// p-th chunk of a of in[a][e] (* in2[a][e]).
+__global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ in, const float* __restrict__ in2,
+                                                     int64_t A, int E, int64_t achunk, float* __restrict__ part) {
+  const int p = blockIdx.y;
+  const int64_t a0 = (int64_t)p * achunk, a1 = min(A, a0 + achunk);
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t aa = a0; aa < a1; ++aa) {
+      float v = in[aa * E + e];
+      if (in2) v *= in2[aa * E + e];
+      s += v;
+    }
+    part[(int64_t)p * E + e] = s;
+  }
+}
+// stage 2: out[o] = beta*out[o] + sum_p sum_i part[p][o*I + i]
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int P, int O, int I,
+                                                     float* __restrict__ out, int64_t ostride, float beta) {
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int p = 0; p < P; ++p)
+      for (int i = 0; i < I; ++i) s += part[((int64_t)p * O + o) * I + i];
+    float* d = out + (int64_t)o * ostride;
+    *d = (beta != 0.f ? beta * *d : 0.f) + s;
+  }
+}
+
+// out[a][i] = beta*out + sum_m in[a][m][i]
+__global__ __launch_bounds__(256) void sum_middle_kernel(const float* __restrict__ in, int64_t A, int Mm, int64_t I,
+                                                         float* __restrict__ out, float beta) {
+  const int64_t total = A * I;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t a = idx / I, i = idx % I;
+    float s = 0.f;
+    for (int m = 0; m < Mm; ++m) s += in[(a * Mm + m) * I + i];
+    out[idx] = (beta != 0.f ? beta * out[idx] : 0.f) + s;
+  }
+}
+
+__global__ __launch_bounds__(256) void relu_mask_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                        float* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = y[i] > 0.f ? g[i] : 0.f;
+}
+
+// =====================================================================================
+// Chebyshev spatial-attention softmax (column softmax over source node i)
+// grid (ceil(N/64), B*K), block 256 = 64 columns x 4 row groups
+// =====================================================================================
+__global__ __launch_bounds__(256) void cheb_softmax_fwd_kernel(ChebSm a) {
+  __shared__ float sm_m[4][64], sm_l[4][64];
+  const int N = a.N;
+  const int bk = blockIdx.y;
+  const int k = bk % a.K;
+  const int cj = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cj;
+  const float* S = a.S + (int64_t)bk * N * N;
+  const float* Mk = a.mask[k];
+  const float* Tk = a.cheb + (int64_t)k * N * N;
+  float m = -INFINITY, l = 0.f;
+  if (j < N) {
+    for (int i = g; i < N; i += 4) {
+      int64_t o = (int64_t)i * N + j;
+      float z = S[o] + a.apa[o] * Mk[o];
+      float mn = fmaxf(m, z);
+      l = l * expf(m - mn) + expf(z - mn);
+      m = mn;
+    }
+  }
+  sm_m[g][cj] = m; sm_l[g][cj] = l;
+  __syncthreads();
+  float M = sm_m[0][cj];
+  for (int q = 1; q < 4; ++q) M = fmaxf(M, sm_m[q][cj]);
+  float L = 0.f;
+  for (int q = 0; q < 4; ++q) L += sm_l[q][cj] * expf(sm_m[q][cj] - M);
+  const float inv = 1.f / L;
+  if (j < N) {
+    float* P = a.P + (int64_t)bk * N * N;
+    float* W = a.W + (int64_t)bk * N * N;
+    for (int i = g; i < N; i += 4) {
+      int64_t o = (int64_t)i * N + j;
+      float z = S[o] + a.apa[o] * Mk[o];
+      float p = expf(z - M) * inv;
+      P[o] = p;
+      W[o] = Tk[o] * p;
+    }
+  }
+}
+
+// dz = P * (T*dW - sum_i P*T*dW)   written to dz (may alias dW)
+__global__ __launch_bounds__(256) void cheb_softmax_bwd_kernel(ChebSm a) {
+  __shared__ float sm_c[4][64];
+  const int N = a.N;
+  const int bk = blockIdx.y;
+  const int k = bk % a.K;
+  const int cj = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cj;
+  const float* P = a.P + (int64_t)bk * N * N;
+  const float* dW = a.dW + (int64_t)bk * N * N;
+  const float* Tk = a.cheb + (int64_t)k * N * N;
+  float c = 0.f;
+  if (j < N)
+    for (int i = g; i < N; i += 4) {
+      int64_t o = (int64_t)i * N + j;
+      c += P[o] * Tk[o] * dW[o];
+    }
+  sm_c[g][cj] = c;
+  __syncthreads();
+  c = sm_c[0][cj] + sm_c[1][cj] + sm_c[2][cj] + sm_c[3][cj];
+  if (j < N) {
+    float* dz = a.dz + (int64_t)bk * N * N;
+    for (int i = g; i < N; i += 4) {
+      int64_t o = (int64_t)i * N + j;
+      dz[o] = P[o] * (Tk[o] * dW[o] - c);
+    }
+  }
+}
+
+// dM_k[i][j] = A_pa[i][j] * sum_b dz[b][k][i][j]
+__global__ __launch_bounds__(256) void cheb_mask_grad_kernel(ChebSm a) {
+  const int64_t NN = (int64_t)a.N * a.N;
+  const int k = blockIdx.y;
+  float* out = a.dmask[k];
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < NN; o += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < a.B; ++b) s += a.dz[((int64_t)b * a.K + k) * NN + o];
+    out[o] = a.apa[o] * s;
+  }
+}
+
+// =====================================================================================
+// GTU gates.  conv_g layout [bn][2C][Tg], Tg = T - ks + 1; Gcat [bn][C][3T-12]
+// =====================================================================================
+__global__ __launch_bounds__(256) void gate_fwd_kernel(GateArgs a) {
+  const int S = 3 * a.T - 12;
+  const int64_t total = (int64_t)a.BN * a.C * S;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int s = (int)(idx % S);
+    int64_t r = idx / S;
+    int c = (int)(r % a.C);
+    int64_t bn = r / a.C;
+    int gi = 0, t = s;
+    while (gi < 2 && t >= a.T - 2 - 2 * gi) { t -= a.T - 2 - 2 * gi; ++gi; }
+    const int Tg = a.T - 2 - 2 * gi;
+    const float* cv = a.conv[gi] + bn * 2 * a.C * Tg;
+    float p = cv[(int64_t)c * Tg + t];
+    float q = cv[(int64_t)(a.C + c) * Tg + t];
+    a.G[idx] = tanhf(p) * (1.f / (1.f + expf(-q)));
+  }
+}
+
+// dconv_pad_g[bn][o][Lp], Lp = T + ks - 1, data at [ks-1, ks-1+Tg), zeros elsewhere
+__global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a, int gi) {
+  const int S = 3 * a.T - 12;
+  const int ks = 3 + 2 * gi;
+  const int Tg = a.T - ks + 1;
+  const int Lp = a.T + ks - 1;
+  const int off = gi == 0 ? 0 : (gi == 1 ? a.T - 2 : 2 * a.T - 6);
+  const int64_t total = (int64_t)a.BN * 2 * a.C * Lp;
+  float* out = a.dconv_pad[gi];
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int l = (int)(idx % Lp);
+    int64_t r = idx / Lp;
+    int o = (int)(r % (2 * a.C));
+    int64_t bn = r / (2 * a.C);
+    int t = l - (ks - 1);
+    float v = 0.f;
+    if (t >= 0 && t < Tg) {
+      int c = o < a.C ? o : o - a.C;
+      const float* cv = a.conv[gi] + bn * 2 * a.C * Tg;
+      float p = cv[(int64_t)c * Tg + t];
+      float q = cv[(int64_t)(a.C + c) * Tg + t];
+      float dg = a.dG[(bn * a.C + c) * S + off + t];
+      float th = tanhf(p), sg = 1.f / (1.f + expf(-q));
+      v = o < a.C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
+    }
+    out[idx] = v;
+  }
+}
+
+// =====================================================================================
+// block tail: fcmy dropout, residual, ReLUs and LN over C (one thread per (b,n,t) row)
+// =====================================================================================
+__global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
+  const int C = a.C, T = a.T;
+  const int64_t R = (int64_t)a.BN * T;
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < R; row += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bn = row / T;
+    const int t = (int)(row % T);
+    const int64_t base = bn * C * T + t;
+    float sum = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const int64_t o = base + (int64_t)c * T;
+      float tc = a.tc[o];
+      if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
+      float tco, xres;
+      if (a.first) {
+        tco = fmaxf(tc, 0.f);
+        xres = a.res_w[c] * a.x[bn * T + t] + a.res_b[c];
+      } else {
+        tco = fmaxf(a.X[o] + tc, 0.f);
+        xres = a.x[o];
+      }
+      float r = fmaxf(xres + tco, 0.f);
+      a.tco[o] = tco;
+      a.r[o] = r;
+      sum += r;
+    }
+    const float mean = sum / C;
+    float var = 0.f;
+    for (int c = 0; c < C; ++c) { float d = a.r[base + (int64_t)c * T] - mean; var += d * d; }
+    var /= C;
+    const float rs = rsqrtf(var + 1e-5f);
+    a.mu[row] = mean; a.rs[row] = rs;
+    for (int c = 0; c < C; ++c) {
+      const int64_t o = base + (int64_t)c * T;
+      a.out[o] = (a.r[o] - mean) * rs * a.ln_g[c] + a.ln_b[c];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void tail_bwd_kernel(TailArgs a) {
+  const int C = a.C, T = a.T;
+  const int64_t R = (int64_t)a.BN * T;
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < R; row += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bn = row / T;
+    const int t = (int)(row % T);
+    const int64_t base = bn * C * T + t;
+    const float mean = a.mu[row], rs = a.rs[row];
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const int64_t o = base + (int64_t)c * T;
+      float dy = a.dout[o];
+      float xh = (a.r[o] - mean) * rs;
+      float dxh = dy * a.ln_g[c];
+      s1 += dxh; s2 += dxh * xh;
+      a.gcontrib[o] = dy * xh;
+    }
+    s1 /= C; s2 /= C;
+    float dxsum = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const int64_t o = base + (int64_t)c * T;
+      float ro = a.r[o];
+      float xh = (ro - mean) * rs;
+      float dr = rs * (a.dout[o] * a.ln_g[c] - s1 - xh * s2);
+      dr = ro > 0.f ? dr : 0.f;                       // relu(xres + tco)
+      float dtco = a.tco[o] > 0.f ? dr : 0.f;          // tco = relu(...)
+      float dtc = dtco;
+      if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
+      a.dtc[o] = dtc;
+      if (a.first) {
+        a.dX[o] = 0.f;
+        a.rcontrib[o] = dr * a.x[bn * T + t];   // d residual_conv.weight contributions
+        a.dres[o] = dr;                          // d residual_conv.bias contributions
+        dxsum += a.res_w[c] * dr;
+      } else {
+        a.dX[o] = dtco;
+        a.dx[o] = dr;
+      }
+    }
+    if (a.first) a.dx[bn * T + t] = dxsum;
+  }
+}
+
+__global__ void dropout_mask_kernel(float* out, int64_t n, uint64_t seed, uint32_t which, float p) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = drop_scale(seed, which, (uint64_t)i, p);
+}
+
+inline unsigned grid1d(int64_t n, int64_t cap = 8192) {
+  int64_t b = cdiv64(n, 256);
+  return (unsigned)std::max<int64_t>(1, std::min(b, cap));
+}
+
+}  // namespace
+
+// =====================================================================================
+// launchers
+// =====================================================================================
+int op_transpose(const float* in, float* out, int R, int Cc, int batch, int64_t in_bs, int64_t out_bs, float beta,
+                 hipStream_t st) {
+  dim3 grid((unsigned)cdiv64(Cc, 32), (unsigned)cdiv64(R, 32), (unsigned)batch);
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, st, in, out, R, Cc, in_bs, out_bs, beta);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+static size_t tat_fwd_lds(int T, int dk, int dv) {
+  return sizeof(float) * (size_t)(2 * T * (dk + 1) + T * (dv + 1) + T * T);
+}
+static size_t tat_bwd_lds(int T, int dk, int dv) {
+  return sizeof(float) * (size_t)(2 * T * (dk + 1) + 2 * T * (dv + 1) + 2 * T * T);
+}
+
+int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
+               float* re_at, float* att, float* ctx, hipStream_t st) {
+  TatArgs a{};
+  a.B = B; a.F = F; a.T = T; a.h = h; a.dk = dk; a.dv = dv;
+  a.qkv = qkv; a.res = res; a.res_mode = res ? res_mode : 0; a.scale = 1.f / sqrtf((float)dk);
+  a.re_at = re_at; a.att = att; a.ctx = ctx;
+  size_t lds = tat_fwd_lds(T, dk, dv);
+  if (lds > 160 * 1024) { set_last_error("tat_fwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  hipLaunchKernelGGL(tat_fwd_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
+               const float* dre, float* dqkv, float* dscore, hipStream_t st) {
+  TatArgs a{};
+  a.B = B; a.F = F; a.T = T; a.h = h; a.dk = dk; a.dv = dv;
+  a.qkv = qkv; a.att = const_cast<float*>(att); a.scale = 1.f / sqrtf((float)dk);
+  a.dctx = dctx; a.dre = dre; a.dqkv = dqkv; a.dscore = dscore;
+  size_t lds = tat_bwd_lds(T, dk, dv);
+  if (lds > 160 * 1024) { set_last_error("tat_bwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  hipLaunchKernelGGL(tat_bwd_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_ln_fwd(const LnFwd& a, hipStream_t st) {
+  dim3 grid((unsigned)cdiv64(a.R, 4));
+  int vpt = (int)cdiv64(a.L, 64);
+  if (vpt <= 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 4) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 8) hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 16) hipLaunchKernelGGL(ln_fwd_kernel<16>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 64) hipLaunchKernelGGL(ln_fwd_kernel<64>, grid, dim3(256), 0, st, a);
+  else { set_last_error("ln_fwd: row too long"); return DSTAGNN_E_SHAPE; }
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_ln_bwd(const LnBwd& a, hipStream_t st) {
+  dim3 grid((unsigned)cdiv64(a.R, 4));
+  int vpt = (int)cdiv64(a.L, 64);
+  if (vpt <= 1) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 2) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 4) hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 8) hipLaunchKernelGGL(ln_bwd_kernel<8>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 16) hipLaunchKernelGGL(ln_bwd_kernel<16>, grid, dim3(256), 0, st, a);
+  else if (vpt <= 64) hipLaunchKernelGGL(ln_bwd_kernel<64>, grid, dim3(256), 0, st, a);
+  else { set_last_error("ln_bwd: row too long"); return DSTAGNN_E_SHAPE; }
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+// out[o*ostride] = beta*out + sum_{a<A, i<I} in[a][o][i] (* in2)
+int op_colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
+              float* part, size_t part_floats, hipStream_t st) {
+  const int E = O * I;
+  int P = (int)std::min<int64_t>(256, std::max<int64_t>(1, A / 64));
+  while (P > 1 && (size_t)P * E > part_floats) P /= 2;
+  if ((size_t)P * E > part_floats) { set_last_error("colsum: scratch too small"); return DSTAGNN_E_SPACE; }
+  const int64_t achunk = cdiv64(A, P);
+  dim3 g1((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv64(E, 256), 64)), (unsigned)P);
+  hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, st, in, in2, A, E, achunk, part);
+  DS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_stage2, dim3(grid1d(O)), dim3(256), 0, st, part, P, O, I, out, ostride, beta);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_sum_middle(const float* in, int64_t A, int Mm, int64_t I, float* out, float beta, hipStream_t st) {
+  hipLaunchKernelGGL(sum_middle_kernel, dim3(grid1d(A * I)), dim3(256), 0, st, in, A, Mm, I, out, beta);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_relu_mask(const float* g, const float* y, float* out, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid1d(n)), dim3(256), 0, st, g, y, out, n);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st) {
+  dim3 grid((unsigned)cdiv64(a.N, 64), (unsigned)(a.B * a.K));
+  hipLaunchKernelGGL(cheb_softmax_fwd_kernel, grid, dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st) {
+  dim3 grid((unsigned)cdiv64(a.N, 64), (unsigned)(a.B * a.K));
+  hipLaunchKernelGGL(cheb_softmax_bwd_kernel, grid, dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+int op_cheb_mask_grad(const ChebSm& a, hipStream_t st) {
+  dim3 grid(grid1d((int64_t)a.N * a.N, 1024), (unsigned)a.K);
+  hipLaunchKernelGGL(cheb_mask_grad_kernel, grid, dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_gate_fwd(const GateArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(gate_fwd_kernel, dim3(grid1d((int64_t)a.BN * a.C * (3 * a.T - 12))), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+int op_gate_bwd(const GateArgs& a, hipStream_t st) {
+  for (int gi = 0; gi < 3; ++gi) {
+    int Lp = a.T + 2 + 2 * gi + 0;  // T + ks - 1
+    hipLaunchKernelGGL(gate_bwd_kernel, dim3(grid1d((int64_t)a.BN * 2 * a.C * Lp)), dim3(256), 0, st, a, gi);
+    DS_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+int op_tail_fwd(const TailArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(tail_fwd_kernel, dim3(grid1d((int64_t)a.BN * a.T)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+int op_tail_bwd(const TailArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(tail_bwd_kernel, dim3(grid1d((int64_t)a.BN * a.T)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st) {
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid1d(n)), dim3(256), 0, st, out, n, seed, which, p);
+  DS_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,91 @@
+// ops.hpp — argument structs and launchers of the non-GEMM kernels (ops.hip).
+#pragma once
+#include "common.hpp"
+
+struct LnSrc {
+  const float* p = nullptr;
+  Idx2 row;          // row r -> base offset
+  int64_t es = 1;    // element stride
+};
+
+struct LnFwd {
+  int R = 0, L = 0;
+  LnSrc src[3];
+  int nsrc = 0;
+  const float* g = nullptr;
+  const float* b = nullptr;
+  float eps = 1e-5f;
+  float* y = nullptr; Idx2 yrow; int64_t yes = 1;
+  float* u = nullptr;           // optional (R, L) copy of the LN input sum
+  float* mu = nullptr; float* rs = nullptr;
+  float drop_p = 0.f; uint64_t seed = 0; uint32_t which = 0;  // dropout on the output
+};
+
+struct LnBwd {
+  int R = 0, L = 0;
+  const float* dy = nullptr; Idx2 dyrow; int64_t dyes = 1;
+  const float* u = nullptr; const float* mu = nullptr; const float* rs = nullptr; const float* g = nullptr;
+  float drop_p = 0.f; uint64_t seed = 0; uint32_t which = 0;  // mask applied to dy
+  float* dx = nullptr; Idx2 dxrow; int64_t dxes = 1; float beta = 0.f;
+  float* gcontrib = nullptr;    // optional (R, L): dy' * xhat  (gamma grad contributions)
+  float* bcontrib = nullptr;    // optional (R, L): dy'         (beta grad contributions)
+};
+
+struct ChebSm {
+  int B = 0, K = 0, N = 0;
+  const float* S = nullptr;       // (B,K,N,N) scores
+  const float* apa = nullptr;     // (N,N)
+  const float* mask[DSTAGNN_MAX_K] = {};
+  const float* cheb = nullptr;    // (K,N,N)
+  float* P = nullptr;             // (B,K,N,N)
+  float* W = nullptr;             // (B,K,N,N)
+  // bwd
+  const float* dW = nullptr;
+  float* dz = nullptr;
+  float* dmask[DSTAGNN_MAX_K] = {};
+};
+
+struct GateArgs {
+  int64_t BN = 0; int C = 0, T = 0;
+  const float* conv[3] = {};      // [bn][2C][T-ks+1]
+  float* G = nullptr;             // [bn][C][3T-12]
+  const float* dG = nullptr;
+  float* dconv_pad[3] = {};       // [bn][2C][T+ks-1]
+};
+
+struct TailArgs {
+  int64_t BN = 0; int C = 0, T = 0; int first = 0;
+  const float* X = nullptr;       // cheb output (B,N,C,T)
+  const float* tc = nullptr;      // fcmy output (B,N,C,T)
+  const float* x = nullptr;       // block input (B,N,F,T)
+  const float* res_w = nullptr; const float* res_b = nullptr;
+  const float* ln_g = nullptr; const float* ln_b = nullptr;
+  float drop_p = 0.f; uint64_t seed = 0;
+  float* tco = nullptr; float* r = nullptr; float* mu = nullptr; float* rs = nullptr; float* out = nullptr;
+  // bwd
+  const float* dout = nullptr;
+  float* gcontrib = nullptr;      // dout * xhat
+  float* dtc = nullptr; float* dX = nullptr; float* dx = nullptr;
+  float* rcontrib = nullptr; float* dres = nullptr;  // first block residual_conv grads
+};
+
+int op_transpose(const float* in, float* out, int R, int Cc, int batch, int64_t in_bs, int64_t out_bs, float beta,
+                 hipStream_t st);
+int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
+               float* re_at, float* att, float* ctx, hipStream_t st);
+int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
+               const float* dre, float* dqkv, float* dscore, hipStream_t st);
+int op_ln_fwd(const LnFwd& a, hipStream_t st);
+int op_ln_bwd(const LnBwd& a, hipStream_t st);
+int op_colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
+              float* part, size_t part_floats, hipStream_t st);
+int op_sum_middle(const float* in, int64_t A, int Mm, int64_t I, float* out, float beta, hipStream_t st);
+int op_relu_mask(const float* g, const float* y, float* out, int64_t n, hipStream_t st);
+int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st);
+int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st);
+int op_cheb_mask_grad(const ChebSm& a, hipStream_t st);
+int op_gate_fwd(const GateArgs& a, hipStream_t st);
+int op_gate_bwd(const GateArgs& a, hipStream_t st);
+int op_tail_fwd(const TailArgs& a, hipStream_t st);
+int op_tail_bwd(const TailArgs& a, hipStream_t st);
+int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st);

@@ -1,0 +1,213 @@
+"""DSTAGNN model surface, MI355X-native (drop-in for model/DSTAGNN_my.py).
+
+Same class names, constructor signatures, submodule / parameter names (hence
+identical state_dict keys) and construction order (hence the
+identical RNG-driven make_model init, quirk 9) as the reference.  The compute
+of DSTAGNN_block — temporal attention, pre_conv, spatial attention,
+cheb_conv_withSAt, the three GTUs, fcmy, residual and LayerNorms, forward AND
+backward — runs in libdstagnn.so (hand-written gfx950 kernels) through
+DSTAGNNBlockFunction.  There is no CPU/eager fallback: a block called on a
+non-HIP tensor raises.
+
+Differences from the reference that do not change results:
+  * adj_pa and the Chebyshev polynomials are non-persistent buffers (they follow
+    .to(device); state_dict keys are unchanged — quirk 10).
+  * the T x K softmax loop of cheb_conv_withSAt is computed once per k (quirk 3).
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .block_fn import DSTAGNNBlockFunction
+from .graph import cheb_polynomial, scaled_Laplacian
+
+HIP_ONLY = ("dstagnn_drought_amd: DSTAGNN_block runs only on the MI355X HIP path; "
+            "move the model and inputs to a 'cuda' (HIP) device. There is no CPU fallback.")
+
+
+class SScaledDotProductAttention(nn.Module):
+    """Spatial scores Q K^T / sqrt(d_k), no softmax (model/DSTAGNN_my.py:8-22)."""
+
+    def __init__(self, d_k):
+        super().__init__()
+        self.d_k = d_k
+
+
+class ScaledDotProductAttention(nn.Module):
+    """Temporal attention core (model/DSTAGNN_my.py:24-42); executed inside the HIP block."""
+
+    def __init__(self, d_k, num_of_d):
+        super().__init__()
+        self.d_k = d_k
+        self.num_of_d = num_of_d
+
+
+class SMultiHeadAttention(nn.Module):
+    """model/DSTAGNN_my.py:44-67 — parameters W_Q, W_K (d_model -> d_k * n_heads, no bias)."""
+
+    def __init__(self, DEVICE, d_model, d_k, d_v, n_heads):
+        super().__init__()
+        self.d_model, self.d_k, self.d_v, self.n_heads, self.DEVICE = d_model, d_k, d_v, n_heads, DEVICE
+        self.W_Q = nn.Linear(d_model, d_k * n_heads, bias=False)
+        self.W_K = nn.Linear(d_model, d_k * n_heads, bias=False)
+
+
+class MultiHeadAttention(nn.Module):
+    """model/DSTAGNN_my.py:69-100 — W_Q, W_K, W_V, fc and layer_norm over d_model (= N)."""
+
+    def __init__(self, DEVICE, d_model, d_k, d_v, n_heads, num_of_d):
+        super().__init__()
+        self.d_model, self.d_k, self.d_v, self.n_heads, self.num_of_d = d_model, d_k, d_v, n_heads, num_of_d
+        self.DEVICE = DEVICE
+        self.W_Q = nn.Linear(d_model, d_k * n_heads, bias=False)
+        self.W_K = nn.Linear(d_model, d_k * n_heads, bias=False)
+        self.W_V = nn.Linear(d_model, d_v * n_heads, bias=False)
+        self.fc = nn.Linear(n_heads * d_v, d_model, bias=False)
+        self.layer_norm = nn.LayerNorm(self.d_model)
+
+
+class cheb_conv_withSAt(nn.Module):
+    """K-order Chebyshev graph convolution with spatial attention (model/DSTAGNN_my.py:102-133).
+    Parameters Theta.k (in_channels, out_channels) and mask.k (N, N), left uninitialised
+    exactly like the reference (make_model initialises them)."""
+
+    def __init__(self, K, cheb_polynomials, in_channels, out_channels, num_of_vertices, DEVICE):
+        super().__init__()
+        self.K = K
+        self.in_channels, self.out_channels, self.DEVICE = in_channels, out_channels, DEVICE
+        self.Theta = nn.ParameterList([nn.Parameter(torch.empty(in_channels, out_channels)) for _ in range(K)])
+        self.mask = nn.ParameterList([nn.Parameter(torch.empty(num_of_vertices, num_of_vertices)) for _ in range(K)])
+        cp = torch.stack([torch.as_tensor(np.asarray(c), dtype=torch.float32) for c in cheb_polynomials[:K]])
+        self.register_buffer("cheb_stack", cp.contiguous(), persistent=False)
+
+    @property
+    def cheb_polynomials(self):
+        return list(self.cheb_stack.unbind(0))
+
+
+class cheb_conv(nn.Module):
+    """Plain K-order Chebyshev conv (model/DSTAGNN_my.py:135-160).  Never instantiated by
+    DSTAGNN; kept for API completeness (parameters only)."""
+
+    def __init__(self, K, cheb_polynomials, in_channels, out_channels):
+        super().__init__()
+        self.K, self.in_channels, self.out_channels = K, in_channels, out_channels
+        self.Theta = nn.ParameterList([nn.Parameter(torch.empty(in_channels, out_channels)) for _ in range(K)])
+
+
+class Embedding(nn.Module):
+    """Positional embedding + LayerNorm (model/DSTAGNN_my.py:162-182); 'T' over N, 'S' over d_model."""
+
+    def __init__(self, nb_seq, d_Em, num_of_features, Etype, DEVICE):
+        super().__init__()
+        self.nb_seq, self.Etype, self.num_of_features, self.DEVICE = nb_seq, Etype, num_of_features, DEVICE
+        self.pos_embed = nn.Embedding(nb_seq, d_Em)
+        self.norm = nn.LayerNorm(d_Em)
+
+
+class GTU(nn.Module):
+    """Gated temporal unit (model/DSTAGNN_my.py:184-197): Conv2d(C -> 2C, (1,k)), tanh * sigmoid."""
+
+    def __init__(self, in_channels, time_strides, kernel_size):
+        super().__init__()
+        self.in_channels = in_channels
+        self.con2out = nn.Conv2d(in_channels, 2 * in_channels, kernel_size=(1, kernel_size), stride=(1, time_strides))
+
+
+class DSTAGNN_block(nn.Module):
+    """One spatial-temporal block (model/DSTAGNN_my.py:199-253), forward/backward on the HIP path."""
+
+    def __init__(self, DEVICE, num_of_d, in_channels, K, nb_chev_filter, nb_time_filter, time_strides,
+                 cheb_polynomials, adj_pa, adj_TMD, num_of_vertices, num_of_timesteps, d_model, d_k, d_v, n_heads):
+        super().__init__()
+        if time_strides != 1:
+            raise ValueError("time_strides must be 1 (train_DSTAGNN_my.py:93 forces it)")
+        if nb_chev_filter != nb_time_filter:
+            raise ValueError("nb_chev_filter must equal nb_time_filter (GTU consumes the cheb output)")
+        self.sigmoid = nn.Sigmoid()
+        self.tanh = nn.Tanh()
+        self.relu = nn.ReLU(inplace=True)
+        apa = adj_pa.detach().cpu().float() if torch.is_tensor(adj_pa) else torch.as_tensor(np.asarray(adj_pa), dtype=torch.float32)
+        self.register_buffer("adj_pa", apa.contiguous(), persistent=False)
+        self.pre_conv = nn.Conv2d(num_of_timesteps, d_model, kernel_size=(1, num_of_d))
+        self.EmbedT = Embedding(num_of_timesteps, num_of_vertices, num_of_d, "T", DEVICE)
+        self.EmbedS = Embedding(num_of_vertices, d_model, num_of_d, "S", DEVICE)
+        self.TAt = MultiHeadAttention(DEVICE, num_of_vertices, d_k, d_v, n_heads, num_of_d)
+        self.SAt = SMultiHeadAttention(DEVICE, d_model, d_k, d_v, K)
+        self.cheb_conv_SAt = cheb_conv_withSAt(K, cheb_polynomials, in_channels, nb_chev_filter, num_of_vertices,
+                                               DEVICE)
+        self.gtu3 = GTU(nb_time_filter, time_strides, 3)
+        self.gtu5 = GTU(nb_time_filter, time_strides, 5)
+        self.gtu7 = GTU(nb_time_filter, time_strides, 7)
+        self.pooling = nn.MaxPool2d(kernel_size=(1, 2), stride=None, padding=0)  # unused, as in the reference
+        self.residual_conv = nn.Conv2d(in_channels, nb_time_filter, kernel_size=(1, 1), stride=(1, time_strides))
+        self.dropout = nn.Dropout(p=0.05)
+        self.fcmy = nn.Sequential(nn.Linear(3 * num_of_timesteps - 12, num_of_timesteps), nn.Dropout(0.05))
+        self.ln = nn.LayerNorm(nb_time_filter)
+        self.meta = dict(n_heads=n_heads, d_k=d_k, d_v=d_v, d_model=d_model, K=K, C=nb_chev_filter, drop_p=0.05)
+        self.num_of_d = num_of_d
+        self.nb_time_filter = nb_time_filter
+
+    def forward(self, x, res_att):
+        B, N, Fd, T = x.shape
+        if Fd != 1 and Fd != self.nb_time_filter:
+            # reference: RuntimeError at model/DSTAGNN_my.py:252 (quirk 8)
+            raise RuntimeError(f"The size of tensor a ({Fd}) must match the size of tensor b "
+                               f"({self.nb_time_filter}) at non-singleton dimension 1")
+        if x.device.type != "cuda":
+            raise RuntimeError(HIP_ONLY)
+        meta = dict(self.meta)
+        meta["train"] = bool(self.training)
+        meta["seed"] = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
+        names, params = zip(*self.named_parameters())
+        cheb = self.cheb_conv_SAt.cheb_stack
+        return DSTAGNNBlockFunction.apply(meta, names, x.float(), res_att, cheb, self.adj_pa, *params)
+
+
+class DSTAGNN_submodule(nn.Module):
+    """Stack of blocks + final_conv / final_fc (model/DSTAGNN_my.py:255-280)."""
+
+    def __init__(self, DEVICE, num_of_d, nb_block, in_channels, K, nb_chev_filter, nb_time_filter, time_strides,
+                 cheb_polynomials, adj_pa, adj_TMD, num_for_predict, len_input, num_of_vertices, d_model, d_k, d_v,
+                 n_heads):
+        super().__init__()
+        self.BlockList = nn.ModuleList([DSTAGNN_block(DEVICE, num_of_d, in_channels, K, nb_chev_filter,
+                                                      nb_time_filter, time_strides, cheb_polynomials, adj_pa,
+                                                      adj_TMD, num_of_vertices, len_input, d_model, d_k, d_v,
+                                                      n_heads)])
+        self.BlockList.extend([DSTAGNN_block(DEVICE, num_of_d * nb_time_filter, nb_chev_filter, K, nb_chev_filter,
+                                             nb_time_filter, 1, cheb_polynomials, adj_pa, adj_TMD, num_of_vertices,
+                                             len_input // time_strides, d_model, d_k, d_v, n_heads)
+                               for _ in range(nb_block - 1)])
+        self.final_conv = nn.Conv2d(int((len_input / time_strides) * nb_block), 128, kernel_size=(1, nb_time_filter))
+        self.final_fc = nn.Linear(128, num_for_predict)
+        self.DEVICE = DEVICE
+        self.to(DEVICE)
+
+    def forward(self, x):
+        need_concat = []
+        res_att = 0
+        for block in self.BlockList:
+            x, res_att = block(x, res_att)
+            need_concat.append(x)
+        final_x = torch.cat(need_concat, dim=-1)
+        output1 = self.final_conv(final_x.permute(0, 3, 1, 2))[:, :, :, -1].permute(0, 2, 1)
+        return self.final_fc(output1)
+
+
+def make_model(DEVICE, num_of_d, nb_block, in_channels, K, nb_chev_filter, nb_time_filter, time_strides, adj_mx,
+               adj_pa, adj_TMD, num_for_predict, len_input, num_of_vertices, d_model, d_k, d_v, n_heads):
+    """model/DSTAGNN_my.py:282-297: scaled Laplacian + Chebyshev polynomials, then the
+    xavier (dim>1) / U(0,1) (dim<=1, LayerNorm gamma/beta included) initialisation."""
+    L_tilde = scaled_Laplacian(adj_mx)
+    Lt = L_tilde if isinstance(L_tilde, np.ndarray) else L_tilde.cpu().numpy()
+    cheb_polynomials = [torch.from_numpy(np.asarray(c)).type(torch.FloatTensor) for c in cheb_polynomial(Lt, K)]
+    model = DSTAGNN_submodule(DEVICE, num_of_d, nb_block, in_channels, K, nb_chev_filter, nb_time_filter,
+                              time_strides, cheb_polynomials, adj_pa, adj_TMD, num_for_predict, len_input,
+                              num_of_vertices, d_model, d_k, d_v, n_heads)
+    for p in model.parameters():
+        if p.dim() > 1:
+            nn.init.xavier_uniform_(p)
+        else:
+            nn.init.uniform_(p)
+    return model

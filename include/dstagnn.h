@@ -1,0 +1,193 @@
+/*
+ * dstagnn.h — C-ABI of the MI355X-native DSTAGNN block (libdstagnn.so).
+ *
+ * Drop-in boundary for the hot path named by BASELINE.json.north_star:
+ * DSTAGNN_block forward/backward of Ghoul-tn/DSTAGNN_Drought
+ * (model/DSTAGNN_my.py:199-253).  The reference is pure Python/PyTorch with no
+ * FFI; its "operator API" is the nn.Module surface.  The Python package
+ * dstagnn_drought_amd mirrors that surface (make_model / DSTAGNN_block with the
+ * same signatures and state_dict keys) and binds the entry points below through
+ * ctypes.  No torch types cross this boundary: plain device
+ * pointers, sizes and a hipStream_t.
+ *
+ * Conventions
+ *   - All tensors are fp32, contiguous, row-major, device resident (HBM).
+ *   - Every entry point is asynchronous on `stream` and returns 0 on success or a
+ *     positive hipError_t / DSTAGNN_E_* code.  dstagnn_last_error() returns text.
+ *   - Inputs are borrowed read-only; outputs are written (overwritten) in place.
+ *   - No allocation happens inside any entry point: the caller passes a `save`
+ *     buffer (kept from forward to backward) and a `scratch` buffer whose sizes
+ *     come from dstagnn_block_sizes().
+ */
+#ifndef DSTAGNN_H
+#define DSTAGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* dstagnn_stream_t; /* a hipStream_t (0 = default stream) */
+
+#define DSTAGNN_MAX_K 8
+
+enum {
+  DSTAGNN_OK = 0,
+  DSTAGNN_E_SHAPE = 10001,   /* shape / dims mismatch (reference raises RuntimeError)     */
+  DSTAGNN_E_ARG = 10002,     /* null pointer or unsupported argument                      */
+  DSTAGNN_E_SPACE = 10003    /* save / scratch buffer smaller than dstagnn_block_sizes()  */
+};
+
+/* res_att modes (ScaledDotProductAttention.forward, model/DSTAGNN_my.py:37):
+ * 0 = the int 0 passed to the first block (DSTAGNN_submodule.forward:273)
+ * 1 = tensor (B,1,h,T,T) broadcast over F (block 2 receives block 1's re_At)
+ * 2 = tensor (B,F,h,T,T)                                                      */
+enum { DSTAGNN_RES_NONE = 0, DSTAGNN_RES_BCAST = 1, DSTAGNN_RES_FULL = 2 };
+
+/* Shape of one DSTAGNN_block (DSTAGNN_block.__init__, model/DSTAGNN_my.py:200-201).
+ * F = num_of_features of x (1 for the first block, else == C).               */
+typedef struct dstagnn_block_dims {
+  int B, N, F, T;          /* x is (B, N, F, T)                                   */
+  int n_heads, d_k, d_v;   /* temporal attention (TAt)                            */
+  int d_model;             /* D                                                   */
+  int K;                   /* Chebyshev order == SAt heads (quirk 6)              */
+  int C;                   /* nb_chev_filter == nb_time_filter                    */
+  int res_mode;            /* DSTAGNN_RES_*                                       */
+  int train;               /* 1: Dropout(0.05) at :234 and :221 active           */
+  float drop_p;            /* 0.05 in the reference                               */
+  uint64_t seed;           /* dropout RNG seed (counter-based hash, per call)     */
+} dstagnn_block_dims;
+
+/* Parameter pointers in state_dict order.  For the first block
+ * (F==1) residual_conv / EmbedT are used; for inner blocks they are ignored
+ * (their grads stay untouched, matching the reference's None grads, quirk 11). */
+typedef struct dstagnn_block_params {
+  const float* pre_conv_w;   /* (D, T, 1, F)          :207 */
+  const float* pre_conv_b;   /* (D)                        */
+  const float* embT_pos;     /* (T, N)   EmbedT.pos_embed  */
+  const float* embT_g;       /* (N)      EmbedT.norm       */
+  const float* embT_b;       /* (N)                        */
+  const float* embS_pos;     /* (N, D)   EmbedS.pos_embed  */
+  const float* embS_g;       /* (D)                        */
+  const float* embS_b;       /* (D)                        */
+  const float* tat_wq;       /* (h*dk, N) TAt.W_Q          */
+  const float* tat_wk;       /* (h*dk, N)                  */
+  const float* tat_wv;       /* (h*dv, N)                  */
+  const float* tat_fc;       /* (N, h*dv)                  */
+  const float* tat_ln_g;     /* (N)                        */
+  const float* tat_ln_b;     /* (N)                        */
+  const float* sat_wq;       /* (K*dk, D) SAt.W_Q          */
+  const float* sat_wk;       /* (K*dk, D)                  */
+  const float* theta[DSTAGNN_MAX_K]; /* (F, C) cheb_conv_SAt.Theta.k */
+  const float* mask[DSTAGNN_MAX_K];  /* (N, N) cheb_conv_SAt.mask.k  */
+  const float* gtu_w[3];     /* (2C, C, 1, k), k = 3,5,7   */
+  const float* gtu_b[3];     /* (2C)                       */
+  const float* res_w;        /* (C, F, 1, 1) residual_conv */
+  const float* res_b;        /* (C)                        */
+  const float* fcmy_w;       /* (T, 3T-12)                 */
+  const float* fcmy_b;       /* (T)                        */
+  const float* ln_g;         /* (C)                        */
+  const float* ln_b;         /* (C)                        */
+} dstagnn_block_params;
+
+/* Same layout, writable: gradients (overwritten, not accumulated). */
+typedef struct dstagnn_block_grads {
+  float* pre_conv_w; float* pre_conv_b;
+  float* embT_pos; float* embT_g; float* embT_b;
+  float* embS_pos; float* embS_g; float* embS_b;
+  float* tat_wq; float* tat_wk; float* tat_wv; float* tat_fc; float* tat_ln_g; float* tat_ln_b;
+  float* sat_wq; float* sat_wk;
+  float* theta[DSTAGNN_MAX_K]; float* mask[DSTAGNN_MAX_K];
+  float* gtu_w[3]; float* gtu_b[3];
+  float* res_w; float* res_b;
+  float* fcmy_w; float* fcmy_b;
+  float* ln_g; float* ln_b;
+} dstagnn_block_grads;
+
+/* Graph constants of cheb_conv_withSAt (init-time, lib/utils.py:149-203):
+ * cheb = K stacked (N,N) Chebyshev polynomials T_k; adj_pa = (N,N) binary.   */
+typedef struct dstagnn_graph {
+  const float* cheb;     /* (K, N, N) */
+  const float* adj_pa;   /* (N, N)    */
+} dstagnn_graph;
+
+/* Bytes needed for the forward->backward `save` buffer and the per-call scratch. */
+int dstagnn_block_sizes(const dstagnn_block_dims* d, size_t* save_bytes, size_t* scratch_bytes);
+
+/* DSTAGNN_block.forward(x, res_att) -> (x_out, re_At)   (model/DSTAGNN_my.py:225-253)
+ *   x       (B,N,F,T)      res_att  per res_mode (NULL for mode 0)
+ *   out     (B,N,C,T)      re_at    (B,F,h,T,T)  pre-softmax TAt scores (quirk 7)  */
+int dstagnn_block_forward(const dstagnn_block_dims* d, const dstagnn_block_params* p, const dstagnn_graph* g,
+                          const float* x, const float* res_att, float* out, float* re_at,
+                          void* save, size_t save_bytes, void* scratch, size_t scratch_bytes,
+                          dstagnn_stream_t stream);
+
+/* Autograd backward of the block (replaces torch autograd over :225-253).
+ *   d_out (B,N,C,T); d_re_at (B,F,h,T,T) or NULL (no gradient flows into re_At)
+ *   d_x (B,N,F,T) written; d_res_att written per res_mode (NULL for mode 0)
+ *   grads: every pointer used by this block kind is written.                     */
+int dstagnn_block_backward(const dstagnn_block_dims* d, const dstagnn_block_params* p, const dstagnn_graph* g,
+                           const float* x, const float* res_att, const float* d_out, const float* d_re_at,
+                           float* d_x, float* d_res_att, const dstagnn_block_grads* grads,
+                           void* save, size_t save_bytes, void* scratch, size_t scratch_bytes,
+                           dstagnn_stream_t stream);
+
+/* ---- individual hot-path operators (unit-testable pieces of the block) ---- */
+
+/* cheb_conv_withSAt.forward (model/DSTAGNN_my.py:117-133), dense-T_k form.
+ *   x (B,N,F,T); sat (B,K,N,N) spatial-attention scores (pre-softmax);
+ *   theta_cat (F, K*C) = [Theta_0 | ... | Theta_{K-1}]; mask_cat (K,N,N);
+ *   out (B,N,C,T) = ReLU(sum_k (T_k o softmax_i(sat_k + A_pa o M_k))^T x Theta_k)
+ *   save: P, W = T o P (each B*K*N*N) and xTheta (B*N*K*C*T) for the backward.  */
+int dstagnn_cheb_sat_forward(int B, int N, int F, int T, int K, int C,
+                             const float* x, const float* sat, const float* theta_cat, const float* mask_cat,
+                             const float* cheb, const float* adj_pa, float* out,
+                             float* P, float* W, float* xth, void* scratch, size_t scratch_bytes,
+                             dstagnn_stream_t stream);
+/* Backward: d_out (B,N,C,T) -> d_x (B,N,F,T), d_sat (B,K,N,N), d_theta_cat (F,K*C),
+ * d_mask_cat (K,N,N).  `out` is the forward output (ReLU mask).                  */
+int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C,
+                              const float* x, const float* theta_cat, const float* cheb, const float* adj_pa,
+                              const float* out, const float* P, const float* W, const float* xth,
+                              const float* d_out, float* d_x, float* d_sat, float* d_theta_cat, float* d_mask_cat,
+                              void* scratch, size_t scratch_bytes, dstagnn_stream_t stream);
+
+/* Generic strided fp32 GEMM on the f32 MFMA path (v_mfma_f32_32x32x2_f32):
+ *   C(m,n) = alpha * sum_k A(m,k) B(k,n) + beta * C(m,n) + bias[n]   (opt. ReLU)
+ * Every index may be a two-level affine map  off(i) = (i % div)*s0 + (i / div)*s1
+ * (div = 0: off(i) = i*s0), so permuted / im2col views need no copies.          */
+typedef struct dstagnn_idx { int64_t div, s0, s1; } dstagnn_idx;
+typedef struct dstagnn_gemm_desc {
+  int M, N, K, batch;
+  const float* A; dstagnn_idx a_m, a_k, a_z; int64_t a_off;
+  const float* B; dstagnn_idx b_k, b_n, b_z; int64_t b_off;
+  float* C;       dstagnn_idx c_m, c_n, c_z; int64_t c_off;
+  float alpha, beta;
+  const float* bias; int64_t bias_stride;  /* bias[n*bias_stride], may be NULL */
+  int relu;
+} dstagnn_gemm_desc;
+int dstagnn_gemm_f32(const dstagnn_gemm_desc* g, void* scratch, size_t scratch_bytes, dstagnn_stream_t stream);
+
+/* Time `iters` back-to-back launches of one block stage with HIP events on
+ * `stream`; writes the mean per-launch milliseconds.  stage: 0 = whole forward,
+ * 2 = cheb_sat forward stage, 3 = pre_conv stage, 10 = the single kernel the
+ * benchmark reports as dominant (gemm_f32_hot_kernel: the pre_conv fwd GEMM).
+ * Buffers must be those of a preceding dstagnn_block_forward.                  */
+int dstagnn_block_time_stage(const dstagnn_block_dims* d, const dstagnn_block_params* p, const dstagnn_graph* g,
+                             const float* x, const float* res_att, float* out, float* re_at,
+                             void* save, size_t save_bytes, void* scratch, size_t scratch_bytes,
+                             int stage, int iters, float* ms_per_launch, dstagnn_stream_t stream);
+
+/* Dropout keep-mask the block draws (value 1/(1-p) or 0) for tests:
+ * which = 0 (EmbedS output, (B,N,D)), 1 (fcmy output, (B,N,C,T) order of out). */
+int dstagnn_dropout_mask(const dstagnn_block_dims* d, int which, float* mask, dstagnn_stream_t stream);
+
+const char* dstagnn_last_error(void);
+int dstagnn_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSTAGNN_H */

@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU-box driver: run each GPU step under its own time limit; stop at the first
+# fault / abort / timeout (exit codes other than 0 or 1).  Logs in gpurun_out/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1
+run() {
+  local name=$1 to=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "FATAL: $name rc=$rc, stopping"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-pytest,smoke,bench,prof}
+IFS=',' read -ra S <<< "$STEPS"
+for s in "${S[@]}"; do
+  case $s in
+    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    *) echo "unknown step $s" ;;
+  esac
+done

@@ -1,0 +1,293 @@
+"""GPU parity: the HIP path (libdstagnn.so through its C-ABI / the autograd Function)
+against the reference's golden vectors and the CPU oracle.
+
+Tolerance (north_star: "outputs matching the CPU reference within 1e-4 fp32"):
+    max |hip - ref| <= 1e-4 * max(1, max |ref|)      per tensor
+i.e. 1e-4 absolute for O(1) tensors and 1e-4 relative to the tensor's scale for large
+gradients (sums over up to B*N*T terms in a different order than the reference).
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def close(a, b, tol=TOL, what=""):
+    a = a.detach().float().cpu().numpy() if torch.is_tensor(a) else np.asarray(a, np.float32)
+    b = b.detach().float().cpu().numpy() if torch.is_tensor(b) else np.asarray(b, np.float32)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    scale = max(1.0, float(np.abs(b).max()) if b.size else 1.0)
+    err = float(np.abs(a - b).max()) if b.size else 0.0
+    assert err <= tol * scale, f"{what}: max err {err:.3e} > {tol:.0e} * {scale:.3e}"
+
+
+def load(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name), allow_pickle=False))
+
+
+# ---------------------------------------------------------------------------------------
+# generic strided GEMM
+# ---------------------------------------------------------------------------------------
+def _gemm(A, B, C, M, N, K, am, ak, bk, bn, cm, cn, batch=1, az=(0, 0, 0), bz=(0, 0, 0), cz=(0, 0, 0),
+          alpha=1.0, beta=0.0, bias=None, relu=0, scratch_mb=64):
+    from dstagnn_drought_amd import _lib
+    lib = _lib.load()
+    d = _lib.GemmDesc()
+    d.M, d.N, d.K, d.batch = M, N, K, batch
+    d.A, d.B, d.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
+    d.a_m, d.a_k, d.a_z = _lib.idx(*am), _lib.idx(*ak), _lib.idx(*az)
+    d.b_k, d.b_n, d.b_z = _lib.idx(*bk), _lib.idx(*bn), _lib.idx(*bz)
+    d.c_m, d.c_n, d.c_z = _lib.idx(*cm), _lib.idx(*cn), _lib.idx(*cz)
+    d.alpha, d.beta = alpha, beta
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.bias_stride = 1
+    d.relu = relu
+    ws = torch.empty(scratch_mb << 20, dtype=torch.uint8, device="cuda")
+    _lib.check(lib.dstagnn_gemm_f32(ctypes.byref(d), _lib.ptr(ws), ws.numel(), _lib.stream_handle()), "gemm")
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 16), (100, 70, 33), (5440, 512, 384), (300, 96, 20000), (7, 3, 1)])
+def test_gemm_plain(M, N, K):
+    _need_gpu()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = (A.double() @ B.double() + bias.double()).float()
+    C = torch.empty(M, N, device="cuda")
+    _gemm(A.cuda(), B.cuda(), C, M, N, K, (0, K, 0), (0, 1, 0), (0, N, 0), (0, 1, 0), (0, N, 0), (0, 1, 0),
+          bias=bias.cuda())
+    close(C, ref, tol=1e-5 * max(1.0, K ** 0.5), what="plain")
+
+
+def test_gemm_transposed_batched_two_level():
+    """A = x viewed (b,n,f,t) -> rows (b,i,t), k = f (two-level m); C scattered with relu + beta."""
+    _need_gpu()
+    g = torch.Generator().manual_seed(3)
+    Bn, Nn, Fd, T, KC = 3, 17, 5, 12, 9
+    x = torch.randn(Bn, Nn, Fd, T, generator=g)
+    th = torch.randn(Fd, KC, generator=g)
+    C0 = torch.randn(Bn, Nn, KC, T, generator=g)
+    ref = torch.relu(torch.einsum("bift,fk->bikt", x, th) * 0.5 + 2.0 * C0)
+    C = C0.clone().cuda()
+    FT, KCT = Fd * T, KC * T
+    _gemm(x.cuda(), th.cuda(), C, Bn * Nn * T, KC, Fd, (T, 1, FT), (0, T, 0), (0, KC, 0), (0, 1, 0),
+          (T, 1, KCT), (0, T, 0), alpha=0.5, beta=2.0, relu=1)
+    close(C, ref, tol=1e-5, what="two-level")
+    # batched over (b,k) with a two-level batch map: C[b,k] = X[b,:,k*4:(k+1)*4] @ Y[b,:,k*4:(k+1)*4]^T
+    Kh, dk = 3, 4
+    X = torch.randn(Bn, Nn, Kh * dk, generator=g)
+    Y = torch.randn(Bn, Nn, Kh * dk, generator=g)
+    ref2 = torch.einsum("bikd,bjkd->bkij", X.view(Bn, Nn, Kh, dk), Y.view(Bn, Nn, Kh, dk))
+    C2 = torch.empty(Bn, Kh, Nn, Nn, device="cuda")
+    ld = Kh * dk
+    _gemm(X.cuda(), Y.cuda(), C2, Nn, Nn, dk, (0, ld, 0), (0, 1, 0), (0, 1, 0), (0, ld, 0), (0, Nn, 0), (0, 1, 0),
+          batch=Bn * Kh, az=(Kh, dk, Nn * ld), bz=(Kh, dk, Nn * ld), cz=(0, Nn * Nn, 0))
+    close(C2, ref2, tol=1e-5, what="batched")
+
+
+# ---------------------------------------------------------------------------------------
+# cheb_conv_withSAt operator vs the reference's golden vectors
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["g1_cheb_pems04.npz", "g5_cheb_dense.npz"])
+def test_cheb_sat_golden(golden_dir, name):
+    _need_gpu()
+    from dstagnn_drought_amd import _lib
+    lib = _lib.load()
+    g = load(golden_dir, name)
+    m = json.loads(str(g["meta"]))
+    B, N, F, T, K, C = m["B"], m["N"], m["F"], m["T"], m["K"], m["C"]
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    x, sat = cu(g["x"]), cu(g["spatial_attention"])
+    thcat = cu(np.concatenate([g[f"Theta_{k}"] for k in range(K)], axis=1))
+    mcat = cu(np.stack([g[f"mask_{k}"] for k in range(K)]))
+    cheb = cu(np.stack([g[f"cheb_{k}"] for k in range(K)]))
+    apa = cu(g["adj_pa"])
+    out = torch.empty(B, N, C, T, device="cuda")
+    P = torch.empty(B, K, N, N, device="cuda")
+    W = torch.empty_like(P)
+    xth = torch.empty(B, N, K, C, T, device="cuda")
+    ws = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+    st = _lib.stream_handle()
+    pt = _lib.ptr
+    _lib.check(lib.dstagnn_cheb_sat_forward(B, N, F, T, K, C, pt(x), pt(sat), pt(thcat), pt(mcat), pt(cheb), pt(apa),
+                                            pt(out), pt(P), pt(W), pt(xth), pt(ws), ws.numel(), st), "cheb fwd")
+    torch.cuda.synchronize()
+    close(out, g["out"], what="out")
+    dout = cu(g["g_out"])
+    dx = torch.empty_like(x)
+    dsat = torch.empty_like(sat)
+    dth = torch.empty_like(thcat)
+    dm = torch.empty_like(mcat)
+    _lib.check(lib.dstagnn_cheb_sat_backward(B, N, F, T, K, C, pt(x), pt(thcat), pt(cheb), pt(apa), pt(out), pt(P),
+                                             pt(W), pt(xth), pt(dout), pt(dx), pt(dsat), pt(dth), pt(dm), pt(ws),
+                                             ws.numel(), st), "cheb bwd")
+    torch.cuda.synchronize()
+    close(dx, g["grad_x"], what="grad_x")
+    close(dsat, g["grad_spatial_attention"], what="grad_sat")
+    for k in range(K):
+        close(dth[:, k * C:(k + 1) * C], g[f"grad_Theta_{k}"], what=f"grad_Theta_{k}")
+        close(dm[k], g[f"grad_mask_{k}"], what=f"grad_mask_{k}")
+
+
+# ---------------------------------------------------------------------------------------
+# DSTAGNN_block (module + autograd Function) vs golden
+# ---------------------------------------------------------------------------------------
+def _block_from_golden(g, m, num_of_d):
+    import dstagnn_drought_amd as D
+    cheb = [torch.from_numpy(g[f"cheb_{k}"]) for k in range(m["K"])]
+    blk = D.DSTAGNN_block("cpu", num_of_d, num_of_d, m["K"], m["C"], m["C"], 1, cheb, g["adj_pa"], g["adj_tmd"],
+                          m["N"], m["T"], m["D"], m["d_k"], m["d_v"], m["n_heads"])
+    sd = {k[6:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("param/")}
+    blk.load_state_dict(sd)
+    return blk.cuda().eval()
+
+
+@pytest.mark.parametrize("name", ["g2_block_first.npz", "g3_block_inner.npz", "g3b_block_inner_full.npz"])
+def test_block_golden(golden_dir, name):
+    _need_gpu()
+    g = load(golden_dir, name)
+    m = json.loads(str(g["meta"]))
+    blk = _block_from_golden(g, m, m["num_of_d"])
+    x = torch.from_numpy(g["x"]).cuda().requires_grad_(True)
+    res = torch.from_numpy(g["res_att"]).cuda().requires_grad_(True) if "res_att" in g else 0
+    out, re_at = blk(x, res)
+    close(out, g["out"], what="out")
+    close(re_at, g["re_at"], what="re_at")
+    ((out * torch.from_numpy(g["g_out"]).cuda()).sum() + (re_at * torch.from_numpy(g["g_re"]).cuda()).sum()).backward()
+    close(x.grad, g["grad_x"], what="grad_x")
+    if "grad_res_att" in g:
+        close(res.grad, g["grad_res_att"], what="grad_res_att")
+    for n, p in blk.named_parameters():
+        if "grad/" + n in g:
+            assert p.grad is not None, n
+            close(p.grad, g["grad/" + n], what=n)
+        else:
+            assert p.grad is None, f"{n} should keep grad None (quirk 11)"
+
+
+def test_model_golden(golden_dir):
+    _need_gpu()
+    import dstagnn_drought_amd as D
+    g = load(golden_dir, "g4_model.npz")
+    m = json.loads(str(g["meta"]))
+    torch.manual_seed(0)
+    model = D.make_model("cpu", 1, m["nb_block"], 1, m["K"], m["C"], m["C"], 1, torch.FloatTensor(g["adj_tmd"]),
+                         torch.FloatTensor(g["adj_pa"]), torch.FloatTensor(g["adj_tmd"]), m["num_for_predict"],
+                         m["T"], m["N"], m["D"], m["d_k"], m["d_k"], m["n_heads"])
+    model.load_state_dict({k[6:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("param/")})
+    cheb = torch.from_numpy(np.stack([g[f"cheb_{k}"] for k in range(m["K"])]))
+    for b in model.BlockList:  # pin the reference's ARPACK lambda_max exactly
+        b.cheb_conv_SAt.cheb_stack.copy_(cheb)
+    model = model.cuda().eval()
+    x = torch.from_numpy(g["x"]).cuda().requires_grad_(True)
+    out = model(x)
+    close(out, g["out"], what="out")
+    loss = torch.nn.SmoothL1Loss()(out, torch.from_numpy(g["target"]).cuda())
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    loss.backward()
+    close(x.grad, g["grad_x"], what="grad_x")
+    for n, p in model.named_parameters():
+        if bool(g["hasgrad/" + n]):
+            close(p.grad, g["grad/" + n], what=n)
+        else:
+            assert p.grad is None, n
+
+
+# ---------------------------------------------------------------------------------------
+# larger shapes vs the CPU oracle (PEMS08 geometry, small batch)
+# ---------------------------------------------------------------------------------------
+def _oracle_case(B, N, T, K, h, D, dk, C, first, res_kind, seed, train=False):
+    from oracle import dstagnn_ref as ref
+    import dstagnn_drought_amd as D_
+    gen = torch.Generator().manual_seed(seed)
+    rs = np.random.RandomState(seed)
+    tmd = np.eye(N)
+    pa = np.zeros((N, N))
+    for i in range(N):
+        tmd[i, rs.choice(N, 2, replace=False)] = 1.0
+        pa[i, rs.choice(N, 4, replace=False)] = 1.0
+    Lt = D_.scaled_Laplacian(tmd)
+    cheb = [torch.from_numpy(c).float() for c in D_.cheb_polynomial(Lt, K)][:K]
+    F = 1 if first else C
+    p = ref.random_block_params(gen, F, F, K, C, N, T, D, dk, dk, h)
+    x = torch.randn(B, N, F, T, generator=gen)
+    if res_kind == 0:
+        res = 0
+    else:
+        res = torch.randn(B, 1 if res_kind == 1 else F, h, T, T, generator=gen)
+    return ref, p, x, res, cheb, torch.from_numpy(pa).float(), dict(n_heads=h, d_k=dk, d_v=dk, K=K), gen
+
+
+@pytest.mark.parametrize("first,res_kind", [(False, 1), (True, 0), (False, 2)])
+def test_block_vs_oracle_pems08_geometry(first, res_kind):
+    _need_gpu()
+    import dstagnn_drought_amd as D_
+    B, N, T, K, h, D, dk, C = 2, 170, 12, 3, 3, 512, 32, 32
+    ref, p, x, res, cheb, apa, dims, gen = _oracle_case(B, N, T, K, h, D, dk, C, first, res_kind, seed=7)
+    g_out = torch.randn(B, N, C, T, generator=gen)
+    g_re = torch.randn(B, x.shape[2], h, T, T, generator=gen)
+    out_r, re_r, gx_r, gra_r, grads_r = ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re)
+    F = x.shape[2]
+    blk = D_.DSTAGNN_block("cpu", F, F, K, C, C, 1, cheb, apa, apa, N, T, D, dk, dk, h)
+    blk.load_state_dict(p)
+    blk = blk.cuda().eval()
+    xg = x.cuda().requires_grad_(True)
+    rg = res.cuda().requires_grad_(True) if torch.is_tensor(res) else 0
+    out, re_at = blk(xg, rg)
+    close(out, out_r, what="out")
+    close(re_at, re_r, what="re_at")
+    ((out * g_out.cuda()).sum() + (re_at * g_re.cuda()).sum()).backward()
+    close(xg.grad, gx_r, what="grad_x")
+    if torch.is_tensor(res):
+        close(rg.grad, gra_r, what="grad_res_att")
+    for n, prm in blk.named_parameters():
+        if grads_r[n] is None:
+            assert prm.grad is None, n
+        else:
+            close(prm.grad, grads_r[n], what=n)
+
+
+def test_block_train_mode_dropout_vs_oracle():
+    """Train mode: both Dropout(0.05) active; the oracle gets the exact masks the HIP path drew."""
+    _need_gpu()
+    import dstagnn_drought_amd as D_
+    from dstagnn_drought_amd.block_fn import dropout_masks
+    B, N, T, K, h, D, dk, C = 2, 40, 12, 3, 3, 64, 16, 32
+    ref, p, x, res, cheb, apa, dims, gen = _oracle_case(B, N, T, K, h, D, dk, C, False, 1, seed=11)
+    blk = D_.DSTAGNN_block("cpu", C, C, K, C, C, 1, cheb, apa, apa, N, T, D, dk, dk, h)
+    blk.load_state_dict(p)
+    blk = blk.cuda().train()
+    torch.manual_seed(1234)
+    xg = x.cuda().requires_grad_(True)
+    out, re_at = blk(xg, res.cuda())
+    torch.manual_seed(1234)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    m0, m1 = dropout_masks(blk.meta, x.shape, seed)
+    keep = float((m0 > 0).float().mean())
+    assert 0.93 < keep < 0.97, keep  # p = 0.05
+    pp = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    xx = x.clone().requires_grad_(True)
+    out_r, re_r = ref.block_forward(pp, xx, res, cheb, apa, dims, train=True,
+                                    drop_masks=(m0.cpu(), m1.cpu().permute(0, 2, 1, 3)), hoist=True)
+    close(out, out_r, what="out(train)")
+    g_out = torch.randn(out.shape, generator=gen)
+    (out * g_out.cuda()).sum().backward()
+    (out_r * g_out).sum().backward()
+    close(xg.grad, xx.grad, what="grad_x(train)")
+    for n, prm in blk.named_parameters():
+        if pp[n].grad is not None:
+            close(prm.grad, pp[n].grad, what=n + "(train)")

@@ -31,10 +31,10 @@ def close(a, b, **kw):
 def test_laplacian_cheb_pems04(golden_dir):
     g = load(golden_dir, "g6_laplacian_pems04.npz")
     Lt = ref.scaled_laplacian(T(g["adj_tmd"]))
-    close(Lt, g["L_tilde"], rtol=1e-5, atol=1e-6)
+    close(Lt, g["L_tilde"], rtol=1e-4, atol=1e-5)  # ARPACK random v0: ~1e-5 run-to-run
     cps = ref.cheb_polynomials(Lt.numpy(), 3)
     for k in range(3):
-        close(cps[k].astype(np.float32), g[f"cheb_{k}"], rtol=1e-5, atol=1e-6)
+        close(cps[k].astype(np.float32), g[f"cheb_{k}"], rtol=1e-4, atol=1e-5)
     # quirk 4: elementwise recurrence keeps the support of L~ u I
     supp = (g["L_tilde"] != 0) | np.eye(307, dtype=bool)
     assert np.all((g["cheb_2"] != 0) <= supp)
