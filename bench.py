@@ -70,11 +70,29 @@ def algorithmic_flops_per_sample(c=CFG):
     return 3 * fwd
 
 
+def host_cores():
+    """CPU share of this process: the GPU box exposes the whole machine in os.cpu_count()
+    but grants ~16 cores per GPU (OMP_NUM_THREADS); use the smallest of the three."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(budget_s=12.0):
     """Oracle (literal restatement of the reference loops) on this host's cores."""
     from oracle import dstagnn_ref as ref
     c = CFG
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(host_cores())
     threads = torch.get_num_threads()
     gen = torch.Generator().manual_seed(0)
     tmd, pa = synth_graph(c["N"])
@@ -122,7 +140,6 @@ def main():
 
     from dstagnn_drought_amd import _lib
     from dstagnn_drought_amd.block_fn import make_dims, workspace_sizes, _fill
-    import dstagnn_drought_amd.block_fn as bf
 
     blk, cheb, apa = build_block(dev)
     c = CFG
@@ -133,23 +150,20 @@ def main():
     g_out = torch.randn(B, c["N"], c["C"], c["T"], device=dev, generator=gen)
     g_re = torch.randn(B, c["C"], c["n_heads"], c["T"], c["T"], device=dev, generator=gen)
     params = [p for p in blk.parameters()]
+    reducer = None
+    if world > 1:
+        from dstagnn_drought_amd.dp import GradAllReducer, mask_support_of
+        reducer = GradAllReducer(blk.named_parameters(), mask_support=mask_support_of(blk))
 
     def step():
         for p in params:
             p.grad = None
         out, re_at = blk(x, res)
         torch.autograd.backward([out, re_at], [g_out, g_re])
-        if world > 1:
-            grads = [p.grad for p in params if p.grad is not None]
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            dist.all_reduce(flat)
-            flat.div_(world)
-            off = 0
-            for g in grads:
-                n = g.numel()
-                g.copy_(flat[off:off + n].view_as(g))
-                off += n
+        if reducer is not None:  # the DP exchange step: bucketed RCCL all-reduce (mean)
+            reducer.all_reduce()
 
+    log(f"rank {rank}/{world}: block built, warmup {args.warmup}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -169,6 +183,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
+    log(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step")
     value = world * B * args.steps / elapsed
 
     # ---- dominant kernel: the pre_conv fwd GEMM (gemm_f32_hot_kernel), HIP events on its stream
@@ -206,8 +221,10 @@ def main():
             "kernel": "gemm_f32_hot_kernel (pre_conv fwd GEMM %dx%dx%d)" % (M, Nn, Kk),
             "avg_launch_us": round(hot_ms * 1e3, 3)}
 
+    log(f"hot kernel {hot_ms * 1e3:.2f} us/launch")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log(f"cpu baseline on {host_cores()} threads")
         cpu = cpu_baseline()
 
     if rank == 0:

@@ -89,8 +89,8 @@ def load():
                                   _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp],
         "dstagnn_block_backward": [P(BlockDims), P(BlockParams), P(Graph), _vp, _vp, _vp, _vp, _vp, _vp,
                                    P(BlockGrads), _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp],
-        "dstagnn_cheb_sat_forward": [ctypes.c_int] * 6 + [_vp] * 10 + [ctypes.c_size_t, _vp],
-        "dstagnn_cheb_sat_backward": [ctypes.c_int] * 6 + [_vp] * 13 + [ctypes.c_size_t, _vp],
+        "dstagnn_cheb_sat_forward": [ctypes.c_int] * 6 + [_vp] * 11 + [ctypes.c_size_t, _vp],
+        "dstagnn_cheb_sat_backward": [ctypes.c_int] * 6 + [_vp] * 14 + [ctypes.c_size_t, _vp],
         "dstagnn_gemm_f32": [P(GemmDesc), _vp, ctypes.c_size_t, _vp],
         "dstagnn_block_time_stage": [P(BlockDims), P(BlockParams), P(Graph), _vp, _vp, _vp, _vp,
                                      _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
