@@ -275,21 +275,16 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
 }
 
 int pack_theta(const float* const* theta, int K, int F, int C, float* thcat, hipStream_t st) {
-  for (int k = 0; k < K; ++k) {
-    hipError_t e = hipMemcpy2DAsync(thcat + (int64_t)k * C, sizeof(float) * K * C, theta[k], sizeof(float) * C,
-                                    sizeof(float) * C, F, hipMemcpyDeviceToDevice, st);
-    if (e != hipSuccess) { set_last_error(std::string("pack_theta: ") + hipGetErrorString(e)); return (int)e; }
-  }
-  return 0;
+  PackTheta a;
+  a.K = K; a.F = F; a.C = C; a.unpack = 0; a.cat_out = thcat;
+  for (int k = 0; k < K; ++k) a.src[k] = theta[k];
+  return op_pack_theta(a, st);
 }
 int unpack_theta(const float* thcat, int K, int F, int C, float* const* dtheta, hipStream_t st) {
-  for (int k = 0; k < K; ++k) {
-    if (!dtheta[k]) continue;
-    hipError_t e = hipMemcpy2DAsync(dtheta[k], sizeof(float) * C, thcat + (int64_t)k * C, sizeof(float) * K * C,
-                                    sizeof(float) * C, F, hipMemcpyDeviceToDevice, st);
-    if (e != hipSuccess) { set_last_error(std::string("unpack_theta: ") + hipGetErrorString(e)); return (int)e; }
-  }
-  return 0;
+  PackTheta a;
+  a.K = K; a.F = F; a.C = C; a.unpack = 1; a.cat_in = thcat;
+  for (int k = 0; k < K; ++k) a.dst[k] = dtheta[k];
+  return op_pack_theta(a, st);
 }
 
 // ------------------------------------------------------------------------------

@@ -277,31 +277,66 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
 // =====================================================================================
 // reductions
 // =====================================================================================
-// stage 1: in viewed as (A, E) (E = O*I contiguous per a).  part[p][e] = sum over the
-// p-th chunk of a of in[a][e] (* in2[a][e]).
+// stage 1: in viewed as (A, E) rows (E = O*I contiguous per row a).
+// part[p][e] = sum over the p-th chunk of rows of in[a][e] (* in2[a][e]).
+// E <= 256: the block is R' = 256/E row-lanes x E columns (consecutive threads read
+// consecutive addresses), combined through LDS; E > 256: threads stride over e.
 __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ in, const float* __restrict__ in2,
                                                      int64_t A, int E, int64_t achunk, float* __restrict__ part) {
-  const int p = blockIdx.y;
+  __shared__ float red[256];
+  const int p = blockIdx.x;
   const int64_t a0 = (int64_t)p * achunk, a1 = min(A, a0 + achunk);
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+  const int t = threadIdx.x;
+  if (E <= 256) {
+    const int R = 256 / E;
+    const int r = t / E, e = t % E;
     float s = 0.f;
-    for (int64_t aa = a0; aa < a1; ++aa) {
-      float v = in[aa * E + e];
-      if (in2) v *= in2[aa * E + e];
-      s += v;
+    if (r < R) {
+      for (int64_t aa = a0 + r; aa < a1; aa += R) {
+        float v = in[aa * E + e];
+        if (in2) v *= in2[aa * E + e];
+        s += v;
+      }
     }
-    part[(int64_t)p * E + e] = s;
+    red[t] = s;
+    __syncthreads();
+    if (t < E) {
+      float tot = 0.f;
+      for (int q = 0; q < R; ++q) tot += red[q * E + t];
+      part[(int64_t)p * E + t] = tot;
+    }
+  } else {
+    for (int e = t; e < E; e += 256) {
+      float s = 0.f;
+      for (int64_t aa = a0; aa < a1; ++aa) {
+        float v = in[aa * E + e];
+        if (in2) v *= in2[aa * E + e];
+        s += v;
+      }
+      part[(int64_t)p * E + e] = s;
+    }
   }
 }
-// stage 2: out[o] = beta*out[o] + sum_p sum_i part[p][o*I + i]
+// stage 2: one workgroup per output o: out[o] = beta*out[o] + sum_p sum_i part[p][o*I + i]
 __global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int P, int O, int I,
                                                      float* __restrict__ out, int64_t ostride, float beta) {
-  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int p = 0; p < P; ++p)
-      for (int i = 0; i < I; ++i) s += part[((int64_t)p * O + o) * I + i];
+  __shared__ float red[256];
+  const int o = blockIdx.x;
+  float s = 0.f;
+  const int n = P * I;
+  for (int q = threadIdx.x; q < n; q += 256) {
+    const int pp = q / I, i = q % I;
+    s += part[((int64_t)pp * O + o) * I + i];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
     float* d = out + (int64_t)o * ostride;
-    *d = (beta != 0.f ? beta * *d : 0.f) + s;
+    *d = (beta != 0.f ? beta * *d : 0.f) + red[0];
   }
 }
 
@@ -328,8 +363,10 @@ __global__ __launch_bounds__(256) void relu_mask_kernel(const float* __restrict_
 // Chebyshev spatial-attention softmax (column softmax over source node i)
 // grid (ceil(N/64), B*K), block 256 = 64 columns x 4 row groups
 // =====================================================================================
-__global__ __launch_bounds__(256) void cheb_softmax_fwd_kernel(ChebSm a) {
-  __shared__ float sm_m[4][64], sm_l[4][64];
+constexpr int kSmG = 8;  // row groups per workgroup (64 columns x 8 groups = 512 threads)
+
+__global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
+  __shared__ float sm_m[kSmG][64], sm_l[kSmG][64];
   const int N = a.N;
   const int bk = blockIdx.y;
   const int k = bk % a.K;
@@ -340,28 +377,32 @@ __global__ __launch_bounds__(256) void cheb_softmax_fwd_kernel(ChebSm a) {
   const float* Tk = a.cheb + (int64_t)k * N * N;
   float m = -INFINITY, l = 0.f;
   if (j < N) {
-    for (int i = g; i < N; i += 4) {
-      int64_t o = (int64_t)i * N + j;
-      float z = S[o] + a.apa[o] * Mk[o];
-      float mn = fmaxf(m, z);
-      l = l * expf(m - mn) + expf(z - mn);
+#pragma unroll 2
+    for (int i = g; i < N; i += kSmG) {
+      const int64_t o = (int64_t)i * N + j;
+      const float z = S[o] + a.apa[o] * Mk[o];
+      const float mn = fmaxf(m, z);
+      l = l * __expf(m - mn) + __expf(z - mn);
       m = mn;
     }
   }
   sm_m[g][cj] = m; sm_l[g][cj] = l;
   __syncthreads();
   float M = sm_m[0][cj];
-  for (int q = 1; q < 4; ++q) M = fmaxf(M, sm_m[q][cj]);
+#pragma unroll
+  for (int q = 1; q < kSmG; ++q) M = fmaxf(M, sm_m[q][cj]);
   float L = 0.f;
-  for (int q = 0; q < 4; ++q) L += sm_l[q][cj] * expf(sm_m[q][cj] - M);
+#pragma unroll
+  for (int q = 0; q < kSmG; ++q) L += sm_l[q][cj] * __expf(sm_m[q][cj] - M);
   const float inv = 1.f / L;
   if (j < N) {
     float* P = a.P + (int64_t)bk * N * N;
     float* W = a.W + (int64_t)bk * N * N;
-    for (int i = g; i < N; i += 4) {
-      int64_t o = (int64_t)i * N + j;
-      float z = S[o] + a.apa[o] * Mk[o];
-      float p = expf(z - M) * inv;
+#pragma unroll 2
+    for (int i = g; i < N; i += kSmG) {
+      const int64_t o = (int64_t)i * N + j;
+      const float z = S[o] + a.apa[o] * Mk[o];
+      const float p = __expf(z - M) * inv;
       P[o] = p;
       W[o] = Tk[o] * p;
     }
@@ -369,8 +410,8 @@ __global__ __launch_bounds__(256) void cheb_softmax_fwd_kernel(ChebSm a) {
 }
 
 // dz = P * (T*dW - sum_i P*T*dW)   written to dz (may alias dW)
-__global__ __launch_bounds__(256) void cheb_softmax_bwd_kernel(ChebSm a) {
-  __shared__ float sm_c[4][64];
+__global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
+  __shared__ float sm_c[kSmG][64];
   const int N = a.N;
   const int bk = blockIdx.y;
   const int k = bk % a.K;
@@ -381,17 +422,21 @@ __global__ __launch_bounds__(256) void cheb_softmax_bwd_kernel(ChebSm a) {
   const float* Tk = a.cheb + (int64_t)k * N * N;
   float c = 0.f;
   if (j < N)
-    for (int i = g; i < N; i += 4) {
-      int64_t o = (int64_t)i * N + j;
+#pragma unroll 2
+    for (int i = g; i < N; i += kSmG) {
+      const int64_t o = (int64_t)i * N + j;
       c += P[o] * Tk[o] * dW[o];
     }
   sm_c[g][cj] = c;
   __syncthreads();
-  c = sm_c[0][cj] + sm_c[1][cj] + sm_c[2][cj] + sm_c[3][cj];
+  c = 0.f;
+#pragma unroll
+  for (int q = 0; q < kSmG; ++q) c += sm_c[q][cj];
   if (j < N) {
     float* dz = a.dz + (int64_t)bk * N * N;
-    for (int i = g; i < N; i += 4) {
-      int64_t o = (int64_t)i * N + j;
+#pragma unroll 2
+    for (int i = g; i < N; i += kSmG) {
+      const int64_t o = (int64_t)i * N + j;
       dz[o] = P[o] * (Tk[o] * dW[o] - c);
     }
   }
@@ -464,84 +509,116 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a, int gi) {
 // =====================================================================================
 // block tail: fcmy dropout, residual, ReLUs and LN over C (one thread per (b,n,t) row)
 // =====================================================================================
+// one workgroup per node (b,n): its C*T elements are contiguous in (B,N,C,T), so every
+// pass is a coalesced sweep; the LN over C (stride T) goes through LDS.
+constexpr int kTailMaxCT = 4096, kTailMaxT = 256;
+
 __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
-  const int C = a.C, T = a.T;
-  const int64_t R = (int64_t)a.BN * T;
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < R; row += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t bn = row / T;
-    const int t = (int)(row % T);
-    const int64_t base = bn * C * T + t;
-    float sum = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const int64_t o = base + (int64_t)c * T;
-      float tc = a.tc[o];
-      if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
-      float tco, xres;
-      if (a.first) {
-        tco = fmaxf(tc, 0.f);
-        xres = a.res_w[c] * a.x[bn * T + t] + a.res_b[c];
-      } else {
-        tco = fmaxf(a.X[o] + tc, 0.f);
-        xres = a.x[o];
-      }
-      float r = fmaxf(xres + tco, 0.f);
-      a.tco[o] = tco;
-      a.r[o] = r;
-      sum += r;
+  __shared__ float rl[kTailMaxCT];
+  __shared__ float mus[kTailMaxT], rss[kTailMaxT];
+  const int C = a.C, T = a.T, CT = C * T;
+  const int64_t bn = blockIdx.x;
+  const int64_t base = bn * CT;
+  for (int e = threadIdx.x; e < CT; e += 256) {
+    const int c = e / T, t = e - (e / T) * T;
+    const int64_t o = base + e;
+    float tc = a.tc[o];
+    if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
+    float tco, xres;
+    if (a.first) {
+      tco = fmaxf(tc, 0.f);
+      xres = a.res_w[c] * a.x[bn * T + t] + a.res_b[c];
+    } else {
+      tco = fmaxf(a.X[o] + tc, 0.f);
+      xres = a.x[o];
     }
+    const float r = fmaxf(xres + tco, 0.f);
+    a.tco[o] = tco;
+    a.r[o] = r;
+    rl[e] = r;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += 256) {
+    float sum = 0.f;
+    for (int c = 0; c < C; ++c) sum += rl[c * T + t];
     const float mean = sum / C;
     float var = 0.f;
-    for (int c = 0; c < C; ++c) { float d = a.r[base + (int64_t)c * T] - mean; var += d * d; }
-    var /= C;
-    const float rs = rsqrtf(var + 1e-5f);
-    a.mu[row] = mean; a.rs[row] = rs;
-    for (int c = 0; c < C; ++c) {
-      const int64_t o = base + (int64_t)c * T;
-      a.out[o] = (a.r[o] - mean) * rs * a.ln_g[c] + a.ln_b[c];
-    }
+    for (int c = 0; c < C; ++c) { const float d = rl[c * T + t] - mean; var += d * d; }
+    const float rs = rsqrtf(var / C + 1e-5f);
+    mus[t] = mean; rss[t] = rs;
+    a.mu[bn * T + t] = mean; a.rs[bn * T + t] = rs;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < CT; e += 256) {
+    const int c = e / T, t = e - (e / T) * T;
+    a.out[base + e] = (rl[e] - mus[t]) * rss[t] * a.ln_g[c] + a.ln_b[c];
   }
 }
 
 __global__ __launch_bounds__(256) void tail_bwd_kernel(TailArgs a) {
-  const int C = a.C, T = a.T;
-  const int64_t R = (int64_t)a.BN * T;
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < R; row += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t bn = row / T;
-    const int t = (int)(row % T);
-    const int64_t base = bn * C * T + t;
-    const float mean = a.mu[row], rs = a.rs[row];
+  __shared__ float dxh[kTailMaxCT], xhl[kTailMaxCT];
+  __shared__ float s1s[kTailMaxT], s2s[kTailMaxT];
+  const int C = a.C, T = a.T, CT = C * T;
+  const int64_t bn = blockIdx.x;
+  const int64_t base = bn * CT;
+  const float* mu = a.mu + bn * T;
+  const float* rsv = a.rs + bn * T;
+  for (int e = threadIdx.x; e < CT; e += 256) {
+    const int c = e / T, t = e - (e / T) * T;
+    const int64_t o = base + e;
+    const float dy = a.dout[o];
+    const float xh = (a.r[o] - mu[t]) * rsv[t];
+    xhl[e] = xh;
+    dxh[e] = dy * a.ln_g[c];
+    a.gcontrib[o] = dy * xh;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += 256) {
     float s1 = 0.f, s2 = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const int64_t o = base + (int64_t)c * T;
-      float dy = a.dout[o];
-      float xh = (a.r[o] - mean) * rs;
-      float dxh = dy * a.ln_g[c];
-      s1 += dxh; s2 += dxh * xh;
-      a.gcontrib[o] = dy * xh;
+    for (int c = 0; c < C; ++c) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
+    s1s[t] = s1 / C; s2s[t] = s2 / C;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < CT; e += 256) {
+    const int t = e - (e / T) * T;
+    const int64_t o = base + e;
+    float dr = rsv[t] * (dxh[e] - s1s[t] - xhl[e] * s2s[t]);
+    dr = a.r[o] > 0.f ? dr : 0.f;                    // relu(xres + tco)
+    const float dtco = a.tco[o] > 0.f ? dr : 0.f;      // tco = relu(...)
+    float dtc = dtco;
+    if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
+    a.dtc[o] = dtc;
+    if (a.first) {
+      a.dX[o] = 0.f;
+      a.rcontrib[o] = dr * a.x[bn * T + t];  // d residual_conv.weight contributions
+      a.dres[o] = dr;                         // d residual_conv.bias contributions
+      dxh[e] = dr;                            // reuse LDS for the channel reduction below
+    } else {
+      a.dX[o] = dtco;
+      a.dx[o] = dr;
     }
-    s1 /= C; s2 /= C;
-    float dxsum = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const int64_t o = base + (int64_t)c * T;
-      float ro = a.r[o];
-      float xh = (ro - mean) * rs;
-      float dr = rs * (a.dout[o] * a.ln_g[c] - s1 - xh * s2);
-      dr = ro > 0.f ? dr : 0.f;                       // relu(xres + tco)
-      float dtco = a.tco[o] > 0.f ? dr : 0.f;          // tco = relu(...)
-      float dtc = dtco;
-      if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
-      a.dtc[o] = dtc;
-      if (a.first) {
-        a.dX[o] = 0.f;
-        a.rcontrib[o] = dr * a.x[bn * T + t];   // d residual_conv.weight contributions
-        a.dres[o] = dr;                          // d residual_conv.bias contributions
-        dxsum += a.res_w[c] * dr;
-      } else {
-        a.dX[o] = dtco;
-        a.dx[o] = dr;
-      }
+  }
+  if (a.first) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += 256) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += a.res_w[c] * dxh[c * T + t];
+      a.dx[bn * T + t] = s;
     }
-    if (a.first) a.dx[bn * T + t] = dxsum;
+  }
+}
+
+// thcat[f][k*C + c] = theta_k[f][c]   (and the inverse for the gradients)
+__global__ __launch_bounds__(256) void pack_theta_kernel(PackTheta a) {
+  const int total = a.K * a.F * a.C;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % a.C, r = i / a.C, f = r % a.F, k = r / a.F;
+    const int64_t cat = (int64_t)f * a.K * a.C + (int64_t)k * a.C + c;
+    if (a.unpack) {
+      if (a.dst[k]) a.dst[k][(int64_t)f * a.C + c] = a.cat_in[cat];
+    } else {
+      a.cat_out[cat] = a.src[k][(int64_t)f * a.C + c];
+    }
   }
 }
 
@@ -633,14 +710,16 @@ int op_ln_bwd(const LnBwd& a, hipStream_t st) {
 int op_colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
               float* part, size_t part_floats, hipStream_t st) {
   const int E = O * I;
-  int P = (int)std::min<int64_t>(256, std::max<int64_t>(1, A / 64));
+  // ~16K elements per stage-1 workgroup, at most 1024 partial rows
+  int64_t P = std::max<int64_t>(1, std::min<int64_t>(1024, cdiv64(A * E, 16384)));
+  P = std::min<int64_t>(P, A);
   while (P > 1 && (size_t)P * E > part_floats) P /= 2;
   if ((size_t)P * E > part_floats) { set_last_error("colsum: scratch too small"); return DSTAGNN_E_SPACE; }
   const int64_t achunk = cdiv64(A, P);
-  dim3 g1((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv64(E, 256), 64)), (unsigned)P);
-  hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, st, in, in2, A, E, achunk, part);
+  P = cdiv64(A, achunk);
+  hipLaunchKernelGGL(colsum_stage1, dim3((unsigned)P), dim3(256), 0, st, in, in2, A, E, achunk, part);
   DS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_stage2, dim3(grid1d(O)), dim3(256), 0, st, part, P, O, I, out, ostride, beta);
+  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)O), dim3(256), 0, st, part, (int)P, O, I, out, ostride, beta);
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -659,13 +738,13 @@ int op_relu_mask(const float* g, const float* y, float* out, int64_t n, hipStrea
 
 int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st) {
   dim3 grid((unsigned)cdiv64(a.N, 64), (unsigned)(a.B * a.K));
-  hipLaunchKernelGGL(cheb_softmax_fwd_kernel, grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(cheb_softmax_fwd_kernel, grid, dim3(64 * kSmG), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st) {
   dim3 grid((unsigned)cdiv64(a.N, 64), (unsigned)(a.B * a.K));
-  hipLaunchKernelGGL(cheb_softmax_bwd_kernel, grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(cheb_softmax_bwd_kernel, grid, dim3(64 * kSmG), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -691,18 +770,26 @@ int op_gate_bwd(const GateArgs& a, hipStream_t st) {
 }
 
 int op_tail_fwd(const TailArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(tail_fwd_kernel, dim3(grid1d((int64_t)a.BN * a.T)), dim3(256), 0, st, a);
+  if (a.C * a.T > kTailMaxCT || a.T > kTailMaxT) { set_last_error("tail: C*T too large"); return DSTAGNN_E_SHAPE; }
+  hipLaunchKernelGGL(tail_fwd_kernel, dim3((unsigned)a.BN), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_tail_bwd(const TailArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(tail_bwd_kernel, dim3(grid1d((int64_t)a.BN * a.T)), dim3(256), 0, st, a);
+  if (a.C * a.T > kTailMaxCT || a.T > kTailMaxT) { set_last_error("tail: C*T too large"); return DSTAGNN_E_SHAPE; }
+  hipLaunchKernelGGL(tail_bwd_kernel, dim3((unsigned)a.BN), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 
 int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st) {
   hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid1d(n)), dim3(256), 0, st, out, n, seed, which, p);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_pack_theta(const PackTheta& a, hipStream_t st) {
+  hipLaunchKernelGGL(pack_theta_kernel, dim3(grid1d((int64_t)a.K * a.F * a.C, 256)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -69,6 +69,15 @@ struct TailArgs {
   float* rcontrib = nullptr; float* dres = nullptr;  // first block residual_conv grads
 };
 
+struct PackTheta {
+  int K = 0, F = 0, C = 0, unpack = 0;
+  const float* src[DSTAGNN_MAX_K] = {};   // pack: K x (F,C)
+  float* cat_out = nullptr;               // pack: (F, K*C)
+  const float* cat_in = nullptr;          // unpack: (F, K*C)
+  float* dst[DSTAGNN_MAX_K] = {};         // unpack: K x (F,C) (null entries skipped)
+};
+
+int op_pack_theta(const PackTheta& a, hipStream_t st);
 int op_transpose(const float* in, float* out, int R, int Cc, int batch, int64_t in_bs, int64_t out_bs, float beta,
                  hipStream_t st);
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
