@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/dstagnn.h"
@@ -61,6 +62,37 @@ __device__ __forceinline__ int64_t ioff(const Idx2& m, uint32_t i) {
   uint32_t q = fdiv(i, m.f);
   uint32_t r = i - q * m.f.d;
   return (int64_t)r * m.s0 + (int64_t)q * m.s1;
+}
+
+// Branch-free 32-bit variant for the inner (k) loop of the GEMM: a single-level map is
+// encoded with d = 2^31 so q = 0 for every valid index; offsets are int32 (the host
+// checks the range), so no 64-bit multiplies and no control flow between the loads.
+struct KIdx {
+  uint32_t d = 0x80000000u, m = 1, s = 31;
+  int32_t s0 = 0, s1 = 0;
+};
+
+inline bool make_kidx(const Idx2& x, int64_t K, KIdx* out) {
+  KIdx k;
+  int64_t maxoff;
+  if (x.two) {
+    k.d = x.f.d; k.m = x.f.m; k.s = x.f.s;
+    int64_t nq = K > 0 ? (K - 1) / x.f.d + 1 : 1;
+    maxoff = std::llabs(x.s0) * (int64_t)(std::min<int64_t>(x.f.d, K)) + std::llabs(x.s1) * nq;
+  } else {
+    maxoff = std::llabs(x.s0) * K;
+  }
+  if (maxoff >= (1ll << 31) || std::llabs(x.s0) >= (1ll << 31) || std::llabs(x.s1) >= (1ll << 31)) return false;
+  k.s0 = (int32_t)x.s0;
+  k.s1 = (int32_t)x.s1;
+  *out = k;
+  return true;
+}
+
+__device__ __forceinline__ int32_t koff(const KIdx& m, uint32_t i) {
+  const uint32_t q = (__umulhi(i, m.m) + i) >> m.s;
+  const uint32_t r = i - q * m.d;
+  return (int32_t)r * m.s0 + (int32_t)q * m.s1;
 }
 
 // ---------------------------------------------------------------------------------

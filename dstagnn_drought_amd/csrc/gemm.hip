@@ -9,9 +9,10 @@
 // peak; gfx950 has no xf32).  A workgroup is 4 waves arranged WGM x WGN; each wave
 // owns WM x WN 32x32 accumulators, so the block tile is (32*WM*WGM) x (32*WN*WGN) x 16
 // (64x64, 128x64, 128x128, 128x32, 256x32 are instantiated; a cost model picks one).
-// Global loads are issued UNCONDITIONALLY (out-of-range coordinates are clamped to a
-// valid address and zeroed after the load): a predicated load makes hipcc branch and
-// wait vmcnt(0) per element, serialising the k-tile prefetch.  The next k-tile is
+// Global loads of full k-tiles are issued UNCONDITIONALLY (out-of-range rows/columns are
+// clamped to a valid address; their products land only in unstored C entries): a
+// predicated load makes hipcc branch and wait vmcnt(0) per element, serialising the
+// k-tile prefetch.  The next k-tile is
 // prefetched into registers while the MFMAs consume the current LDS buffer (2 LDS
 // buffers, one barrier per k-tile).  Long reductions are split over workgroups into
 // fp32 partial slabs summed by a deterministic second pass (no float atomics).
@@ -23,8 +24,8 @@ constexpr int BK = 16;
 
 struct GemmK {
   int M, N, K, batch, splitk, kchunk;
-  const float* A; Idx2 am, ak, az;
-  const float* B; Idx2 bk, bn, bz;
+  const float* A; Idx2 am, az; KIdx ak;
+  const float* B; Idx2 bn, bz; KIdx bk;
   float* C; Idx2 cm, cn, cz;
   float alpha, beta;
   const float* bias; int64_t bias_stride;
@@ -77,35 +78,40 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
   }
   const float* pa[LA];
   const float* pb[LB];
-  bool a_mv[LA], b_nv[LB];
 #pragma unroll
   for (int j = 0; j < LA; ++j) {
-    int m = m0 + a_ml[j];
-    a_mv[j] = m < g.M;
-    pa[j] = A + (a_mv[j] ? ioff(g.am, m) : 0);  // clamped: row 0 is always valid
+    const int m = m0 + a_ml[j];
+    pa[j] = A + (m < g.M ? ioff(g.am, m) : 0);  // clamped: row 0 is always valid
   }
 #pragma unroll
   for (int j = 0; j < LB; ++j) {
-    int n = n0 + b_nl[j];
-    b_nv[j] = n < g.N;
-    pb[j] = Bp + (b_nv[j] ? ioff(g.bn, n) : 0);
+    const int n = n0 + b_nl[j];
+    pb[j] = Bp + (n < g.N ? ioff(g.bn, n) : 0);
   }
 
   float ra[LA], rb[LB];
+  // Rows m >= M / columns n >= N read row/column 0 (valid memory): they only feed C
+  // rows/columns the epilogue never stores, so they need no masking.  k >= kend must
+  // read as 0; that happens only in the last k-tile, handled by a uniform branch so the
+  // full tiles issue all their loads back to back with no per-element predicate (a
+  // predicated load is sunk into an exec-masked region and waited on alone).
   auto load_tile = [&](int k0) {
+    if (k0 + BK <= kend) {
 #pragma unroll
-    for (int j = 0; j < LA; ++j) {
-      const int k = k0 + a_kl[j];
-      const int kc = min(k, kend - 1);
-      const float v = pa[j][ioff(g.ak, kc)];
-      ra[j] = (a_mv[j] && k < kend) ? v : 0.f;
-    }
+      for (int j = 0; j < LA; ++j) ra[j] = pa[j][koff(g.ak, k0 + a_kl[j])];
 #pragma unroll
-    for (int j = 0; j < LB; ++j) {
-      const int k = k0 + b_kl[j];
-      const int kc = min(k, kend - 1);
-      const float v = pb[j][ioff(g.bk, kc)];
-      rb[j] = (b_nv[j] && k < kend) ? v : 0.f;
+      for (int j = 0; j < LB; ++j) rb[j] = pb[j][koff(g.bk, k0 + b_kl[j])];
+    } else {
+#pragma unroll
+      for (int j = 0; j < LA; ++j) {
+        const int k = k0 + a_kl[j];
+        ra[j] = k < kend ? pa[j][koff(g.ak, k)] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const int k = k0 + b_kl[j];
+        rb[j] = k < kend ? pb[j][koff(g.bk, k)] : 0.f;
+      }
     }
   };
   auto store_tile = [&](int buf) {
@@ -232,8 +238,12 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   if (!g.A || !g.B || !g.C) { set_last_error("gemm: null operand"); return DSTAGNN_E_ARG; }
   GemmK k;
   k.M = g.M; k.N = g.N; k.K = g.K; k.batch = g.batch;
-  k.A = g.A + g.a_off; k.am = g.am; k.ak = g.ak; k.az = g.az;
-  k.B = g.B + g.b_off; k.bk = g.bk; k.bn = g.bn; k.bz = g.bz;
+  k.A = g.A + g.a_off; k.am = g.am; k.az = g.az;
+  k.B = g.B + g.b_off; k.bn = g.bn; k.bz = g.bz;
+  if (!make_kidx(g.ak, g.K, &k.ak) || !make_kidx(g.bk, g.K, &k.bk)) {
+    set_last_error("gemm: k-dimension offsets exceed int32");
+    return DSTAGNN_E_SHAPE;
+  }
   k.C = g.C + g.c_off; k.cm = g.cm; k.cn = g.cn; k.cz = g.cz;
   k.alpha = g.alpha; k.beta = g.beta; k.bias = g.bias; k.bias_stride = g.bias_stride; k.relu = g.relu;
   k.ws = ws;
