@@ -16,11 +16,13 @@
 // prefetched into registers while the MFMAs consume the current LDS buffer (2 LDS
 // buffers, one barrier per k-tile).  Long reductions are split over workgroups into
 // fp32 partial slabs summed by a deterministic second pass (no float atomics).
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
 
-constexpr int BK = 16;
+constexpr int BKMAX = 32;  // k-tile depth (16 or 32, template parameter)
 
 struct GemmK {
   int M, N, K, batch, splitk, kchunk;
@@ -45,7 +47,7 @@ __device__ __forceinline__ void epilogue_store(const GemmK& g, int zb, int m, in
 
 // A_KC: A is contiguous along k (16 lanes read one row's k-tile).  Otherwise lanes run
 // along m.  B_NC: B contiguous along n (lanes along n), otherwise lanes along k.
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, int BK>
 __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // elements per thread per k-tile
@@ -176,38 +178,43 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
     }
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, int BK>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmK g) {
-  gemm_f32_body<WGM, WGN, WM, WN, A_KC, B_NC>(g);
+  gemm_f32_body<WGM, WGN, WM, WN, A_KC, B_NC, BK>(g);
 }
 // identical body under its own symbol: the call site the benchmark reports as the
 // dominant kernel (rocprofv3 then lists exactly that call site's launches)
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, int BK>
 __global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmK g) {
-  gemm_f32_body<WGM, WGN, WM, WN, A_KC, B_NC>(g);
+  gemm_f32_body<WGM, WGN, WM, WN, A_KC, B_NC, BK>(g);
 }
 
-// out[zb][m][n] = epilogue( sum_s ws[zb][s][m][n] ): 64 outputs x 4 split groups / block
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmK g) {
-  __shared__ float red[4][64];
+// out[zb][m][n] = epilogue( sum_s ws[zb][s][m][n] ).  A workgroup takes 256/G outputs and
+// G split groups per output (G = power of two ~ splitk/8), combined by an LDS tree.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmK g, int G) {
+  __shared__ float red[256];
   const int64_t MN = (int64_t)g.M * g.N;
   const int64_t total = (int64_t)g.batch * MN;
-  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int64_t idx = (int64_t)blockIdx.x * 64 + c;
+  const int per = 256 / G;
+  const int c = threadIdx.x / G, q = threadIdx.x % G;
+  const int64_t idx = (int64_t)blockIdx.x * per + c;
   float s = 0.f;
-  int zb = 0;
-  int64_t mn = 0;
   if (idx < total) {
-    zb = (int)(idx / MN);
-    mn = idx % MN;
+    const int zb = (int)(idx / MN);
+    const int64_t mn = idx % MN;
     const float* p = g.ws + (int64_t)zb * g.splitk * MN + mn;
-    for (int sp = q; sp < g.splitk; sp += 4) s += p[(int64_t)sp * MN];
+    for (int sp = q; sp < g.splitk; sp += G) s += p[(int64_t)sp * MN];
   }
-  red[q][c] = s;
+  red[threadIdx.x] = s;
   __syncthreads();
+  for (int w = G / 2; w > 0; w >>= 1) {
+    if (q < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
   if (q == 0 && idx < total) {
-    s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-    epilogue_store(g, zb, (int)(mn / g.N), (int)(mn % g.N), s);
+    const int zb = (int)(idx / MN);
+    const int64_t mn = idx % MN;
+    epilogue_store(g, zb, (int)(mn / g.N), (int)(mn % g.N), red[threadIdx.x]);
   }
 }
 
@@ -218,15 +225,15 @@ struct Cfg {
 };
 constexpr Cfg kCfgs[] = {{2, 2, 1, 1}, {2, 2, 2, 1}, {2, 2, 2, 2}, {4, 1, 1, 1}, {4, 1, 2, 1}};
 
-template <int WGM, int WGN, int WM, int WN>
+template <int WGM, int WGN, int WM, int WN, int BK>
 void launch_cfg(const GemmK& k, bool akc, bool bnc, bool hot, hipStream_t st) {
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   dim3 grid((unsigned)cdiv64(k.M, BM), (unsigned)cdiv64(k.N, BN), (unsigned)(k.batch * k.splitk));
 #define DS_GEMM_LAUNCH(KER)                                                                                  \
-  if (akc && bnc) hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, true>), grid, dim3(256), 0, st, k);       \
-  else if (akc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, false>), grid, dim3(256), 0, st, k);      \
-  else if (bnc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, true>), grid, dim3(256), 0, st, k);      \
-  else            hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, false>), grid, dim3(256), 0, st, k);
+  if (akc && bnc) hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, true, BK>), grid, dim3(256), 0, st, k);       \
+  else if (akc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, false, BK>), grid, dim3(256), 0, st, k);      \
+  else if (bnc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, true, BK>), grid, dim3(256), 0, st, k);      \
+  else            hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, false, BK>), grid, dim3(256), 0, st, k);
   if (hot) { DS_GEMM_LAUNCH(gemm_f32_hot_kernel) } else { DS_GEMM_LAUNCH(gemm_f32_kernel) }
 #undef DS_GEMM_LAUNCH
 }
@@ -248,6 +255,11 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   k.alpha = g.alpha; k.beta = g.beta; k.bias = g.bias; k.bias_stride = g.bias_stride; k.relu = g.relu;
   k.ws = ws;
 
+  // optional overrides for tuning sweeps (scripts/gemm_sweep.py)
+  static const int env_cfg = getenv("DSTAGNN_GEMM_CFG") ? atoi(getenv("DSTAGNN_GEMM_CFG")) : -1;
+  static const int env_bk = getenv("DSTAGNN_GEMM_BK") ? atoi(getenv("DSTAGNN_GEMM_BK")) : 0;
+  static const int env_split = getenv("DSTAGNN_GEMM_SPLITK") ? atoi(getenv("DSTAGNN_GEMM_SPLITK")) : 0;
+  const int BK = env_bk == 16 ? 16 : 32;
   // tile choice by a small cost model: waves of ~2 workgroups per CU, each costing its
   // MFMA area plus a per-edge load overhead
   int best = 0;
@@ -259,6 +271,7 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
     const double cost = waves * bm * bn * (1.0 + 48.0 / bm + 48.0 / bn);
     if (cost < best_cost - 1e-9) { best_cost = cost; best = c; }
   }
+  if (env_cfg >= 0 && env_cfg < (int)(sizeof(kCfgs) / sizeof(kCfgs[0]))) best = env_cfg;
   Cfg cfg = kCfgs[best];
   int64_t blocks = cdiv64(g.M, cfg.bm()) * cdiv64(g.N, cfg.bn()) * g.batch;
 
@@ -268,11 +281,12 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
     int want = (int)std::min<int64_t>(512, cdiv64(512, blocks));
     int maxk = g.K / 128;  // keep >= 128 k per split
     splitk = std::max(1, std::min(want, maxk));
+    if (env_split > 0) splitk = std::min(env_split, std::max(1, g.K / 64));
     while (splitk > 1 && (size_t)g.batch * splitk * g.M * g.N > ws_floats) --splitk;
   }
   int kchunk = g.K;
   if (splitk > 1) {
-    kchunk = (int)cdiv64(cdiv64(g.K, splitk), BK) * BK;
+    kchunk = (int)cdiv64(cdiv64(g.K, splitk), BKMAX) * BKMAX;
     splitk = (int)cdiv64(g.K, kchunk);
   }
   if (g.K <= 0) { splitk = 1; kchunk = 0; }
@@ -281,17 +295,22 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   const bool akc = !g.ak.two && g.ak.s0 == 1;
   const bool bnc = !g.bn.two && g.bn.s0 == 1;
   const bool hot = g.hot != 0;
-  switch (best) {
-    case 0: launch_cfg<2, 2, 1, 1>(k, akc, bnc, hot, st); break;
-    case 1: launch_cfg<2, 2, 2, 1>(k, akc, bnc, hot, st); break;
-    case 2: launch_cfg<2, 2, 2, 2>(k, akc, bnc, hot, st); break;
-    case 3: launch_cfg<4, 1, 1, 1>(k, akc, bnc, hot, st); break;
-    default: launch_cfg<4, 1, 2, 1>(k, akc, bnc, hot, st); break;
+#define DS_CFG_SWITCH(BKV)                                          \
+  switch (best) {                                                   \
+    case 0: launch_cfg<2, 2, 1, 1, BKV>(k, akc, bnc, hot, st); break; \
+    case 1: launch_cfg<2, 2, 2, 1, BKV>(k, akc, bnc, hot, st); break; \
+    case 2: launch_cfg<2, 2, 2, 2, BKV>(k, akc, bnc, hot, st); break; \
+    case 3: launch_cfg<4, 1, 1, 1, BKV>(k, akc, bnc, hot, st); break; \
+    default: launch_cfg<4, 1, 2, 1, BKV>(k, akc, bnc, hot, st); break; \
   }
+  if (BK == 16) { DS_CFG_SWITCH(16) } else { DS_CFG_SWITCH(32) }
+#undef DS_CFG_SWITCH
   DS_CHECK_LAUNCH();
   if (splitk > 1) {
     int64_t total = (int64_t)g.batch * g.M * g.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv64(total, 64)), dim3(256), 0, st, k);
+    int G = 1;
+    while (G < 64 && G * 8 < splitk) G *= 2;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv64(total, 256 / G)), dim3(256), 0, st, k, G);
     DS_CHECK_LAUNCH();
   }
   return 0;

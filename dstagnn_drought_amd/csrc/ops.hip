@@ -292,10 +292,12 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ i
     const int r = t / E, e = t % E;
     float s = 0.f;
     if (r < R) {
-      for (int64_t aa = a0 + r; aa < a1; aa += R) {
-        float v = in[aa * E + e];
-        if (in2) v *= in2[aa * E + e];
-        s += v;
+      if (in2) {
+#pragma unroll 4
+        for (int64_t aa = a0 + r; aa < a1; aa += R) s += in[aa * E + e] * in2[aa * E + e];
+      } else {
+#pragma unroll 4
+        for (int64_t aa = a0 + r; aa < a1; aa += R) s += in[aa * E + e];
       }
     }
     red[t] = s;
@@ -710,8 +712,8 @@ int op_ln_bwd(const LnBwd& a, hipStream_t st) {
 int op_colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
               float* part, size_t part_floats, hipStream_t st) {
   const int E = O * I;
-  // ~16K elements per stage-1 workgroup, at most 1024 partial rows
-  int64_t P = std::max<int64_t>(1, std::min<int64_t>(1024, cdiv64(A * E, 16384)));
+  // ~4K elements per stage-1 workgroup, at most 2048 partial rows
+  int64_t P = std::max<int64_t>(1, std::min<int64_t>(2048, cdiv64(A * E, 4096)));
   P = std::min<int64_t>(P, A);
   while (P > 1 && (size_t)P * E > part_floats) P /= 2;
   if ((size_t)P * E > part_floats) { set_last_error("colsum: scratch too small"); return DSTAGNN_E_SPACE; }

@@ -1,0 +1,115 @@
+#!/usr/bin/env python
+"""Tuning sweep for the strided f32-MFMA GEMM (dstagnn_gemm_f32) on the DSTAGNN block's
+GEMM shapes (PEMS08, B=32).  Each (tile config, BK) runs in its own subprocess because
+the overrides (DSTAGNN_GEMM_CFG / DSTAGNN_GEMM_BK) are read once per process.
+
+    python scripts/gemm_sweep.py            # full sweep, prints a table
+    python scripts/gemm_sweep.py --child    # (internal) one config
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# name, M, N, K, batch, A k-contiguous?, B n-contiguous?
+SHAPES = [
+    ("qkv", 12288, 96, 170, 1, True, False),
+    ("fc", 12288, 170, 96, 1, True, False),
+    ("preconv", 5440, 512, 384, 1, False, False),
+    ("sat_proj", 5440, 96, 512, 1, True, False),
+    ("sat_scores", 170, 170, 32, 96, True, False),
+    ("cheb_agg", 170, 384, 510, 32, False, True),
+    ("gtu7", 32640, 64, 224, 1, False, False),
+    ("gtu3", 54400, 64, 96, 1, False, False),
+    ("fcmy", 174080, 12, 24, 1, True, False),
+    ("gtu_dX7", 65280, 32, 448, 1, False, False),
+    ("cheb_dW", 170, 170, 384, 96, True, False),
+    ("cheb_dxth", 170, 384, 170, 96, True, True),
+    ("dthcat", 32, 96, 65280, 1, False, False),
+    ("sat_dW", 96, 512, 5440, 1, False, True),
+    ("dZd", 5440, 512, 96, 1, True, True),
+    ("dWp", 512, 384, 5440, 1, False, False),
+    ("dO", 384, 5440, 512, 1, False, False),
+    ("gtu_dW7", 64, 224, 32640, 1, False, False),
+    ("fcmy_dW", 12, 24, 174080, 1, False, True),
+]
+
+
+def child(iters):
+    import torch
+    from dstagnn_drought_amd import _lib
+    lib = _lib.load()
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    res = {}
+    for name, M, N, K, batch, akc, bnc in SHAPES:
+        A = torch.randn(batch, M, K, device="cuda") if akc else torch.randn(batch, K, M, device="cuda")
+        B = torch.randn(batch, K, N, device="cuda") if bnc else torch.randn(batch, N, K, device="cuda")
+        C = torch.empty(batch, M, N, device="cuda")
+        d = _lib.GemmDesc()
+        d.M, d.N, d.K, d.batch = M, N, K, batch
+        d.A, d.B, d.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
+        d.a_m, d.a_k = (_lib.idx(0, K), _lib.idx(0, 1)) if akc else (_lib.idx(0, 1), _lib.idx(0, M))
+        d.b_k, d.b_n = (_lib.idx(0, N), _lib.idx(0, 1)) if bnc else (_lib.idx(0, 1), _lib.idx(0, K))
+        d.a_z, d.b_z, d.c_z = _lib.idx(0, M * K), _lib.idx(0, K * N), _lib.idx(0, M * N)
+        d.c_m, d.c_n = _lib.idx(0, N), _lib.idx(0, 1)
+        d.alpha, d.beta, d.bias, d.bias_stride, d.relu = 1.0, 0.0, None, 1, 0
+        st = _lib.stream_handle()
+
+        def run():
+            _lib.check(lib.dstagnn_gemm_f32(ctypes.byref(d), _lib.ptr(ws), ws.numel(), st), name)
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / iters * 1e3
+        if os.environ.get("DSTAGNN_GEMM_CHECK"):
+            ref = torch.bmm(A if akc else A.transpose(1, 2), B if bnc else B.transpose(1, 2))
+            err = float((C - ref).abs().max() / ref.abs().max())
+            assert err < 1e-5, (name, err)
+        res[name] = us
+    print(json.dumps(res))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--child", action="store_true")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--configs", default="auto:16,auto:32,0:32,1:32,2:32,3:32,4:32,0:16,1:16")
+    args = ap.parse_args()
+    if args.child:
+        child(args.iters)
+        return
+    table = {}
+    for spec in args.configs.split(","):
+        cfg, bk = spec.split(":")
+        env = dict(os.environ, DSTAGNN_GEMM_BK=bk)
+        if cfg != "auto":
+            env["DSTAGNN_GEMM_CFG"] = cfg
+        env["DSTAGNN_GEMM_CHECK"] = "1" if spec == "auto:32" else ""
+        out = subprocess.run([sys.executable, __file__, "--child", "--iters", str(args.iters)], env=env,
+                             capture_output=True, text=True, timeout=300)
+        if out.returncode != 0:
+            print(spec, "FAILED", out.stderr[-2000:], flush=True)
+            continue
+        table[spec] = json.loads(out.stdout.strip().splitlines()[-1])
+        print(spec, "done", flush=True)
+    specs = list(table)
+    print(f"{'shape':12s} {'GFLOP':>7s} " + " ".join(f"{s:>9s}" for s in specs) + "   best TF/s")
+    for name, M, N, K, batch, _, _ in SHAPES:
+        gf = 2.0 * M * N * K * batch / 1e9
+        row = [table[s].get(name, float('nan')) for s in specs]
+        best = min(row)
+        print(f"{name:12s} {gf:7.3f} " + " ".join(f"{v:9.1f}" for v in row) + f"   {gf / best * 1e3:7.1f}")
+
+
+if __name__ == "__main__":
+    main()
