@@ -139,7 +139,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from dstagnn_drought_amd import _lib
-    from dstagnn_drought_amd.block_fn import make_dims, workspace_sizes, _fill
+    from dstagnn_drought_amd.block_fn import make_dims, workspace_sizes, _fill, graph_struct, use_sparse
 
     blk, cheb, apa = build_block(dev)
     c = CFG
@@ -188,13 +188,14 @@ def main():
 
     # ---- dominant kernel: the pre_conv fwd GEMM (gemm_f32_hot_kernel), HIP events on its stream
     meta = dict(blk.meta, train=True, seed=1)
-    dims = make_dims(x, meta, _lib.RES_BCAST, True, 1)
+    graph = blk.cheb_conv_SAt.graph(blk.adj_pa)
+    dims = make_dims(x, meta, _lib.RES_BCAST, True, 1, use_sparse(graph, meta, c["T"]))
     sv, sc = workspace_sizes(dims)
     save = torch.empty(sv, dtype=torch.uint8, device=dev)
     scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
     names, ps = zip(*blk.named_parameters())
     pstruct = _fill(_lib.BlockParams(), names, ps)
-    gstruct = _lib.Graph(blk.cheb_conv_SAt.cheb_stack.data_ptr(), blk.adj_pa.data_ptr())
+    gstruct = graph_struct(graph)
     out = torch.empty(B, c["N"], c["C"], c["T"], device=dev)
     re_at = torch.empty(B, c["C"], c["n_heads"], c["T"], c["T"], device=dev)
     lib = _lib.load()

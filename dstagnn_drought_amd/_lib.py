@@ -28,7 +28,7 @@ class BlockDims(ctypes.Structure):
                 ("n_heads", ctypes.c_int), ("d_k", ctypes.c_int), ("d_v", ctypes.c_int),
                 ("d_model", ctypes.c_int), ("K", ctypes.c_int), ("C", ctypes.c_int),
                 ("res_mode", ctypes.c_int), ("train", ctypes.c_int), ("drop_p", ctypes.c_float),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("cheb_sparse", ctypes.c_int)]
 
 
 # field order == struct dstagnn_block_params / dstagnn_block_grads
@@ -53,7 +53,8 @@ BlockGrads = _mk_struct("BlockGrads")
 
 
 class Graph(ctypes.Structure):
-    _fields_ = [("cheb", _vp), ("adj_pa", _vp)]
+    _fields_ = [("cheb", _vp), ("adj_pa", _vp), ("nnz", ctypes.c_int), ("csc_ptr", _vp), ("csc_row", _vp),
+                ("csr_ptr", _vp), ("csr_col", _vp)]
 
 
 class Idx(ctypes.Structure):
@@ -89,8 +90,10 @@ def load():
                                   _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp],
         "dstagnn_block_backward": [P(BlockDims), P(BlockParams), P(Graph), _vp, _vp, _vp, _vp, _vp, _vp,
                                    P(BlockGrads), _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp],
-        "dstagnn_cheb_sat_forward": [ctypes.c_int] * 6 + [_vp] * 11 + [ctypes.c_size_t, _vp],
-        "dstagnn_cheb_sat_backward": [ctypes.c_int] * 6 + [_vp] * 14 + [ctypes.c_size_t, _vp],
+        "dstagnn_cheb_sat_forward": [ctypes.c_int] * 7 + [_vp] * 4 + [P(Graph)] + [_vp] * 5
+                                    + [ctypes.c_size_t, _vp],
+        "dstagnn_cheb_sat_backward": [ctypes.c_int] * 7 + [_vp] * 2 + [P(Graph)] + [_vp] * 10
+                                     + [ctypes.c_size_t, _vp],
         "dstagnn_gemm_f32": [P(GemmDesc), _vp, ctypes.c_size_t, _vp],
         "dstagnn_block_time_stage": [P(BlockDims), P(BlockParams), P(Graph), _vp, _vp, _vp, _vp,
                                      _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,

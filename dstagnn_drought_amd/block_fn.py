@@ -64,10 +64,31 @@ def res_mode_of(res_att, F):
                        "at non-singleton dimension 1")
 
 
-def make_dims(x, meta, res_mode, train, seed):
+def make_dims(x, meta, res_mode, train, seed, sparse=0):
     B, N, F, T = x.shape
     return _lib.BlockDims(B, N, F, T, meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"],
-                          meta["C"], res_mode, 1 if train else 0, float(meta.get("drop_p", 0.05)), seed)
+                          meta["C"], res_mode, 1 if train else 0, float(meta.get("drop_p", 0.05)), seed, int(sparse))
+
+
+def graph_struct(graph):
+    """dstagnn_graph from a dict of device tensors: cheb (K,N,N), adj_pa (N,N) and, for the
+    sparse path, int32 csc_ptr / csc_row / csr_ptr / csr_col of the union support."""
+    g = _lib.Graph()
+    g.cheb = graph["cheb"].data_ptr()
+    g.adj_pa = graph["adj_pa"].data_ptr()
+    if graph.get("csc_row") is not None:
+        g.nnz = int(graph["csc_row"].numel())
+        for k in ("csc_ptr", "csc_row", "csr_ptr", "csr_col"):
+            setattr(g, k, graph[k].data_ptr())
+    return g
+
+
+def use_sparse(graph, meta, T):
+    """Sparse Chebyshev aggregation when the union support is <= 1/4 dense and C*T <= 1024."""
+    if graph.get("csc_row") is None:
+        return False
+    N = graph["adj_pa"].shape[0]
+    return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= 1024
 
 
 def workspace_sizes(dims):
@@ -79,7 +100,7 @@ def workspace_sizes(dims):
 
 class DSTAGNNBlockFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, meta, names, x, res_att, cheb, adj_pa, *params):
+    def forward(ctx, meta, names, x, res_att, graph, *params):
         lib = _lib.load()
         ctx.set_materialize_grads(False)
         dev = x.device
@@ -89,28 +110,28 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         ra = res_att.contiguous() if mode != _lib.RES_NONE else None
         train = bool(meta.get("train", False))
         seed = int(meta.get("seed", 0))
-        dims = make_dims(x, meta, mode, train, seed)
+        dims = make_dims(x, meta, mode, train, seed, use_sparse(graph, meta, T))
         sv, sc = workspace_sizes(dims)
         save = torch.empty(sv, dtype=torch.uint8, device=dev)
         scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
         out = torch.empty(B, N, meta["C"], T, dtype=torch.float32, device=dev)
         re_at = torch.empty(B, F, meta["n_heads"], T, T, dtype=torch.float32, device=dev)
         p = _fill(_lib.BlockParams(), names, params)
-        g = _lib.Graph(cheb.data_ptr(), adj_pa.data_ptr())
+        g = graph_struct(graph)
         rc = lib.dstagnn_block_forward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
                                        _lib.ptr(ra), _lib.ptr(out), _lib.ptr(re_at), _lib.ptr(save), sv,
                                        _lib.ptr(scratch), sc, _lib.stream_handle(dev))
         _lib.check(rc, "dstagnn_block_forward")
         del scratch
-        ctx.meta, ctx.names, ctx.mode, ctx.dims = meta, names, mode, dims
+        ctx.meta, ctx.names, ctx.mode, ctx.dims, ctx.graph = meta, names, mode, dims, graph
         ctx.save_buf, ctx.sizes = save, (sv, sc)
-        ctx.save_for_backward(x, ra if ra is not None else torch.empty(0, device=dev), cheb, adj_pa, *params)
+        ctx.save_for_backward(x, ra if ra is not None else torch.empty(0, device=dev), *params)
         return out, re_at
 
     @staticmethod
     def backward(ctx, d_out, d_re_at):
         lib = _lib.load()
-        x, ra, cheb, adj_pa, *params = ctx.saved_tensors
+        x, ra, *params = ctx.saved_tensors
         dev = x.device
         names, mode, dims = ctx.names, ctx.mode, ctx.dims
         if d_out is None:
@@ -124,7 +145,7 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
             grads.append(torch.empty_like(t) if used else None)
         gs = _fill(_lib.BlockGrads(), names, grads)
         p = _fill(_lib.BlockParams(), names, params)
-        g = _lib.Graph(cheb.data_ptr(), adj_pa.data_ptr())
+        g = graph_struct(ctx.graph)
         d_x = torch.empty_like(x)
         d_ra = torch.empty_like(ra) if mode != _lib.RES_NONE else None
         sv, sc = ctx.sizes
@@ -136,7 +157,7 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
                                         _lib.stream_handle(dev))
         _lib.check(rc, "dstagnn_block_backward")
         ctx.save_buf = None
-        return (None, None, d_x, d_ra, None, None, *grads)
+        return (None, None, d_x, d_ra, None, *grads)
 
 
 def dropout_masks(meta, x_shape, seed):

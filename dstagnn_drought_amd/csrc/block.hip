@@ -40,7 +40,7 @@ struct Dims {
   int B, N, F, T, h, dk, dv, D, K, C;
   int64_t FT, BFT, BN, NN, HQ, HV, QW, KD, KC, CT, KCT, S;
   int Tg[3], Lp[3], ks[3];
-  bool first;
+  bool first, sparse;
 };
 
 Dims mkdims(const dstagnn_block_dims& d) {
@@ -52,6 +52,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.KC = (int64_t)m.K * m.C; m.CT = (int64_t)m.C * m.T; m.KCT = m.KC * m.T; m.S = 3 * (int64_t)m.T - 12;
   for (int g = 0; g < 3; ++g) { m.ks[g] = 3 + 2 * g; m.Tg[g] = m.T - m.ks[g] + 1; m.Lp[g] = m.T + m.ks[g] - 1; }
   m.first = (m.F == 1);
+  m.sparse = d.cheb_sparse != 0;
   return m;
 }
 
@@ -77,7 +78,7 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   s.Zd = a.take(m.BN * m.D);
   s.qk = a.take(m.BN * 2 * m.KD);
   s.P = a.take((int64_t)m.B * m.K * m.NN);
-  s.W = a.take((int64_t)m.B * m.K * m.NN);
+  s.W = m.sparse ? nullptr : a.take((int64_t)m.B * m.K * m.NN);
   s.xth = a.take(m.BN * m.KCT);
   s.X = a.take(m.BN * m.CT);
   for (int g = 0; g < 3; ++g) s.conv[g] = a.take(m.BN * 2 * m.C * std::max(m.Tg[g], 0));
@@ -156,6 +157,10 @@ int check_dims(const dstagnn_block_dims* d) {
   }
   if (d->K > DSTAGNN_MAX_K) { set_last_error("K > DSTAGNN_MAX_K"); return DSTAGNN_E_SHAPE; }
   if (d->T < 7) { set_last_error("T must be >= 7 (GTU kernel 7, fcmy 3T-12)"); return DSTAGNN_E_SHAPE; }
+  if (d->cheb_sparse && !cheb_sparse_ok(d->C * d->T)) {
+    set_last_error("cheb_sparse requires C*T <= 1024");
+    return DSTAGNN_E_SHAPE;
+  }
   if (d->F != 1 && d->F != d->C) {
     // the reference fails at model/DSTAGNN_my.py:252 (x.permute + time_conv_output)
     set_last_error("The size of tensor a (" + std::to_string(d->F) + ") must match the size of tensor b (" +
@@ -173,17 +178,26 @@ struct ChebIO {
   const float* x;
   const float* S;          // scores (B,K,N,N) (may alias P)
   const float* const* mask;
-  const float* cheb;
-  const float* apa;
+  const dstagnn_graph* g;  // cheb (K,N,N), adj_pa, and the CSC/CSR support
+  bool sparse;
   const float* thcat;      // (F, K*C)
-  float *P, *W, *xth, *X;
+  float *P, *W, *xth, *X;  // W unused (null) on the sparse path
 };
+
+ChebSp make_sp(int B, int N, int K, int CT, const dstagnn_graph* g) {
+  ChebSp a;
+  a.B = B; a.N = N; a.K = K; a.CT = CT;
+  a.csc_ptr = g->csc_ptr; a.csc_row = g->csc_row; a.csr_ptr = g->csr_ptr; a.csr_col = g->csr_col;
+  a.cheb = g->cheb;
+  return a;
+}
 
 int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
   const int64_t NN = (int64_t)c.N * c.N, KC = (int64_t)c.K * c.C, T = c.T, CT = (int64_t)c.C * T,
                 KCT = KC * T, FT = (int64_t)c.F * T;
   ChebSm sm;
-  sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.S = c.S; sm.apa = c.apa; sm.cheb = c.cheb; sm.P = c.P; sm.W = c.W;
+  sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.S = c.S; sm.apa = c.g->adj_pa; sm.cheb = c.g->cheb; sm.P = c.P;
+  sm.W = c.sparse ? nullptr : c.W;
   for (int k = 0; k < c.K; ++k) sm.mask[k] = c.mask[k];
   DS_TRY(op_cheb_softmax_fwd(sm, st));
   // xth[(b,i,t),(k,c)] = sum_f x[b,i,f,t] Theta_k[f,c]
@@ -196,6 +210,11 @@ int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
     DS_TRY(run_gemm(g, ws, kGemmWs, st));
   }
   // X[b,j,(c,t)] = relu( sum_{k,i} W[b,k,i,j] xth[b,i,k,(c,t)] )
+  if (c.sparse) {
+    ChebSp sp = make_sp(c.B, c.N, c.K, (int)CT, c.g);
+    sp.P = c.P; sp.xth = c.xth; sp.out = c.X;
+    return op_cheb_spmm_fwd(sp, st);
+  }
   {
     Gemm g;
     g.M = c.N; g.N = (int)CT; g.K = c.K * c.N; g.batch = c.B;
@@ -212,8 +231,8 @@ struct ChebGradIO {
   int B, N, F, T, K, C;
   const float* x;
   const float* thcat;
-  const float* cheb;
-  const float* apa;
+  const dstagnn_graph* g;
+  bool sparse;
   const float *P, *W, *xth;
   const float* gpre;       // d(pre-ReLU out) (B,N,C,T)
   float* dx;               // accumulated (beta = dx_beta)
@@ -227,8 +246,17 @@ struct ChebGradIO {
 int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
   const int64_t NN = (int64_t)c.N * c.N, KC = (int64_t)c.K * c.C, T = c.T, CT = (int64_t)c.C * T,
                 KCT = KC * T, FT = (int64_t)c.F * T;
+  if (c.sparse) {
+    // dW only on the support (zero elsewhere); dxth by the transposed sparse product
+    hipError_t e = hipMemsetAsync(c.dz, 0, sizeof(float) * (size_t)c.B * c.K * NN, st);
+    if (e != hipSuccess) { set_last_error(std::string("memset: ") + hipGetErrorString(e)); return (int)e; }
+    ChebSp sp = make_sp(c.B, c.N, c.K, (int)CT, c.g);
+    sp.P = c.P; sp.xth = c.xth; sp.g = c.gpre; sp.dW = c.dz; sp.dxth = c.dxth;
+    DS_TRY(op_cheb_sddmm_bwd(sp, st));
+    DS_TRY(op_cheb_spmm_t_bwd(sp, st));
+  }
   // dW[b,k,i,j] = sum_ct xth[b,i,k,ct] g[b,j,ct]
-  {
+  if (!c.sparse) {
     Gemm g;
     g.M = c.N; g.N = c.N; g.K = (int)CT; g.batch = c.B * c.K;
     g.A = c.xth; g.am = idx1(KCT); g.ak = idx1(1); g.az = idx2(c.K, CT, c.N * KCT);
@@ -237,7 +265,7 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
     DS_TRY(run_gemm(g, ws, kGemmWs, st));
   }
   // dxth[b,i,k,ct] = sum_j W[b,k,i,j] g[b,j,ct]
-  {
+  if (!c.sparse) {
     Gemm g;
     g.M = c.N; g.N = (int)CT; g.K = c.N; g.batch = c.B * c.K;
     g.A = c.W; g.am = idx1(c.N); g.ak = idx1(1); g.az = idx1(NN);
@@ -247,7 +275,7 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
   }
   // softmax backward in place: dz = P * (T o dW - colsum(P T o dW))
   ChebSm sm;
-  sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.apa = c.apa; sm.cheb = c.cheb; sm.P = const_cast<float*>(c.P);
+  sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.apa = c.g->adj_pa; sm.cheb = c.g->cheb; sm.P = const_cast<float*>(c.P);
   sm.dW = c.dz; sm.dz = c.dz;
   for (int k = 0; k < c.K; ++k) sm.dmask[k] = c.dmask[k];
   DS_TRY(op_cheb_softmax_bwd(sm, st));
@@ -411,7 +439,7 @@ struct Fwd {
     DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, w.thcat, st));
     ChebIO c;
     c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
-    c.x = x; c.S = s.P; c.mask = p.mask; c.cheb = gr.cheb; c.apa = gr.adj_pa; c.thcat = w.thcat;
+    c.x = x; c.S = s.P; c.mask = p.mask; c.g = &gr; c.sparse = m.sparse; c.thcat = w.thcat;
     c.P = s.P; c.W = s.W; c.xth = s.xth; c.X = s.X;
     return cheb_forward(c, w.gemm_ws, st);
   }
@@ -552,7 +580,7 @@ struct Bwd {
     DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, w.thcat, st));
     ChebGradIO c;
     c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
-    c.x = x; c.thcat = w.thcat; c.cheb = gr.cheb; c.apa = gr.adj_pa; c.P = s.P; c.W = s.W; c.xth = s.xth;
+    c.x = x; c.thcat = w.thcat; c.g = &gr; c.sparse = m.sparse; c.P = s.P; c.W = s.W; c.xth = s.xth;
     c.gpre = w.gpre; c.dx = dx; c.dx_beta = 1.f; c.dz = w.dW; c.dthcat = w.dthcat; c.dmask = gd.mask;
     c.dxth = w.dxth;
     DS_TRY(cheb_backward(c, w.gemm_ws, st));
@@ -731,6 +759,15 @@ int check_space(const Dims& m, size_t save_bytes, size_t scratch_bytes) {
   return 0;
 }
 
+int check_graph(const Dims& m, const dstagnn_graph* g) {
+  if (!g->cheb || !g->adj_pa) { set_last_error("graph: null cheb / adj_pa"); return DSTAGNN_E_ARG; }
+  if (m.sparse && (g->nnz <= 0 || !g->csc_ptr || !g->csc_row || !g->csr_ptr || !g->csr_col)) {
+    set_last_error("cheb_sparse set but the graph carries no CSC/CSR support");
+    return DSTAGNN_E_ARG;
+  }
+  return 0;
+}
+
 void* align256(void* p) { return (void*)(((uintptr_t)p + 255) & ~uintptr_t(255)); }
 
 }  // namespace
@@ -758,6 +795,7 @@ int dstagnn_block_forward(const dstagnn_block_dims* d, const dstagnn_block_param
   if (d->res_mode != DSTAGNN_RES_NONE && !res_att) { set_last_error("res_att missing"); return DSTAGNN_E_ARG; }
   Dims m = mkdims(*d);
   DS_TRY(check_space(m, save_bytes, scratch_bytes));
+  DS_TRY(check_graph(m, g));
   Arena a(align256(save)), b(align256(scratch));
   SaveBufs s = plan_save(m, a);
   Scratch w = plan_scratch(m, b);
@@ -777,6 +815,7 @@ int dstagnn_block_backward(const dstagnn_block_dims* d, const dstagnn_block_para
   }
   Dims m = mkdims(*d);
   DS_TRY(check_space(m, save_bytes, scratch_bytes));
+  DS_TRY(check_graph(m, g));
   Arena a(align256(save)), b(align256(scratch));
   SaveBufs s = plan_save(m, a);
   Scratch w = plan_scratch(m, b);
@@ -784,26 +823,29 @@ int dstagnn_block_backward(const dstagnn_block_dims* d, const dstagnn_block_para
   return bw.run();
 }
 
-int dstagnn_cheb_sat_forward(int B, int N, int F, int T, int K, int C, const float* x, const float* sat,
-                             const float* theta_cat, const float* mask_cat, const float* cheb, const float* adj_pa,
-                             float* out, float* P, float* W, float* xth, void* scratch, size_t scratch_bytes,
+int dstagnn_cheb_sat_forward(int B, int N, int F, int T, int K, int C, int sparse, const float* x, const float* sat,
+                             const float* theta_cat, const float* mask_cat, const dstagnn_graph* g, float* out,
+                             float* P, float* W, float* xth, void* scratch, size_t scratch_bytes,
                              dstagnn_stream_t stream) {
-  if (K > DSTAGNN_MAX_K || K <= 0) return DSTAGNN_E_SHAPE;
+  if (K > DSTAGNN_MAX_K || K <= 0 || !g) return DSTAGNN_E_SHAPE;
   if (scratch_bytes < kGemmWs * sizeof(float) + 256) { set_last_error("scratch too small"); return DSTAGNN_E_SPACE; }
+  if (sparse && (!cheb_sparse_ok(C * T) || g->nnz <= 0)) { set_last_error("sparse path unavailable"); return DSTAGNN_E_ARG; }
   const float* masks[DSTAGNN_MAX_K];
   for (int k = 0; k < K; ++k) masks[k] = mask_cat + (int64_t)k * N * N;
   ChebIO c;
   c.B = B; c.N = N; c.F = F; c.T = T; c.K = K; c.C = C;
-  c.x = x; c.S = sat; c.mask = masks; c.cheb = cheb; c.apa = adj_pa; c.thcat = theta_cat;
+  c.x = x; c.S = sat; c.mask = masks; c.g = g; c.sparse = sparse != 0; c.thcat = theta_cat;
   c.P = P; c.W = W; c.xth = xth; c.X = out;
   return cheb_forward(c, (float*)align256(scratch), (hipStream_t)stream);
 }
 
-int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C, const float* x, const float* theta_cat,
-                              const float* cheb, const float* adj_pa, const float* out, const float* P, const float* W,
-                              const float* xth, const float* d_out, float* d_x, float* d_sat, float* d_theta_cat,
-                              float* d_mask_cat, void* scratch, size_t scratch_bytes, dstagnn_stream_t stream) {
-  if (K > DSTAGNN_MAX_K || K <= 0) return DSTAGNN_E_SHAPE;
+int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C, int sparse, const float* x,
+                              const float* theta_cat, const dstagnn_graph* g, const float* out, const float* P,
+                              const float* W, const float* xth, const float* d_out, float* d_x, float* d_sat,
+                              float* d_theta_cat, float* d_mask_cat, void* scratch, size_t scratch_bytes,
+                              dstagnn_stream_t stream) {
+  if (K > DSTAGNN_MAX_K || K <= 0 || !g) return DSTAGNN_E_SHAPE;
+  if (sparse && (!cheb_sparse_ok(C * T) || g->nnz <= 0)) { set_last_error("sparse path unavailable"); return DSTAGNN_E_ARG; }
   const int64_t nbig = (int64_t)B * N * C * T;
   const int64_t nxth = (int64_t)B * N * K * C * T;
   size_t need = (kGemmWs + nbig + nxth) * sizeof(float) + 3 * 256;
@@ -818,7 +860,7 @@ int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C, const fl
   for (int k = 0; k < K; ++k) dmask[k] = d_mask_cat + (int64_t)k * N * N;
   ChebGradIO c;
   c.B = B; c.N = N; c.F = F; c.T = T; c.K = K; c.C = C;
-  c.x = x; c.thcat = theta_cat; c.cheb = cheb; c.apa = adj_pa; c.P = P; c.W = W; c.xth = xth;
+  c.x = x; c.thcat = theta_cat; c.g = g; c.sparse = sparse != 0; c.P = P; c.W = W; c.xth = xth;
   c.gpre = gpre; c.dx = d_x; c.dx_beta = 0.f; c.dz = d_sat; c.dthcat = d_theta_cat; c.dmask = dmask; c.dxth = dxth;
   return cheb_backward(c, ws, st);
 }

@@ -140,7 +140,9 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
   const int lr = lane & 31, lk = lane >> 5;
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
+#ifndef DSTAGNN_ABLATE_LOADS
     if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BK);
+#endif
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       float a[WM], b[WN];
@@ -152,7 +154,11 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
       for (int i = 0; i < WM; ++i)
 #pragma unroll
         for (int j = 0; j < WN; ++j)
+#ifdef DSTAGNN_ABLATE_MFMA
+          { acc[i][j][0] += a[i] * b[j]; }
+#else
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+#endif
     }
     if (t + 1 < ntiles) store_tile(cur ^ 1);
     __syncthreads();

@@ -399,14 +399,14 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
   const float inv = 1.f / L;
   if (j < N) {
     float* P = a.P + (int64_t)bk * N * N;
-    float* W = a.W + (int64_t)bk * N * N;
+    float* W = a.W ? a.W + (int64_t)bk * N * N : nullptr;
 #pragma unroll 2
     for (int i = g; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
       const float z = S[o] + a.apa[o] * Mk[o];
       const float p = __expf(z - M) * inv;
       P[o] = p;
-      W[o] = Tk[o] * p;
+      if (W) W[o] = Tk[o] * p;
     }
   }
 }

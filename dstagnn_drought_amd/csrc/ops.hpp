@@ -77,6 +77,24 @@ struct PackTheta {
   float* dst[DSTAGNN_MAX_K] = {};         // unpack: K x (F,C) (null entries skipped)
 };
 
+// sparse Chebyshev aggregation over the union support of T_0..T_{K-1} (cheb_sparse.hip)
+struct ChebSp {
+  int B = 0, N = 0, K = 0, CT = 0;
+  const int* csc_ptr = nullptr; const int* csc_row = nullptr;  // column j -> source rows i
+  const int* csr_ptr = nullptr; const int* csr_col = nullptr;  // row i -> destination columns j
+  const float* cheb = nullptr;   // (K,N,N)
+  const float* P = nullptr;      // (B,K,N,N) column softmax
+  const float* xth = nullptr;    // (B,N,K,CT)
+  float* out = nullptr;          // (B,N,CT)  fwd (ReLU applied)
+  const float* g = nullptr;      // (B,N,CT)  bwd: d(pre-ReLU out)
+  float* dW = nullptr;           // (B,K,N,N) bwd: written on the support only
+  float* dxth = nullptr;         // (B,N,K,CT) bwd
+};
+bool cheb_sparse_ok(int CT);
+int op_cheb_spmm_fwd(const ChebSp& a, hipStream_t st);
+int op_cheb_sddmm_bwd(const ChebSp& a, hipStream_t st);
+int op_cheb_spmm_t_bwd(const ChebSp& a, hipStream_t st);
+
 int op_pack_theta(const PackTheta& a, hipStream_t st);
 int op_transpose(const float* in, float* out, int R, int Cc, int batch, int64_t in_bs, int64_t out_bs, float beta,
                  hipStream_t st);

@@ -79,10 +79,39 @@ class cheb_conv_withSAt(nn.Module):
         self.mask = nn.ParameterList([nn.Parameter(torch.empty(num_of_vertices, num_of_vertices)) for _ in range(K)])
         cp = torch.stack([torch.as_tensor(np.asarray(c), dtype=torch.float32) for c in cheb_polynomials[:K]])
         self.register_buffer("cheb_stack", cp.contiguous(), persistent=False)
+        # union support of T_0..T_{K-1} (elementwise recurrence => support of L~ u I, quirk 4)
+        csc_ptr, csc_row, csr_ptr, csr_col = support_index(cp)
+        self.register_buffer("csc_ptr", csc_ptr, persistent=False)
+        self.register_buffer("csc_row", csc_row, persistent=False)
+        self.register_buffer("csr_ptr", csr_ptr, persistent=False)
+        self.register_buffer("csr_col", csr_col, persistent=False)
+
+    def graph(self, adj_pa):
+        return {"cheb": self.cheb_stack, "adj_pa": adj_pa, "csc_ptr": self.csc_ptr, "csc_row": self.csc_row,
+                "csr_ptr": self.csr_ptr, "csr_col": self.csr_col}
 
     @property
     def cheb_polynomials(self):
         return list(self.cheb_stack.unbind(0))
+
+
+def support_index(cheb_stack):
+    """int32 CSC (per destination column j: source rows i) and CSR (per row i: columns j)
+    of the union support of the stacked Chebyshev polynomials (K,N,N)."""
+    nz = (cheb_stack != 0).any(dim=0)
+    N = nz.shape[0]
+    cols = [torch.nonzero(nz[:, j], as_tuple=False).reshape(-1) for j in range(N)]
+    rows = [torch.nonzero(nz[i, :], as_tuple=False).reshape(-1) for i in range(N)]
+
+    def pack(lists):
+        ptr = torch.zeros(N + 1, dtype=torch.int32)
+        ptr[1:] = torch.cumsum(torch.tensor([len(v) for v in lists], dtype=torch.int64), 0).to(torch.int32)
+        idx = torch.cat(lists).to(torch.int32) if lists else torch.zeros(0, dtype=torch.int32)
+        return ptr, idx
+
+    csc_ptr, csc_row = pack(cols)
+    csr_ptr, csr_col = pack(rows)
+    return csc_ptr, csc_row, csr_ptr, csr_col
 
 
 class cheb_conv(nn.Module):
@@ -147,6 +176,7 @@ class DSTAGNN_block(nn.Module):
         self.meta = dict(n_heads=n_heads, d_k=d_k, d_v=d_v, d_model=d_model, K=K, C=nb_chev_filter, drop_p=0.05)
         self.num_of_d = num_of_d
         self.nb_time_filter = nb_time_filter
+        self.sparse_cheb = True  # use the CSC/CSR support path when the support is sparse
 
     def forward(self, x, res_att):
         B, N, Fd, T = x.shape
@@ -160,8 +190,10 @@ class DSTAGNN_block(nn.Module):
         meta["train"] = bool(self.training)
         meta["seed"] = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
         names, params = zip(*self.named_parameters())
-        cheb = self.cheb_conv_SAt.cheb_stack
-        return DSTAGNNBlockFunction.apply(meta, names, x.float(), res_att, cheb, self.adj_pa, *params)
+        graph = self.cheb_conv_SAt.graph(self.adj_pa)
+        if not self.sparse_cheb:
+            graph = {"cheb": graph["cheb"], "adj_pa": graph["adj_pa"]}
+        return DSTAGNNBlockFunction.apply(meta, names, x.float(), res_att, graph, *params)
 
 
 class DSTAGNN_submodule(nn.Module):

@@ -58,6 +58,9 @@ typedef struct dstagnn_block_dims {
   int train;               /* 1: Dropout(0.05) at :234 and :221 active           */
   float drop_p;            /* 0.05 in the reference                               */
   uint64_t seed;           /* dropout RNG seed (counter-based hash, per call)     */
+  int cheb_sparse;         /* 1: aggregate over the CSC/CSR support in dstagnn_graph
+                              (T_k elementwise recurrence => ~3 nnz/column, quirk 4);
+                              0: dense (N,N) T_k.  Requires C*T <= 1024.            */
 } dstagnn_block_dims;
 
 /* Parameter pointers in state_dict order.  For the first block
@@ -107,10 +110,17 @@ typedef struct dstagnn_block_grads {
 } dstagnn_block_grads;
 
 /* Graph constants of cheb_conv_withSAt (init-time, lib/utils.py:149-203):
- * cheb = K stacked (N,N) Chebyshev polynomials T_k; adj_pa = (N,N) binary.   */
+ * cheb = K stacked (N,N) Chebyshev polynomials T_k; adj_pa = (N,N) binary.
+ * For the sparse path: the union support of T_0..T_{K-1} as CSC (per destination
+ * column j the source rows i) and CSR (per row i the columns j), int32.          */
 typedef struct dstagnn_graph {
   const float* cheb;     /* (K, N, N) */
   const float* adj_pa;   /* (N, N)    */
+  int nnz;               /* entries of the union support (0 = none given)       */
+  const int* csc_ptr;    /* (N+1) */
+  const int* csc_row;    /* (nnz) */
+  const int* csr_ptr;    /* (N+1) */
+  const int* csr_col;    /* (nnz) */
 } dstagnn_graph;
 
 /* Bytes needed for the forward->backward `save` buffer and the per-call scratch. */
@@ -136,20 +146,21 @@ int dstagnn_block_backward(const dstagnn_block_dims* d, const dstagnn_block_para
 
 /* ---- individual hot-path operators (unit-testable pieces of the block) ---- */
 
-/* cheb_conv_withSAt.forward (model/DSTAGNN_my.py:117-133), dense-T_k form.
+/* cheb_conv_withSAt.forward (model/DSTAGNN_my.py:117-133).
  *   x (B,N,F,T); sat (B,K,N,N) spatial-attention scores (pre-softmax);
  *   theta_cat (F, K*C) = [Theta_0 | ... | Theta_{K-1}]; mask_cat (K,N,N);
  *   out (B,N,C,T) = ReLU(sum_k (T_k o softmax_i(sat_k + A_pa o M_k))^T x Theta_k)
- *   save: P, W = T o P (each B*K*N*N) and xTheta (B*N*K*C*T) for the backward.  */
-int dstagnn_cheb_sat_forward(int B, int N, int F, int T, int K, int C,
+ *   sparse = 1 aggregates over g's CSC/CSR support (W unused, may be NULL);
+ *   save: P (B*K*N*N), W = T o P (dense path) and xTheta (B*N*K*C*T).           */
+int dstagnn_cheb_sat_forward(int B, int N, int F, int T, int K, int C, int sparse,
                              const float* x, const float* sat, const float* theta_cat, const float* mask_cat,
-                             const float* cheb, const float* adj_pa, float* out,
+                             const dstagnn_graph* g, float* out,
                              float* P, float* W, float* xth, void* scratch, size_t scratch_bytes,
                              dstagnn_stream_t stream);
 /* Backward: d_out (B,N,C,T) -> d_x (B,N,F,T), d_sat (B,K,N,N), d_theta_cat (F,K*C),
  * d_mask_cat (K,N,N).  `out` is the forward output (ReLU mask).                  */
-int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C,
-                              const float* x, const float* theta_cat, const float* cheb, const float* adj_pa,
+int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C, int sparse,
+                              const float* x, const float* theta_cat, const dstagnn_graph* g,
                               const float* out, const float* P, const float* W, const float* xth,
                               const float* d_out, float* d_x, float* d_sat, float* d_theta_cat, float* d_mask_cat,
                               void* scratch, size_t scratch_bytes, dstagnn_stream_t stream);

@@ -103,9 +103,12 @@ def test_gemm_transposed_batched_two_level():
 # cheb_conv_withSAt operator vs the reference's golden vectors
 # ---------------------------------------------------------------------------------------
 @pytest.mark.parametrize("name", ["g1_cheb_pems04.npz", "g5_cheb_dense.npz"])
-def test_cheb_sat_golden(golden_dir, name):
+@pytest.mark.parametrize("sparse", [0, 1])
+def test_cheb_sat_golden(golden_dir, name, sparse):
     _need_gpu()
     from dstagnn_drought_amd import _lib
+    from dstagnn_drought_amd.block_fn import graph_struct
+    from dstagnn_drought_amd.model import support_index
     lib = _lib.load()
     g = load(golden_dir, name)
     m = json.loads(str(g["meta"]))
@@ -116,6 +119,9 @@ def test_cheb_sat_golden(golden_dir, name):
     mcat = cu(np.stack([g[f"mask_{k}"] for k in range(K)]))
     cheb = cu(np.stack([g[f"cheb_{k}"] for k in range(K)]))
     apa = cu(g["adj_pa"])
+    csc_ptr, csc_row, csr_ptr, csr_col = [t.cuda() for t in support_index(cheb.cpu())]
+    gs = graph_struct({"cheb": cheb, "adj_pa": apa, "csc_ptr": csc_ptr, "csc_row": csc_row, "csr_ptr": csr_ptr,
+                       "csr_col": csr_col})
     out = torch.empty(B, N, C, T, device="cuda")
     P = torch.empty(B, K, N, N, device="cuda")
     W = torch.empty_like(P)
@@ -123,8 +129,9 @@ def test_cheb_sat_golden(golden_dir, name):
     ws = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
     st = _lib.stream_handle()
     pt = _lib.ptr
-    _lib.check(lib.dstagnn_cheb_sat_forward(B, N, F, T, K, C, pt(x), pt(sat), pt(thcat), pt(mcat), pt(cheb), pt(apa),
-                                            pt(out), pt(P), pt(W), pt(xth), pt(ws), ws.numel(), st), "cheb fwd")
+    _lib.check(lib.dstagnn_cheb_sat_forward(B, N, F, T, K, C, sparse, pt(x), pt(sat), pt(thcat), pt(mcat),
+                                            ctypes.byref(gs), pt(out), pt(P), pt(W), pt(xth), pt(ws), ws.numel(), st),
+               "cheb fwd")
     torch.cuda.synchronize()
     close(out, g["out"], what="out")
     dout = cu(g["g_out"])
@@ -132,9 +139,9 @@ def test_cheb_sat_golden(golden_dir, name):
     dsat = torch.empty_like(sat)
     dth = torch.empty_like(thcat)
     dm = torch.empty_like(mcat)
-    _lib.check(lib.dstagnn_cheb_sat_backward(B, N, F, T, K, C, pt(x), pt(thcat), pt(cheb), pt(apa), pt(out), pt(P),
-                                             pt(W), pt(xth), pt(dout), pt(dx), pt(dsat), pt(dth), pt(dm), pt(ws),
-                                             ws.numel(), st), "cheb bwd")
+    _lib.check(lib.dstagnn_cheb_sat_backward(B, N, F, T, K, C, sparse, pt(x), pt(thcat), ctypes.byref(gs), pt(out),
+                                             pt(P), pt(W), pt(xth), pt(dout), pt(dx), pt(dsat), pt(dth), pt(dm),
+                                             pt(ws), ws.numel(), st), "cheb bwd")
     torch.cuda.synchronize()
     close(dx, g["grad_x"], what="grad_x")
     close(dsat, g["grad_spatial_attention"], what="grad_sat")
@@ -232,8 +239,9 @@ def _oracle_case(B, N, T, K, h, D, dk, C, first, res_kind, seed, train=False):
     return ref, p, x, res, cheb, torch.from_numpy(pa).float(), dict(n_heads=h, d_k=dk, d_v=dk, K=K), gen
 
 
-@pytest.mark.parametrize("first,res_kind", [(False, 1), (True, 0), (False, 2)])
-def test_block_vs_oracle_pems08_geometry(first, res_kind):
+@pytest.mark.parametrize("first,res_kind,sparse", [(False, 1, True), (True, 0, True), (False, 2, True),
+                                                   (False, 1, False)])
+def test_block_vs_oracle_pems08_geometry(first, res_kind, sparse):
     _need_gpu()
     import dstagnn_drought_amd as D_
     B, N, T, K, h, D, dk, C = 2, 170, 12, 3, 3, 512, 32, 32
@@ -245,6 +253,7 @@ def test_block_vs_oracle_pems08_geometry(first, res_kind):
     blk = D_.DSTAGNN_block("cpu", F, F, K, C, C, 1, cheb, apa, apa, N, T, D, dk, dk, h)
     blk.load_state_dict(p)
     blk = blk.cuda().eval()
+    blk.sparse_cheb = sparse
     xg = x.cuda().requires_grad_(True)
     rg = res.cuda().requires_grad_(True) if torch.is_tensor(res) else 0
     out, re_at = blk(xg, rg)
