@@ -72,6 +72,14 @@ struct KIdx {
   int32_t s0 = 0, s1 = 0;
 };
 
+// largest |offset| an index map produces over [0, count)
+inline int64_t idx_span(const Idx2& x, int64_t count) {
+  if (count <= 0) return 0;
+  if (!x.two) return std::llabs(x.s0) * (count - 1);
+  const int64_t d = x.f.d;
+  return std::llabs(x.s0) * (std::min<int64_t>(d, count) - 1) + std::llabs(x.s1) * ((count - 1) / d);
+}
+
 inline bool make_kidx(const Idx2& x, int64_t K, KIdx* out) {
   KIdx k;
   int64_t maxoff;

@@ -78,45 +78,48 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
     if (B_NC) { b_nl[j] = e % BN; b_kl[j] = e / BN; }
     else      { b_kl[j] = e % BK; b_nl[j] = e / BK; }
   }
-  const float* pa[LA];
-  const float* pb[LB];
+  // per-element row / column offsets as int32 from the (wave-uniform) operand bases:
+  // the host guarantees every offset fits (check_span), halving the pointer registers
+  int32_t ao[LA], bo[LB];
 #pragma unroll
   for (int j = 0; j < LA; ++j) {
     const int m = m0 + a_ml[j];
-    pa[j] = A + (m < g.M ? ioff(g.am, m) : 0);  // clamped: row 0 is always valid
+    ao[j] = m < g.M ? (int32_t)ioff(g.am, m) : 0;  // clamped: row 0 is always valid
   }
 #pragma unroll
   for (int j = 0; j < LB; ++j) {
     const int n = n0 + b_nl[j];
-    pb[j] = Bp + (n < g.N ? ioff(g.bn, n) : 0);
+    bo[j] = n < g.N ? (int32_t)ioff(g.bn, n) : 0;
   }
 
-  float ra[LA], rb[LB];
+  // Two register sets: the loads of tile t+2 are issued while tile t is consumed, so every
+  // global load has two k-tiles of MFMA work to arrive (latency under load ~1-2 us).
+  float ra0[LA], rb0[LB], ra1[LA], rb1[LB];
   // Rows m >= M / columns n >= N read row/column 0 (valid memory): they only feed C
   // rows/columns the epilogue never stores, so they need no masking.  k >= kend must
   // read as 0; that happens only in the last k-tile, handled by a uniform branch so the
   // full tiles issue all their loads back to back with no per-element predicate (a
   // predicated load is sunk into an exec-masked region and waited on alone).
-  auto load_tile = [&](int k0) {
+  auto load_tile = [&](int k0, float (&ra)[LA], float (&rb)[LB]) {
     if (k0 + BK <= kend) {
 #pragma unroll
-      for (int j = 0; j < LA; ++j) ra[j] = pa[j][koff(g.ak, k0 + a_kl[j])];
+      for (int j = 0; j < LA; ++j) ra[j] = A[ao[j] + koff(g.ak, k0 + a_kl[j])];
 #pragma unroll
-      for (int j = 0; j < LB; ++j) rb[j] = pb[j][koff(g.bk, k0 + b_kl[j])];
+      for (int j = 0; j < LB; ++j) rb[j] = Bp[bo[j] + koff(g.bk, k0 + b_kl[j])];
     } else {
 #pragma unroll
       for (int j = 0; j < LA; ++j) {
         const int k = k0 + a_kl[j];
-        ra[j] = k < kend ? pa[j][koff(g.ak, k)] : 0.f;
+        ra[j] = k < kend ? A[ao[j] + koff(g.ak, k)] : 0.f;
       }
 #pragma unroll
       for (int j = 0; j < LB; ++j) {
         const int k = k0 + b_kl[j];
-        rb[j] = k < kend ? pb[j][koff(g.bk, k)] : 0.f;
+        rb[j] = k < kend ? Bp[bo[j] + koff(g.bk, k)] : 0.f;
       }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const float (&ra)[LA], const float (&rb)[LB]) {
 #pragma unroll
     for (int j = 0; j < LA; ++j) As[buf][a_kl[j]][a_ml[j]] = ra[j];
 #pragma unroll
@@ -131,18 +134,8 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if (ntiles > 0) {
-    load_tile(kbeg);
-    store_tile(0);
-    __syncthreads();
-  }
   const int lr = lane & 31, lk = lane >> 5;
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-#ifndef DSTAGNN_ABLATE_LOADS
-    if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BK);
-#endif
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       float a[WM], b[WN];
@@ -160,7 +153,25 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
 #endif
     }
-    if (t + 1 < ntiles) store_tile(cur ^ 1);
+  };
+
+  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (ntiles > 0) load_tile(kbeg, ra0, rb0);
+  if (ntiles > 1) load_tile(kbeg + BK, ra1, rb1);
+  if (ntiles > 0) {
+    store_tile(0, ra0, rb0);
+    __syncthreads();
+  }
+  for (int t = 0; t < ntiles; t += 2) {
+    // LDS buffer 0 holds tile t; registers set 1 hold (or await) tile t+1
+    if (t + 2 < ntiles) load_tile(kbeg + (t + 2) * BK, ra0, rb0);
+    compute(0);
+    if (t + 1 < ntiles) store_tile(1, ra1, rb1);
+    __syncthreads();
+    if (t + 1 >= ntiles) break;
+    if (t + 3 < ntiles) load_tile(kbeg + (t + 3) * BK, ra1, rb1);
+    compute(1);
+    if (t + 2 < ntiles) store_tile(0, ra0, rb0);
     __syncthreads();
   }
 
@@ -253,8 +264,10 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   k.M = g.M; k.N = g.N; k.K = g.K; k.batch = g.batch;
   k.A = g.A + g.a_off; k.am = g.am; k.az = g.az;
   k.B = g.B + g.b_off; k.bn = g.bn; k.bz = g.bz;
-  if (!make_kidx(g.ak, g.K, &k.ak) || !make_kidx(g.bk, g.K, &k.bk)) {
-    set_last_error("gemm: k-dimension offsets exceed int32");
+  if (!make_kidx(g.ak, g.K, &k.ak) || !make_kidx(g.bk, g.K, &k.bk) ||
+      idx_span(g.am, g.M) + idx_span(g.ak, g.K) >= (1ll << 31) ||
+      idx_span(g.bn, g.N) + idx_span(g.bk, g.K) >= (1ll << 31)) {
+    set_last_error("gemm: operand offsets exceed int32 (split the batch)");
     return DSTAGNN_E_SHAPE;
   }
   k.C = g.C + g.c_off; k.cm = g.cm; k.cn = g.cn; k.cz = g.cz;
