@@ -92,15 +92,13 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
     bo[j] = n < g.N ? (int32_t)ioff(g.bn, n) : 0;
   }
 
-  // Two register sets: the loads of tile t+2 are issued while tile t is consumed, so every
-  // global load has two k-tiles of MFMA work to arrive (latency under load ~1-2 us).
-  float ra0[LA], rb0[LB], ra1[LA], rb1[LB];
+  float ra[LA], rb[LB];
   // Rows m >= M / columns n >= N read row/column 0 (valid memory): they only feed C
   // rows/columns the epilogue never stores, so they need no masking.  k >= kend must
   // read as 0; that happens only in the last k-tile, handled by a uniform branch so the
   // full tiles issue all their loads back to back with no per-element predicate (a
   // predicated load is sunk into an exec-masked region and waited on alone).
-  auto load_tile = [&](int k0, float (&ra)[LA], float (&rb)[LB]) {
+  auto load_tile = [&](int k0) {
     if (k0 + BK <= kend) {
 #pragma unroll
       for (int j = 0; j < LA; ++j) ra[j] = A[ao[j] + koff(g.ak, k0 + a_kl[j])];
@@ -119,7 +117,7 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
       }
     }
   };
-  auto store_tile = [&](int buf, const float (&ra)[LA], const float (&rb)[LB]) {
+  auto store_tile = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < LA; ++j) As[buf][a_kl[j]][a_ml[j]] = ra[j];
 #pragma unroll
@@ -134,8 +132,18 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (ntiles > 0) {
+    load_tile(kbeg);
+    store_tile(0);
+    __syncthreads();
+  }
   const int lr = lane & 31, lk = lane >> 5;
-  auto compute = [&](int cur) {
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+#ifndef DSTAGNN_ABLATE_LOADS
+    if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BK);
+#endif
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       float a[WM], b[WN];
@@ -153,25 +161,7 @@ __device__ __forceinline__ void gemm_f32_body(const GemmK& g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
 #endif
     }
-  };
-
-  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if (ntiles > 0) load_tile(kbeg, ra0, rb0);
-  if (ntiles > 1) load_tile(kbeg + BK, ra1, rb1);
-  if (ntiles > 0) {
-    store_tile(0, ra0, rb0);
-    __syncthreads();
-  }
-  for (int t = 0; t < ntiles; t += 2) {
-    // LDS buffer 0 holds tile t; registers set 1 hold (or await) tile t+1
-    if (t + 2 < ntiles) load_tile(kbeg + (t + 2) * BK, ra0, rb0);
-    compute(0);
-    if (t + 1 < ntiles) store_tile(1, ra1, rb1);
-    __syncthreads();
-    if (t + 1 >= ntiles) break;
-    if (t + 3 < ntiles) load_tile(kbeg + (t + 3) * BK, ra1, rb1);
-    compute(1);
-    if (t + 2 < ntiles) store_tile(0, ra0, rb0);
+    if (t + 1 < ntiles) store_tile(cur ^ 1);
     __syncthreads();
   }
 

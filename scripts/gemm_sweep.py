@@ -40,13 +40,15 @@ SHAPES = [
 ]
 
 
-def child(iters):
+def child(iters, only=None):
     import torch
     from dstagnn_drought_amd import _lib
     lib = _lib.load()
     ws = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
     res = {}
     for name, M, N, K, batch, akc, bnc in SHAPES:
+        if only and name not in only.split(","):
+            continue
         A = torch.randn(batch, M, K, device="cuda") if akc else torch.randn(batch, K, M, device="cuda")
         B = torch.randn(batch, K, N, device="cuda") if bnc else torch.randn(batch, N, K, device="cuda")
         C = torch.empty(batch, M, N, device="cuda")
@@ -84,9 +86,10 @@ def main():
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--configs", default="auto:16,auto:32,0:32,1:32,2:32,3:32,4:32,0:16,1:16")
+    ap.add_argument("--only", default=None)
     args = ap.parse_args()
     if args.child:
-        child(args.iters)
+        child(args.iters, args.only)
         return
     table = {}
     for spec in args.configs.split(","):
