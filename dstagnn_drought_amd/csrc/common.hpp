@@ -80,6 +80,15 @@ inline int64_t idx_span(const Idx2& x, int64_t count) {
   return std::llabs(x.s0) * (std::min<int64_t>(d, count) - 1) + std::llabs(x.s1) * ((count - 1) / d);
 }
 
+// most negative offset of the map over [0, count) (0 when all strides are >= 0)
+inline int64_t idx_min(const Idx2& x, int64_t count) {
+  if (count <= 0) return 0;
+  if (!x.two) return std::min<int64_t>(0, x.s0 * (count - 1));
+  const int64_t d = x.f.d;
+  return std::min<int64_t>(0, x.s0 * (std::min<int64_t>(d, count) - 1)) +
+         std::min<int64_t>(0, x.s1 * ((count - 1) / d));
+}
+
 inline bool make_kidx(const Idx2& x, int64_t K, KIdx* out) {
   KIdx k;
   int64_t maxoff;
@@ -101,6 +110,51 @@ __device__ __forceinline__ int32_t koff(const KIdx& m, uint32_t i) {
   const uint32_t q = (__umulhi(i, m.m) + i) >> m.s;
   const uint32_t r = i - q * m.d;
   return (int32_t)r * m.s0 + (int32_t)q * m.s1;
+}
+
+// Branch-free 64-bit variant for batch (z) maps, same encoding as KIdx.
+struct ZIdx {
+  uint32_t d = 0x80000000u, m = 1, s = 31;
+  int64_t s0 = 0, s1 = 0;
+};
+inline ZIdx make_zidx(const Idx2& x) {
+  ZIdx z;
+  if (x.two) { z.d = x.f.d; z.m = x.f.m; z.s = x.f.s; }
+  z.s0 = x.s0;
+  z.s1 = x.s1;
+  return z;
+}
+__device__ __forceinline__ int64_t zoff(const ZIdx& m, uint32_t i) {
+  const uint32_t q = (__umulhi(i, m.m) + i) >> m.s;
+  const uint32_t r = i - q * m.d;
+  return (int64_t)r * m.s0 + (int64_t)q * m.s1;
+}
+
+// ---------------------------------------------------------------------------------
+// Kernel-argument fetch in ONE memory round.  The kernarg segment is cold at every
+// launch (~1000 cycles per access round) and hipcc issues a large struct's s_loads in
+// several dependent rounds (7 for the GEMM descriptor).  Instead every lane loads one
+// dword of the struct (one or two vector loads, a single round) and v_readlane puts each
+// dword back into an SGPR, so the compiler still sees wave-uniform values.
+// ---------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T load_args(const T& in) {
+  constexpr int NW = (int)((sizeof(T) + 3) / 4);
+  static_assert(NW <= 128, "load_args: struct larger than 512 bytes");
+  static_assert(sizeof(T) % 4 == 0, "load_args: struct size must be a multiple of 4");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&in);
+  const int lane = (int)(threadIdx.x & 63);
+  const uint32_t v0 = src[lane < NW ? lane : NW - 1];
+  uint32_t v1 = 0;
+  if (NW > 64) v1 = src[lane + 64 < NW ? lane + 64 : NW - 1];
+  union U {
+    T t;
+    uint32_t w[NW];
+    __device__ U() {}
+  } u;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) u.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)(i < 64 ? v0 : v1), i & 63);
+  return u.t;
 }
 
 // ---------------------------------------------------------------------------------

@@ -277,13 +277,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
 // =====================================================================================
 // reductions
 // =====================================================================================
-// stage 1: in viewed as (A, E) rows (E = O*I contiguous per row a).
-// part[p][e] = sum over the p-th chunk of rows of in[a][e] (* in2[a][e]).
-// E <= 256: the block is R' = 256/E row-lanes x E columns (consecutive threads read
-// consecutive addresses), combined through LDS; E > 256: threads stride over e.
+// stage 1: in viewed as (A, E) rows, E = O*I contiguous per row a.
+// part[p][o] = sum over the p-th chunk of rows, sum_i in[a][o*I+i] (* in2).
+// Column sums land in LDS (colv[E], dynamic), then each output folds its I columns, so
+// stage 2 reads a compact (P, O) slab.  E <= 256: the block is R' = 256/E row-lanes x E
+// columns (consecutive threads read consecutive addresses); E > 256: threads stride e.
 __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ in, const float* __restrict__ in2,
-                                                     int64_t A, int E, int64_t achunk, float* __restrict__ part) {
+                                                     int64_t A, int O, int I, int64_t achunk,
+                                                     float* __restrict__ part) {
+  extern __shared__ float colv[];
   __shared__ float red[256];
+  const int E = O * I;
   const int p = blockIdx.x;
   const int64_t a0 = (int64_t)p * achunk, a1 = min(A, a0 + achunk);
   const int t = threadIdx.x;
@@ -305,40 +309,50 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ i
     if (t < E) {
       float tot = 0.f;
       for (int q = 0; q < R; ++q) tot += red[q * E + t];
-      part[(int64_t)p * E + t] = tot;
+      colv[t] = tot;
     }
   } else {
     for (int e = t; e < E; e += 256) {
       float s = 0.f;
-      for (int64_t aa = a0; aa < a1; ++aa) {
-        float v = in[aa * E + e];
-        if (in2) v *= in2[aa * E + e];
-        s += v;
+      if (in2) {
+#pragma unroll 4
+        for (int64_t aa = a0; aa < a1; ++aa) s += in[aa * E + e] * in2[aa * E + e];
+      } else {
+#pragma unroll 4
+        for (int64_t aa = a0; aa < a1; ++aa) s += in[aa * E + e];
       }
-      part[(int64_t)p * E + e] = s;
+      colv[e] = s;
     }
   }
-}
-// stage 2: one workgroup per output o: out[o] = beta*out[o] + sum_p sum_i part[p][o*I + i]
-__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int P, int O, int I,
-                                                     float* __restrict__ out, int64_t ostride, float beta) {
-  __shared__ float red[256];
-  const int o = blockIdx.x;
-  float s = 0.f;
-  const int n = P * I;
-  for (int q = threadIdx.x; q < n; q += 256) {
-    const int pp = q / I, i = q % I;
-    s += part[((int64_t)pp * O + o) * I + i];
-  }
-  red[threadIdx.x] = s;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+  for (int o = t; o < O; o += 256) {
+    float s = 0.f;
+    for (int i = 0; i < I; ++i) s += colv[o * I + i];
+    part[(int64_t)p * O + o] = s;
+  }
+}
+// stage 2: out[o] = beta*out[o] + sum_p part[p][o].  512 threads = OL output lanes x PG
+// row groups (coalesced along o), LDS tree over the groups (fixed order: deterministic).
+__global__ __launch_bounds__(512) void colsum_stage2(const float* __restrict__ part, int P, int O, int OL,
+                                                     float* __restrict__ out, int64_t ostride, float beta) {
+  __shared__ float red[512];
+  const int t = threadIdx.x;
+  const int PG = 512 / OL, g = t / OL, l = t % OL;
+  const int o = blockIdx.x * OL + l;
+  float s = 0.f;
+  if (o < O) {
+#pragma unroll 4
+    for (int pp = g; pp < P; pp += PG) s += part[(int64_t)pp * O + o];
+  }
+  red[t] = s;
+  __syncthreads();
+  for (int w = PG >> 1; w > 0; w >>= 1) {
+    if (g < w) red[t] += red[t + w * OL];
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (g == 0 && o < O) {
     float* d = out + (int64_t)o * ostride;
-    *d = (beta != 0.f ? beta * *d : 0.f) + red[0];
+    *d = (beta != 0.f ? beta * *d : 0.f) + red[l];
   }
 }
 
@@ -712,16 +726,22 @@ int op_ln_bwd(const LnBwd& a, hipStream_t st) {
 int op_colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
               float* part, size_t part_floats, hipStream_t st) {
   const int E = O * I;
-  // ~4K elements per stage-1 workgroup, at most 2048 partial rows
-  int64_t P = std::max<int64_t>(1, std::min<int64_t>(2048, cdiv64(A * E, 4096)));
+  if (E > 16384) { set_last_error("colsum: O*I > 16384"); return DSTAGNN_E_SHAPE; }
+  if (A <= 0) return 0;
+  // ~4K elements per stage-1 workgroup, at most 1024 partial rows
+  int64_t P = std::max<int64_t>(1, std::min<int64_t>(1024, cdiv64(A * E, 4096)));
   P = std::min<int64_t>(P, A);
-  while (P > 1 && (size_t)P * E > part_floats) P /= 2;
-  if ((size_t)P * E > part_floats) { set_last_error("colsum: scratch too small"); return DSTAGNN_E_SPACE; }
+  while (P > 1 && (size_t)P * O > part_floats) P /= 2;
+  if ((size_t)P * O > part_floats) { set_last_error("colsum: scratch too small"); return DSTAGNN_E_SPACE; }
   const int64_t achunk = cdiv64(A, P);
   P = cdiv64(A, achunk);
-  hipLaunchKernelGGL(colsum_stage1, dim3((unsigned)P), dim3(256), 0, st, in, in2, A, E, achunk, part);
+  hipLaunchKernelGGL(colsum_stage1, dim3((unsigned)P), dim3(256), (size_t)E * sizeof(float), st, in, in2, A, O, I,
+                     achunk, part);
   DS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)O), dim3(256), 0, st, part, (int)P, O, I, out, ostride, beta);
+  int OL = 1;
+  while (OL < O && OL < 64) OL <<= 1;
+  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)cdiv64(O, OL)), dim3(512), 0, st, part, (int)P, O, OL, out,
+                     ostride, beta);
   DS_CHECK_LAUNCH();
   return 0;
 }

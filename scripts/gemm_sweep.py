@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Tuning sweep for the strided f32-MFMA GEMM (dstagnn_gemm_f32) on the DSTAGNN block's
-GEMM shapes (PEMS08, B=32).  Each (tile config, BK) runs in its own subprocess because
-the overrides (DSTAGNN_GEMM_CFG / DSTAGNN_GEMM_BK) are read once per process.
+GEMM shapes (PEMS08, B=32).  Each (tile config, implementation) runs in its own subprocess
+because the overrides (DSTAGNN_GEMM_CFG / DSTAGNN_GEMM_IMPL) are read once per process;
+every run is checked against torch.bmm.
 
     python scripts/gemm_sweep.py            # full sweep, prints a table
     python scripts/gemm_sweep.py --child    # (internal) one config
@@ -38,6 +39,16 @@ SHAPES = [
     ("gtu_dW7", 64, 224, 32640, 1, False, False),
     ("fcmy_dW", 12, 24, 174080, 1, False, True),
 ]
+# steady-state probes (not block shapes): large square GEMMs, all operand layouts
+BIG = [
+    ("big_tn", 4096, 4096, 2048, 1, True, False),
+    ("big_nn", 4096, 4096, 2048, 1, False, False),
+    ("big_nt", 4096, 4096, 2048, 1, False, True),
+]
+# occupancy probes: 64x64 tiles, N=512 (8 n-tiles), K=384 -> M/64*8 blocks
+BIG += [(f"occ{m // 64 * 8}", m, 512, 384, 1, False, False) for m in (2048, 4096, 6144, 8192, 16384, 32768)]
+if os.environ.get("DSTAGNN_SWEEP_BIG"):
+    SHAPES = SHAPES + BIG
 
 
 def child(iters, only=None):
@@ -85,20 +96,29 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--configs", default="auto:16,auto:32,0:32,1:32,2:32,3:32,4:32,0:16,1:16")
+    # spec = <tile config | auto>:<impl: 1 LDS-DMA pipeline, 0 register-staged>
+    ap.add_argument("--configs", default="auto:1,auto:0,0:1,0:0,1:1,1:0,2:1,3:1,3:0,4:1")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--big", action="store_true", help="add large square steady-state probes")
     args = ap.parse_args()
+    if args.big:
+        os.environ["DSTAGNN_SWEEP_BIG"] = "1"
+        global SHAPES
+        SHAPES = SHAPES + BIG
     if args.child:
         child(args.iters, args.only)
         return
     table = {}
     for spec in args.configs.split(","):
-        cfg, bk = spec.split(":")
-        env = dict(os.environ, DSTAGNN_GEMM_BK=bk)
+        cfg, impl = spec.split(":")
+        env = dict(os.environ, DSTAGNN_GEMM_IMPL=impl)
         if cfg != "auto":
             env["DSTAGNN_GEMM_CFG"] = cfg
-        env["DSTAGNN_GEMM_CHECK"] = "1" if (spec == "auto:32" and not os.environ.get("DSTAGNN_NOCHECK")) else ""
-        out = subprocess.run([sys.executable, __file__, "--child", "--iters", str(args.iters)], env=env,
+        env["DSTAGNN_GEMM_CHECK"] = "" if os.environ.get("DSTAGNN_NOCHECK") else "1"
+        cmd = [sys.executable, __file__, "--child", "--iters", str(args.iters)]
+        if args.only:
+            cmd += ["--only", args.only]
+        out = subprocess.run(cmd, env=env,
                              capture_output=True, text=True, timeout=300)
         if out.returncode != 0:
             print(spec, "FAILED", out.stderr[-2000:], flush=True)
@@ -108,6 +128,8 @@ def main():
     specs = list(table)
     print(f"{'shape':12s} {'GFLOP':>7s} " + " ".join(f"{s:>9s}" for s in specs) + "   best TF/s")
     for name, M, N, K, batch, _, _ in SHAPES:
+        if args.only and name not in args.only.split(","):
+            continue
         gf = 2.0 * M * N * K * batch / 1e9
         row = [table[s].get(name, float('nan')) for s in specs]
         best = min(row)

@@ -13,6 +13,9 @@ run() {
   echo "== $name rc=$rc"
   tail -n 25 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "FATAL: $name rc=$rc, stopping"; exit $rc; fi
+  if grep -qE "illegal memory access|hipErrorIllegalAddress|Memory access fault|HSA_STATUS_ERROR" "gpurun_out/$name.log"; then
+    echo "FATAL: $name reported a GPU fault, stopping"; exit 99
+  fi
   return 0
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
