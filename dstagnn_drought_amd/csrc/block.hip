@@ -14,6 +14,8 @@
 #include <string>
 
 #include "common.hpp"
+#include <initializer_list>
+#include <utility>
 #include "ops.hpp"
 
 static thread_local std::string g_last_error;
@@ -506,8 +508,19 @@ struct Bwd {
   hipStream_t st;
 
   int colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out) {
+    (void)in2;
     if (!out) return 0;
-    return op_colsum(in, in2, A, O, I, out, 1, 0.f, w.part, kPart, st);
+    return op_colsum(in, A, O, I, out, 1, 0.f, w.part, kPart, st);
+  }
+  // several same-shape column sums in one launch pair; null outputs are skipped
+  int colsums(std::initializer_list<std::pair<const float*, float*>> io, int64_t A, int O, int I) {
+    const float* ins[4];
+    float* outs[4];
+    int n = 0;
+    for (const auto& q : io)
+      if (q.second && n < 4) { ins[n] = q.first; outs[n] = q.second; ++n; }
+    if (!n) return 0;
+    return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, w.part, kPart, st);
   }
   int gemm(const Gemm& g) { return run_gemm(g, w.gemm_ws, kGemmWs, st); }
 
@@ -520,12 +533,8 @@ struct Bwd {
     t.dout = dout; t.gcontrib = w.gcon; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
     t.rcontrib = w.bcon; t.dres = w.gpre;  // gpre reused as scratch until the cheb stage
     DS_TRY(op_tail_bwd(t, st));
-    DS_TRY(colsum(w.gcon, nullptr, m.BN, m.C, m.T, gd.ln_g));
-    DS_TRY(colsum(dout, nullptr, m.BN, m.C, m.T, gd.ln_b));
-    if (m.first) {
-      DS_TRY(colsum(w.bcon, nullptr, m.BN, m.C, m.T, gd.res_w));
-      DS_TRY(colsum(w.gpre, nullptr, m.BN, m.C, m.T, gd.res_b));
-    }
+    DS_TRY(colsums({{w.gcon, gd.ln_g}, {dout, gd.ln_b}, {w.bcon, m.first ? gd.res_w : nullptr},
+                    {w.gpre, m.first ? gd.res_b : nullptr}}, m.BN, m.C, m.T));
     // fcmy backward
     {
       Gemm g;  // dG = dtc @ W
@@ -637,8 +646,7 @@ struct Bwd {
       a.dx = w.dY; a.dxrow = idx1(m.D);
       a.gcontrib = w.gcon; a.bcontrib = w.bcon;
       DS_TRY(op_ln_bwd(a, st));
-      DS_TRY(colsum(w.gcon, nullptr, m.BN, m.D, 1, gd.embS_g));
-      DS_TRY(colsum(w.bcon, nullptr, m.BN, m.D, 1, gd.embS_b));
+      DS_TRY(colsums({{w.gcon, gd.embS_g}, {w.bcon, gd.embS_b}}, m.BN, m.D, 1));
       if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, st));
     }
     return 0;
@@ -675,8 +683,7 @@ struct Bwd {
       a.dx = w.dU; a.dxrow = idx1(N);
       a.gcontrib = w.gcon; a.bcontrib = nullptr;
       DS_TRY(op_ln_bwd(a, st));
-      DS_TRY(colsum(w.gcon, nullptr, m.BFT, m.N, 1, gd.tat_ln_g));
-      DS_TRY(colsum(w.dO, nullptr, m.BFT, m.N, 1, gd.tat_ln_b));
+      DS_TRY(colsums({{w.gcon, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
     }
     {  // dctx = dU Wfc
       Gemm g;
@@ -729,8 +736,7 @@ struct Bwd {
       a.dx = w.du_et; a.dxrow = idx1(N);
       a.gcontrib = w.gcon; a.bcontrib = nullptr;
       DS_TRY(op_ln_bwd(a, st));
-      DS_TRY(colsum(w.gcon, nullptr, (int64_t)m.B * m.T, m.N, 1, gd.embT_g));
-      DS_TRY(colsum(w.dU, nullptr, (int64_t)m.B * m.T, m.N, 1, gd.embT_b));
+      DS_TRY(colsums({{w.gcon, gd.embT_g}, {w.dU, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
       if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, st));
       DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
     } else {

@@ -135,7 +135,8 @@ __device__ __forceinline__ int64_t zoff(const ZIdx& m, uint32_t i) {
 // launch (~1000 cycles per access round) and hipcc issues a large struct's s_loads in
 // several dependent rounds (7 for the GEMM descriptor).  Instead every lane loads one
 // dword of the struct (one or two vector loads, a single round) and v_readlane puts each
-// dword back into an SGPR, so the compiler still sees wave-uniform values.
+// dword back into an SGPR, so the compiler still sees wave-uniform values.  Call it first
+// thing in the kernel, with every lane active (block sizes are multiples of 64).
 // ---------------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ T load_args(const T& in) {

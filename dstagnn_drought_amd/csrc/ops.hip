@@ -277,95 +277,91 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
 // =====================================================================================
 // reductions
 // =====================================================================================
-// stage 1: in viewed as (A, E) rows, E = O*I contiguous per row a.
-// part[p][o] = sum over the p-th chunk of rows, sum_i in[a][o*I+i] (* in2).
+// Column sums of up to 4 same-shape sources in one launch pair (deterministic: fixed
+// reduction order, no atomics).
+// stage 1: each source viewed as (A, E) rows, E = O*I contiguous per row a.
+// part[p][s*O + o] = sum over the p-th chunk of rows, sum_i in_s[a][o*I+i].
 // Column sums land in LDS (colv[E], dynamic), then each output folds its I columns, so
-// stage 2 reads a compact (P, O) slab.  E <= 256: the block is R' = 256/E row-lanes x E
-// columns (consecutive threads read consecutive addresses); E > 256: threads stride e.
-__global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ in, const float* __restrict__ in2,
-                                                     int64_t A, int O, int I, int64_t achunk,
-                                                     float* __restrict__ part) {
+// stage 2 reads a compact (P, nsrc*O) slab.  E <= 256: the block is R' = 256/E row-lanes x
+// E columns (consecutive threads read consecutive addresses); E > 256: threads stride e.
+__global__ __launch_bounds__(256) void colsum_stage1(ColsumArgs a) {
   extern __shared__ float colv[];
   __shared__ float red[256];
-  const int E = O * I;
+  const int E = a.O * a.I, OT = a.nsrc * a.O;
   const int p = blockIdx.x;
-  const int64_t a0 = (int64_t)p * achunk, a1 = min(A, a0 + achunk);
+  const int64_t a0 = (int64_t)p * a.achunk, a1 = min(a.A, a0 + a.achunk);
   const int t = threadIdx.x;
-  if (E <= 256) {
-    const int R = 256 / E;
-    const int r = t / E, e = t % E;
-    float s = 0.f;
-    if (r < R) {
-      if (in2) {
-#pragma unroll 4
-        for (int64_t aa = a0 + r; aa < a1; aa += R) s += in[aa * E + e] * in2[aa * E + e];
-      } else {
-#pragma unroll 4
-        for (int64_t aa = a0 + r; aa < a1; aa += R) s += in[aa * E + e];
+  for (int src = 0; src < a.nsrc; ++src) {
+    const float* __restrict__ in = a.in[src];
+    if (E <= 256) {
+      const int R = 256 / E;
+      const int r = t / E, e = t % E;
+      float sum = 0.f;
+      if (r < R) {
+#pragma unroll 8
+        for (int64_t aa = a0 + r; aa < a1; aa += R) sum += in[aa * E + e];
+      }
+      red[t] = sum;
+      __syncthreads();
+      if (t < E) {
+        float tot = 0.f;
+        for (int q = 0; q < R; ++q) tot += red[q * E + t];
+        colv[t] = tot;
+      }
+    } else {
+      for (int e = t; e < E; e += 256) {
+        float sum = 0.f;
+#pragma unroll 8
+        for (int64_t aa = a0; aa < a1; ++aa) sum += in[aa * E + e];
+        colv[e] = sum;
       }
     }
-    red[t] = s;
     __syncthreads();
-    if (t < E) {
-      float tot = 0.f;
-      for (int q = 0; q < R; ++q) tot += red[q * E + t];
-      colv[t] = tot;
+    for (int o = t; o < a.O; o += 256) {
+      float sum = 0.f;
+      for (int i = 0; i < a.I; ++i) sum += colv[o * a.I + i];
+      a.part[(int64_t)p * OT + src * a.O + o] = sum;
     }
-  } else {
-    for (int e = t; e < E; e += 256) {
-      float s = 0.f;
-      if (in2) {
-#pragma unroll 4
-        for (int64_t aa = a0; aa < a1; ++aa) s += in[aa * E + e] * in2[aa * E + e];
-      } else {
-#pragma unroll 4
-        for (int64_t aa = a0; aa < a1; ++aa) s += in[aa * E + e];
-      }
-      colv[e] = s;
-    }
-  }
-  __syncthreads();
-  for (int o = t; o < O; o += 256) {
-    float s = 0.f;
-    for (int i = 0; i < I; ++i) s += colv[o * I + i];
-    part[(int64_t)p * O + o] = s;
+    __syncthreads();
   }
 }
-// stage 2: out[o] = beta*out[o] + sum_p part[p][o].  512 threads = OL output lanes x PG
-// row groups (coalesced along o), LDS tree over the groups (fixed order: deterministic).
-__global__ __launch_bounds__(512) void colsum_stage2(const float* __restrict__ part, int P, int O, int OL,
-                                                     float* __restrict__ out, int64_t ostride, float beta) {
-  __shared__ float red[512];
+// stage 2: out_s[o] = beta*out_s[o] + sum_p part[p][s*O + o].  1024 threads = OL output
+// lanes x PG row groups (coalesced along o), LDS tree over the groups (fixed order).
+__global__ __launch_bounds__(1024) void colsum_stage2(ColsumArgs a) {
+  __shared__ float red[1024];
+  const int OT = a.nsrc * a.O;
   const int t = threadIdx.x;
-  const int PG = 512 / OL, g = t / OL, l = t % OL;
-  const int o = blockIdx.x * OL + l;
-  float s = 0.f;
-  if (o < O) {
-#pragma unroll 4
-    for (int pp = g; pp < P; pp += PG) s += part[(int64_t)pp * O + o];
+  const int PG = 1024 / a.OL, g = t / a.OL, l = t % a.OL;
+  const int o = blockIdx.x * a.OL + l;
+  float sum = 0.f;
+  if (o < OT) {
+#pragma unroll 8
+    for (int pp = g; pp < a.P; pp += PG) sum += a.part[(int64_t)pp * OT + o];
   }
-  red[t] = s;
+  red[t] = sum;
   __syncthreads();
   for (int w = PG >> 1; w > 0; w >>= 1) {
-    if (g < w) red[t] += red[t + w * OL];
+    if (g < w) red[t] += red[t + w * a.OL];
     __syncthreads();
   }
-  if (g == 0 && o < O) {
-    float* d = out + (int64_t)o * ostride;
-    *d = (beta != 0.f ? beta * *d : 0.f) + red[l];
+  if (g == 0 && o < OT) {
+    const int src = o / a.O, oo = o - src * a.O;
+    float* d = a.out[src] + (int64_t)oo * a.ostride;
+    *d = (a.beta != 0.f ? a.beta * *d : 0.f) + red[l];
   }
 }
 
-// out[a][i] = beta*out + sum_m in[a][m][i]
+// out[a][i] = beta*out + sum_m in[a][m][i]; grid (i blocks, a)
 __global__ __launch_bounds__(256) void sum_middle_kernel(const float* __restrict__ in, int64_t A, int Mm, int64_t I,
                                                          float* __restrict__ out, float beta) {
-  const int64_t total = A * I;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t a = idx / I, i = idx % I;
+  const int64_t a = blockIdx.y;
+  const float* src = in + a * Mm * I;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int m = 0; m < Mm; ++m) s += in[(a * Mm + m) * I + i];
-    out[idx] = (beta != 0.f ? beta * out[idx] : 0.f) + s;
+#pragma unroll 4
+    for (int m = 0; m < Mm; ++m) s += src[(int64_t)m * I + i];
+    float* d = out + a * I + i;
+    *d = (beta != 0.f ? beta * *d : 0.f) + s;
   }
 }
 
@@ -473,52 +469,54 @@ __global__ __launch_bounds__(256) void cheb_mask_grad_kernel(ChebSm a) {
 // =====================================================================================
 // GTU gates.  conv_g layout [bn][2C][Tg], Tg = T - ks + 1; Gcat [bn][C][3T-12]
 // =====================================================================================
+// One workgroup per (b,n) row at a time (grid-stride over rows), threads over the row's
+// elements with 32-bit index math (no 64-bit division in the element loop).
 __global__ __launch_bounds__(256) void gate_fwd_kernel(GateArgs a) {
   const int S = 3 * a.T - 12;
-  const int64_t total = (int64_t)a.BN * a.C * S;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int s = (int)(idx % S);
-    int64_t r = idx / S;
-    int c = (int)(r % a.C);
-    int64_t bn = r / a.C;
-    int gi = 0, t = s;
-    while (gi < 2 && t >= a.T - 2 - 2 * gi) { t -= a.T - 2 - 2 * gi; ++gi; }
-    const int Tg = a.T - 2 - 2 * gi;
-    const float* cv = a.conv[gi] + bn * 2 * a.C * Tg;
-    float p = cv[(int64_t)c * Tg + t];
-    float q = cv[(int64_t)(a.C + c) * Tg + t];
-    a.G[idx] = tanhf(p) * (1.f / (1.f + expf(-q)));
+  const int E = a.C * S;
+  const int T0 = a.T - 2, T1 = a.T - 4;
+  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
+    float* grow = a.G + bn * E;
+    for (int e = threadIdx.x; e < E; e += 256) {
+      const int c = e / S, s = e - c * S;
+      const int gi = s < T0 ? 0 : (s < T0 + T1 ? 1 : 2);
+      const int t = gi == 0 ? s : (gi == 1 ? s - T0 : s - T0 - T1);
+      const int Tg = a.T - 2 - 2 * gi;
+      const float* cv = a.conv[gi] + bn * 2 * a.C * Tg;
+      const float p = cv[c * Tg + t];
+      const float q = cv[(a.C + c) * Tg + t];
+      grow[e] = tanhf(p) * (1.f / (1.f + __expf(-q)));
+    }
   }
 }
-
-// dconv_pad_g[bn][o][Lp], Lp = T + ks - 1, data at [ks-1, ks-1+Tg), zeros elsewhere
-__global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a, int gi) {
+__global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a) {
   const int S = 3 * a.T - 12;
-  const int ks = 3 + 2 * gi;
-  const int Tg = a.T - ks + 1;
-  const int Lp = a.T + ks - 1;
-  const int off = gi == 0 ? 0 : (gi == 1 ? a.T - 2 : 2 * a.T - 6);
-  const int64_t total = (int64_t)a.BN * 2 * a.C * Lp;
-  float* out = a.dconv_pad[gi];
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int l = (int)(idx % Lp);
-    int64_t r = idx / Lp;
-    int o = (int)(r % (2 * a.C));
-    int64_t bn = r / (2 * a.C);
-    int t = l - (ks - 1);
-    float v = 0.f;
-    if (t >= 0 && t < Tg) {
-      int c = o < a.C ? o : o - a.C;
+  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
+#pragma unroll
+    for (int gi = 0; gi < 3; ++gi) {
+      const int ks = 3 + 2 * gi;
+      const int Tg = a.T - ks + 1;
+      const int Lp = a.T + ks - 1;
+      const int off = gi == 0 ? 0 : (gi == 1 ? a.T - 2 : 2 * a.T - 6);
+      const int E = 2 * a.C * Lp;
+      float* orow = a.dconv_pad[gi] + bn * E;
       const float* cv = a.conv[gi] + bn * 2 * a.C * Tg;
-      float p = cv[(int64_t)c * Tg + t];
-      float q = cv[(int64_t)(a.C + c) * Tg + t];
-      float dg = a.dG[(bn * a.C + c) * S + off + t];
-      float th = tanhf(p), sg = 1.f / (1.f + expf(-q));
-      v = o < a.C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
+      const float* dgr = a.dG + bn * a.C * S + off;
+      for (int e = threadIdx.x; e < E; e += 256) {
+        const int o = e / Lp, l = e - o * Lp;
+        const int t = l - (ks - 1);
+        float v = 0.f;
+        if (t >= 0 && t < Tg) {
+          const int c = o < a.C ? o : o - a.C;
+          const float p = cv[c * Tg + t];
+          const float q = cv[(a.C + c) * Tg + t];
+          const float dg = dgr[c * S + t];
+          const float th = tanhf(p), sg = 1.f / (1.f + __expf(-q));
+          v = o < a.C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
+        }
+        orow[e] = v;
+      }
     }
-    out[idx] = v;
   }
 }
 
@@ -722,32 +720,43 @@ int op_ln_bwd(const LnBwd& a, hipStream_t st) {
   return 0;
 }
 
-// out[o*ostride] = beta*out + sum_{a<A, i<I} in[a][o][i] (* in2)
-int op_colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
-              float* part, size_t part_floats, hipStream_t st) {
+// out_s[o*ostride] = beta*out_s + sum_{a<A, i<I} in_s[a][o][i],  s < nsrc <= 4
+int op_colsum_multi(const float* const* ins, float* const* outs, int nsrc, int64_t A, int O, int I,
+                    int64_t ostride, float beta, float* part, size_t part_floats, hipStream_t st) {
   const int E = O * I;
+  if (nsrc < 1 || nsrc > 4) { set_last_error("colsum: 1..4 sources"); return DSTAGNN_E_ARG; }
   if (E > 16384) { set_last_error("colsum: O*I > 16384"); return DSTAGNN_E_SHAPE; }
-  if (A <= 0) return 0;
-  // ~4K elements per stage-1 workgroup, at most 1024 partial rows
-  int64_t P = std::max<int64_t>(1, std::min<int64_t>(1024, cdiv64(A * E, 4096)));
+  if (A <= 0 || O <= 0) return 0;
+  ColsumArgs a;
+  for (int q = 0; q < nsrc; ++q) { a.in[q] = ins[q]; a.out[q] = outs[q]; }
+  a.nsrc = nsrc; a.A = A; a.O = O; a.I = I; a.ostride = ostride; a.beta = beta; a.part = part;
+  // ~4K elements per stage-1 workgroup, at most 256 partial rows (stage 2's loop over
+  // the partials is latency-bound: keep it short)
+  int64_t P = std::max<int64_t>(1, std::min<int64_t>(256, cdiv64(A * E, 4096)));
   P = std::min<int64_t>(P, A);
-  while (P > 1 && (size_t)P * O > part_floats) P /= 2;
-  if ((size_t)P * O > part_floats) { set_last_error("colsum: scratch too small"); return DSTAGNN_E_SPACE; }
-  const int64_t achunk = cdiv64(A, P);
-  P = cdiv64(A, achunk);
-  hipLaunchKernelGGL(colsum_stage1, dim3((unsigned)P), dim3(256), (size_t)E * sizeof(float), st, in, in2, A, O, I,
-                     achunk, part);
+  while (P > 1 && (size_t)P * nsrc * O > part_floats) P /= 2;
+  if ((size_t)P * nsrc * O > part_floats) { set_last_error("colsum: scratch too small"); return DSTAGNN_E_SPACE; }
+  a.achunk = cdiv64(A, P);
+  a.P = (int)cdiv64(A, a.achunk);
+  hipLaunchKernelGGL(colsum_stage1, dim3((unsigned)a.P), dim3(256), (size_t)E * sizeof(float), st, a);
   DS_CHECK_LAUNCH();
-  int OL = 1;
-  while (OL < O && OL < 64) OL <<= 1;
-  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)cdiv64(O, OL)), dim3(512), 0, st, part, (int)P, O, OL, out,
-                     ostride, beta);
+  const int OT = nsrc * O;
+  a.OL = 1;
+  while (a.OL < OT && a.OL < 64) a.OL <<= 1;
+  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)cdiv64(OT, a.OL)), dim3(1024), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
+int op_colsum(const float* in, int64_t A, int O, int I, float* out, int64_t ostride, float beta, float* part,
+              size_t part_floats, hipStream_t st) {
+  return op_colsum_multi(&in, &out, 1, A, O, I, ostride, beta, part, part_floats, st);
+}
 
 int op_sum_middle(const float* in, int64_t A, int Mm, int64_t I, float* out, float beta, hipStream_t st) {
-  hipLaunchKernelGGL(sum_middle_kernel, dim3(grid1d(A * I)), dim3(256), 0, st, in, A, Mm, I, out, beta);
+  if (A <= 0 || I <= 0) return 0;
+  if (A > 65535) { set_last_error("sum_middle: A > 65535"); return DSTAGNN_E_SHAPE; }
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv64(I, 256), std::max<int64_t>(1, 2048 / A)));
+  hipLaunchKernelGGL(sum_middle_kernel, dim3(gx, (unsigned)A), dim3(256), 0, st, in, A, Mm, I, out, beta);
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -778,16 +787,13 @@ int op_cheb_mask_grad(const ChebSm& a, hipStream_t st) {
 }
 
 int op_gate_fwd(const GateArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(gate_fwd_kernel, dim3(grid1d((int64_t)a.BN * a.C * (3 * a.T - 12))), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(gate_fwd_kernel, dim3((unsigned)std::min<int64_t>(a.BN, 4096)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_gate_bwd(const GateArgs& a, hipStream_t st) {
-  for (int gi = 0; gi < 3; ++gi) {
-    int Lp = a.T + 2 + 2 * gi + 0;  // T + ks - 1
-    hipLaunchKernelGGL(gate_bwd_kernel, dim3(grid1d((int64_t)a.BN * 2 * a.C * Lp)), dim3(256), 0, st, a, gi);
-    DS_CHECK_LAUNCH();
-  }
+  hipLaunchKernelGGL(gate_bwd_kernel, dim3((unsigned)std::min<int64_t>(a.BN, 4096)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
   return 0;
 }
 

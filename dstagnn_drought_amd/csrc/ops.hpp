@@ -45,6 +45,16 @@ struct ChebSm {
   float* dmask[DSTAGNN_MAX_K] = {};
 };
 
+struct ColsumArgs {
+  const float* in[4] = {};
+  float* out[4] = {};
+  int nsrc = 1;
+  int64_t A = 0; int O = 0, I = 1;
+  int64_t achunk = 1;
+  int64_t ostride = 1; float beta = 0.f;
+  float* part = nullptr; int P = 1; int OL = 1;
+};
+
 struct GateArgs {
   int64_t BN = 0; int C = 0, T = 0;
   const float* conv[3] = {};      // [bn][2C][T-ks+1]
@@ -104,8 +114,10 @@ int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
                const float* dre, float* dqkv, float* dscore, hipStream_t st);
 int op_ln_fwd(const LnFwd& a, hipStream_t st);
 int op_ln_bwd(const LnBwd& a, hipStream_t st);
-int op_colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
-              float* part, size_t part_floats, hipStream_t st);
+int op_colsum(const float* in, int64_t A, int O, int I, float* out, int64_t ostride, float beta, float* part,
+              size_t part_floats, hipStream_t st);
+int op_colsum_multi(const float* const* ins, float* const* outs, int nsrc, int64_t A, int O, int I,
+                    int64_t ostride, float beta, float* part, size_t part_floats, hipStream_t st);
 int op_sum_middle(const float* in, int64_t A, int Mm, int64_t I, float* out, float beta, hipStream_t st);
 int op_relu_mask(const float* g, const float* y, float* out, int64_t n, hipStream_t st);
 int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st);
