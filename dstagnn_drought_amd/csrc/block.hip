@@ -103,7 +103,7 @@ constexpr size_t kGemmWs = size_t(8) << 20;   // floats (32 MB) for split-K part
 constexpr size_t kPart = size_t(2) << 20;      // floats (8 MB) for column-sum partials
 
 struct Scratch {
-  float *Wp, *thcat, *tc, *gemm_ws, *part;
+  float *Wp, *thcat, *tc, *gemm_ws, *part, *Wg[3];
   // bwd
   float *dtc, *dX, *gpre, *gcon, *bcon, *dG, *dconv[3], *dW, *dxth, *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dctx,
       *dqkv, *dscore, *du_et;
@@ -115,6 +115,7 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.part = a.take(kPart);
   s.Wp = a.take((int64_t)m.D * m.FT);
   s.thcat = a.take((int64_t)m.F * m.KC);
+  for (int g = 0; g < 3; ++g) s.Wg[g] = a.take(2 * (int64_t)m.C * m.C * m.ks[g]);
   s.tc = a.take(m.BN * m.CT);
   s.dtc = a.take(m.BN * m.CT);
   s.dX = a.take(m.BN * m.CT);
@@ -183,12 +184,12 @@ struct ChebIO {
   const dstagnn_graph* g;  // cheb (K,N,N), adj_pa, and the CSC/CSR support
   bool sparse;
   const float* thcat;      // (F, K*C)
-  float *P, *W, *xth, *X;  // W unused (null) on the sparse path
+  float *P, *W, *xth, *X;  // W unused (null) on the sparse path; xth (B,N,T,K,C), X (B,N,T,C)
 };
 
-ChebSp make_sp(int B, int N, int K, int CT, const dstagnn_graph* g) {
+ChebSp make_sp(int B, int N, int K, int C, int T, const dstagnn_graph* g) {
   ChebSp a;
-  a.B = B; a.N = N; a.K = K; a.CT = CT;
+  a.B = B; a.N = N; a.K = K; a.CT = C * T; a.C = C;
   a.csc_ptr = g->csc_ptr; a.csc_row = g->csc_row; a.csr_ptr = g->csr_ptr; a.csr_col = g->csr_col;
   a.cheb = g->cheb;
   return a;
@@ -202,18 +203,18 @@ int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
   sm.W = c.sparse ? nullptr : c.W;
   for (int k = 0; k < c.K; ++k) sm.mask[k] = c.mask[k];
   DS_TRY(op_cheb_softmax_fwd(sm, st));
-  // xth[(b,i,t),(k,c)] = sum_f x[b,i,f,t] Theta_k[f,c]
+  // xth[(b,i,t),(k,c)] = sum_f x[b,i,f,t] Theta_k[f,c]   (plain row-major (B*N*T, K*C))
   {
     Gemm g;
     g.M = c.B * c.N * c.T; g.N = (int)KC; g.K = c.F;
     g.A = c.x; g.am = idx2(T, 1, FT); g.ak = idx1(T);
     g.B = c.thcat; g.bk = idx1(KC); g.bn = idx1(1);
-    g.C = c.xth; g.cm = idx2(T, 1, KCT); g.cn = idx1(T);
+    g.C = c.xth; g.cm = idx1(KC); g.cn = idx1(1);
     DS_TRY(run_gemm(g, ws, kGemmWs, st));
   }
-  // X[b,j,(c,t)] = relu( sum_{k,i} W[b,k,i,j] xth[b,i,k,(c,t)] )
+  // X[b,j,(t,c)] = relu( sum_{k,i} W[b,k,i,j] xth[b,i,t,k,c] )
   if (c.sparse) {
-    ChebSp sp = make_sp(c.B, c.N, c.K, (int)CT, c.g);
+    ChebSp sp = make_sp(c.B, c.N, c.K, c.C, c.T, c.g);
     sp.P = c.P; sp.xth = c.xth; sp.out = c.X;
     return op_cheb_spmm_fwd(sp, st);
   }
@@ -221,7 +222,7 @@ int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
     Gemm g;
     g.M = c.N; g.N = (int)CT; g.K = c.K * c.N; g.batch = c.B;
     g.A = c.W; g.am = idx1(1); g.ak = idx2(c.N, c.N, NN); g.az = idx1(c.K * NN);
-    g.B = c.xth; g.bk = idx2(c.N, KCT, CT); g.bn = idx1(1); g.bz = idx1(c.N * KCT);
+    g.B = c.xth; g.bk = idx2(c.N, KCT, c.C); g.bn = idx2(c.C, 1, KC); g.bz = idx1(c.N * KCT);
     g.C = c.X; g.cm = idx1(CT); g.cn = idx1(1); g.cz = idx1(c.N * CT);
     g.relu = 1;
     DS_TRY(run_gemm(g, ws, kGemmWs, st));
@@ -236,13 +237,13 @@ struct ChebGradIO {
   const dstagnn_graph* g;
   bool sparse;
   const float *P, *W, *xth;
-  const float* gpre;       // d(pre-ReLU out) (B,N,C,T)
+  const float* gpre;       // d(pre-ReLU out) (B,N,T,C)
   float* dx;               // accumulated (beta = dx_beta)
   float dx_beta;
   float* dz;               // (B,K,N,N) d scores
   float* dthcat;           // (F, K*C)
   float* const* dmask;     // K pointers (N,N)
-  float* dxth;             // scratch (B,N,K,C,T)
+  float* dxth;             // scratch (B,N,T,K,C)
 };
 
 int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
@@ -252,7 +253,7 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
     // dW only on the support (zero elsewhere); dxth by the transposed sparse product
     hipError_t e = hipMemsetAsync(c.dz, 0, sizeof(float) * (size_t)c.B * c.K * NN, st);
     if (e != hipSuccess) { set_last_error(std::string("memset: ") + hipGetErrorString(e)); return (int)e; }
-    ChebSp sp = make_sp(c.B, c.N, c.K, (int)CT, c.g);
+    ChebSp sp = make_sp(c.B, c.N, c.K, c.C, c.T, c.g);
     sp.P = c.P; sp.xth = c.xth; sp.g = c.gpre; sp.dW = c.dz; sp.dxth = c.dxth;
     DS_TRY(op_cheb_sddmm_bwd(sp, st));
     DS_TRY(op_cheb_spmm_t_bwd(sp, st));
@@ -261,7 +262,7 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
   if (!c.sparse) {
     Gemm g;
     g.M = c.N; g.N = c.N; g.K = (int)CT; g.batch = c.B * c.K;
-    g.A = c.xth; g.am = idx1(KCT); g.ak = idx1(1); g.az = idx2(c.K, CT, c.N * KCT);
+    g.A = c.xth; g.am = idx1(KCT); g.ak = idx2(c.C, 1, KC); g.az = idx2(c.K, c.C, c.N * KCT);
     g.B = c.gpre; g.bk = idx1(1); g.bn = idx1(CT); g.bz = idx2(c.K, 0, c.N * CT);
     g.C = c.dz; g.cm = idx1(c.N); g.cn = idx1(1); g.cz = idx1(NN);
     DS_TRY(run_gemm(g, ws, kGemmWs, st));
@@ -272,7 +273,7 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
     g.M = c.N; g.N = (int)CT; g.K = c.N; g.batch = c.B * c.K;
     g.A = c.W; g.am = idx1(c.N); g.ak = idx1(1); g.az = idx1(NN);
     g.B = c.gpre; g.bk = idx1(CT); g.bn = idx1(1); g.bz = idx2(c.K, 0, c.N * CT);
-    g.C = c.dxth; g.cm = idx1(KCT); g.cn = idx1(1); g.cz = idx2(c.K, CT, c.N * KCT);
+    g.C = c.dxth; g.cm = idx1(KCT); g.cn = idx2(c.C, 1, KC); g.cz = idx2(c.K, c.C, c.N * KCT);
     DS_TRY(run_gemm(g, ws, kGemmWs, st));
   }
   // softmax backward in place: dz = P * (T o dW - colsum(P T o dW))
@@ -282,20 +283,20 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
   for (int k = 0; k < c.K; ++k) sm.dmask[k] = c.dmask[k];
   DS_TRY(op_cheb_softmax_bwd(sm, st));
   DS_TRY(op_cheb_mask_grad(sm, st));
-  // dTheta_cat[f,(k,c)] = sum_{b,i,t} x[b,i,f,t] dxth[b,i,k,c,t]
+  // dTheta_cat[f,(k,c)] = sum_{b,i,t} x[b,i,f,t] dxth[b,i,t,k,c]
   {
     Gemm g;
     g.M = c.F; g.N = (int)KC; g.K = c.B * c.N * c.T;
     g.A = c.x; g.am = idx1(T); g.ak = idx2(T, 1, FT);
-    g.B = c.dxth; g.bk = idx2(T, 1, KCT); g.bn = idx1(T);
+    g.B = c.dxth; g.bk = idx1(KC); g.bn = idx1(1);
     g.C = c.dthcat; g.cm = idx1(KC); g.cn = idx1(1);
     DS_TRY(run_gemm(g, ws, kGemmWs, st));
   }
-  // dx[b,i,f,t] += sum_{k,c} Theta_k[f,c] dxth[b,i,k,c,t]
+  // dx[b,i,f,t] += sum_{k,c} Theta_k[f,c] dxth[b,i,t,k,c]
   {
     Gemm g;
     g.M = c.B * c.N * c.T; g.N = c.F; g.K = (int)KC;
-    g.A = c.dxth; g.am = idx2(T, 1, KCT); g.ak = idx1(T);
+    g.A = c.dxth; g.am = idx1(KC); g.ak = idx1(1);
     g.B = c.thcat; g.bk = idx1(1); g.bn = idx1(KC);
     g.C = c.dx; g.cm = idx2(T, 1, FT); g.cn = idx1(T);
     g.beta = c.dx_beta;
@@ -447,13 +448,21 @@ struct Fwd {
   }
 
   int stage_tail() {
+    {  // GTU conv weights re-laid (o, j, c) so the im2col k map is single-level
+      GtuWeights gw;
+      gw.C = m.C; gw.mode = 0;
+      for (int q = 0; q < 3; ++q) { gw.w[q] = p.gtu_w[q]; gw.perm[q] = w.Wg[q]; }
+      DS_TRY(op_gtu_weights(gw, st));
+    }
     for (int q = 0; q < 3; ++q) {  // GTU convs (:190) as implicit-im2col GEMMs
+      // conv[(bn,t), o] = b[o] + sum_{(j,c)} X[bn, t+j, c] W[o,c,j]; with X rows (t,c) the
+      // window (j, c) is one contiguous run of ks*C floats
       const int ks = m.ks[q], Tg = m.Tg[q];
       Gemm g;
       g.M = (int)(m.BN * Tg); g.N = 2 * m.C; g.K = m.C * ks;
-      g.A = s.X; g.am = idx2(Tg, 1, m.CT); g.ak = idx2(ks, 1, m.T);
-      g.B = p.gtu_w[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);
-      g.C = s.conv[q]; g.cm = idx2(Tg, 1, 2 * m.C * Tg); g.cn = idx1(Tg);
+      g.A = s.X; g.am = idx2(Tg, m.C, m.CT); g.ak = idx1(1);
+      g.B = w.Wg[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);
+      g.C = s.conv[q]; g.cm = idx1(2 * m.C); g.cn = idx1(1);
       g.bias = p.gtu_b[q];
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
@@ -559,24 +568,31 @@ struct Bwd {
     for (int q = 0; q < 3; ++q) { ga.conv[q] = s.conv[q]; ga.dconv_pad[q] = w.dconv[q]; }
     ga.dG = w.dG;
     DS_TRY(op_gate_bwd(ga, st));
+    {  // flipped conv weights (j', o, c) for the transposed convolution
+      GtuWeights gw;
+      gw.C = m.C; gw.mode = 1;
+      for (int q = 0; q < 3; ++q) { gw.w[q] = p.gtu_w[q]; gw.perm[q] = w.Wg[q]; }
+      DS_TRY(op_gtu_weights(gw, st));
+    }
     for (int q = 0; q < 3; ++q) {
       const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
-      const int64_t cs = 2 * (int64_t)m.C * Lp;  // per-(b,n) stride of the padded dconv
+      const int64_t C2 = 2 * (int64_t)m.C;
+      const int64_t cs = C2 * Lp;  // per-(b,n) stride of the padded dconv rows (t', o)
       if (gd.gtu_w[q]) {
-        Gemm g;  // dW[o,(c,tau)] = sum_{(bn,t')} dconv[bn,o,t'] X[bn,c,t'+tau]
-        g.M = 2 * m.C; g.N = m.C * ks; g.K = (int)(m.BN * Tg);
-        g.A = w.dconv[q]; g.a_off = ks - 1; g.am = idx1(Lp); g.ak = idx2(Tg, 1, cs);
-        g.B = s.X; g.bk = idx2(Tg, 1, m.CT); g.bn = idx2(ks, 1, m.T);
-        g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx1(1);
+        Gemm g;  // dW[o,c,j] = sum_{(bn,t')} dconv[bn,t',o] X[bn,t'+j,c]
+        g.M = (int)C2; g.N = m.C * ks; g.K = (int)(m.BN * Tg);
+        g.A = w.dconv[q]; g.a_off = (ks - 1) * C2; g.am = idx1(1); g.ak = idx2(Tg, C2, cs);
+        g.B = s.X; g.bk = idx2(Tg, m.C, m.CT); g.bn = idx1(1);
+        g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx2(m.C, ks, 1);
         DS_TRY(gemm(g));
       }
-      DS_TRY(colsum(w.dconv[q], nullptr, m.BN, 2 * m.C, Lp, gd.gtu_b[q]));
+      DS_TRY(colsum(w.dconv[q], nullptr, m.BN * Lp, (int)C2, 1, gd.gtu_b[q]));
       {
-        Gemm g;  // dX[bn,c,t] += sum_{o,tau} W[o,c,tau] dconv[bn,o,t-tau]
-        g.M = (int)(m.BN * m.T); g.N = m.C; g.K = 2 * m.C * ks;
-        g.A = w.dconv[q]; g.a_off = ks - 1; g.am = idx2(m.T, 1, cs); g.ak = idx2(ks, -1, Lp);
-        g.B = p.gtu_w[q]; g.bk = idx2(ks, 1, (int64_t)m.C * ks); g.bn = idx1(ks);
-        g.C = w.dX; g.cm = idx2(m.T, 1, m.CT); g.cn = idx1(m.T);
+        Gemm g;  // dX[bn,t,c] += sum_{(j',o)} dconv_pad[bn,t+j',o] W[o,c,ks-1-j']
+        g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
+        g.A = w.dconv[q]; g.am = idx2(m.T, C2, cs); g.ak = idx1(1);
+        g.B = w.Wg[q]; g.bk = idx1(m.C); g.bn = idx1(1);
+        g.C = w.dX; g.cm = idx1(m.C); g.cn = idx1(1);
         g.beta = 1.f;
         DS_TRY(gemm(g));
       }
@@ -834,15 +850,24 @@ int dstagnn_cheb_sat_forward(int B, int N, int F, int T, int K, int C, int spars
                              float* P, float* W, float* xth, void* scratch, size_t scratch_bytes,
                              dstagnn_stream_t stream) {
   if (K > DSTAGNN_MAX_K || K <= 0 || !g) return DSTAGNN_E_SHAPE;
-  if (scratch_bytes < kGemmWs * sizeof(float) + 256) { set_last_error("scratch too small"); return DSTAGNN_E_SPACE; }
+  const int64_t nbig = (int64_t)B * N * C * T;
+  if (scratch_bytes < (kGemmWs + nbig) * sizeof(float) + 2 * 256) {
+    set_last_error("scratch too small");
+    return DSTAGNN_E_SPACE;
+  }
   if (sparse && (!cheb_sparse_ok(C * T) || g->nnz <= 0)) { set_last_error("sparse path unavailable"); return DSTAGNN_E_ARG; }
+  Arena a(align256(scratch));
+  float* ws = a.take(kGemmWs);
+  float* Xtc = a.take(nbig);  // the block's internal (B,N,T,C) image
   const float* masks[DSTAGNN_MAX_K];
   for (int k = 0; k < K; ++k) masks[k] = mask_cat + (int64_t)k * N * N;
   ChebIO c;
   c.B = B; c.N = N; c.F = F; c.T = T; c.K = K; c.C = C;
   c.x = x; c.S = sat; c.mask = masks; c.g = g; c.sparse = sparse != 0; c.thcat = theta_cat;
-  c.P = P; c.W = W; c.xth = xth; c.X = out;
-  return cheb_forward(c, (float*)align256(scratch), (hipStream_t)stream);
+  c.P = P; c.W = W; c.xth = xth; c.X = Xtc;
+  hipStream_t st = (hipStream_t)stream;
+  DS_TRY(cheb_forward(c, ws, st));
+  return op_transpose(Xtc, out, T, C, B * N, (int64_t)C * T, (int64_t)C * T, 0.f, st);
 }
 
 int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C, int sparse, const float* x,
@@ -854,14 +879,16 @@ int dstagnn_cheb_sat_backward(int B, int N, int F, int T, int K, int C, int spar
   if (sparse && (!cheb_sparse_ok(C * T) || g->nnz <= 0)) { set_last_error("sparse path unavailable"); return DSTAGNN_E_ARG; }
   const int64_t nbig = (int64_t)B * N * C * T;
   const int64_t nxth = (int64_t)B * N * K * C * T;
-  size_t need = (kGemmWs + nbig + nxth) * sizeof(float) + 3 * 256;
+  size_t need = (kGemmWs + 2 * nbig + nxth) * sizeof(float) + 4 * 256;
   if (scratch_bytes < need) { set_last_error("scratch too small"); return DSTAGNN_E_SPACE; }
   Arena a(align256(scratch));
   float* ws = a.take(kGemmWs);
+  float* gct = a.take(nbig);
   float* gpre = a.take(nbig);
   float* dxth = a.take(nxth);
   hipStream_t st = (hipStream_t)stream;
-  DS_TRY(op_relu_mask(d_out, out, gpre, nbig, st));
+  DS_TRY(op_relu_mask(d_out, out, gct, nbig, st));
+  DS_TRY(op_transpose(gct, gpre, C, T, B * N, (int64_t)C * T, (int64_t)C * T, 0.f, st));  // -> (B,N,T,C)
   float* dmask[DSTAGNN_MAX_K];
   for (int k = 0; k < K; ++k) dmask[k] = d_mask_cat + (int64_t)k * N * N;
   ChebGradIO c;

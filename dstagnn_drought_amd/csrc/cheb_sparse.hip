@@ -10,9 +10,12 @@
 // (they normalise over all N source nodes); only the aggregation and its two backward
 // products are sparse.
 //
-//   spmm_fwd    out[b,j,:]   = ReLU( sum_k sum_{i in supp(j)} T_k[i,j] P[b,k,i,j] xth[b,i,k,:] )
-//   sddmm_bwd   dW[b,k,i,j]  = <xth[b,i,k,:], g[b,j,:]>            for (i,j) in supp
-//   spmm_t_bwd  dxth[b,i,k,:]= sum_{j in supp_row(i)} T_k[i,j] P[b,k,i,j] g[b,j,:]
+//   spmm_fwd    out[b,j,:]   = ReLU( sum_k sum_{i in supp(j)} T_k[i,j] P[b,k,i,j] xth[b,i,:,k,:] )
+//   sddmm_bwd   dW[b,k,i,j]  = <xth[b,i,:,k,:], g[b,j,:]>          for (i,j) in supp
+//   spmm_t_bwd  dxth[b,i,:,k,:] = sum_{j in supp_row(i)} T_k[i,j] P[b,k,i,j] g[b,j,:]
+// Layouts: xth (B,N,T,K,C) (the Theta GEMM's plain row-major output), out / g (B,N,T,C).
+// Element e = t*C + c of a node's C*T vector sits at e + t*(K-1)*C inside the node's
+// xth block, plus k*C.
 #include "common.hpp"
 #include "ops.hpp"
 
@@ -22,6 +25,17 @@ constexpr int kMaxNQ = 16;  // C*T <= 64*16 = 1024 (host checks; larger C*T uses
 
 // Lanes past C*T read a clamped (valid) address and are never stored / are zeroed in
 // the one operand loaded outside the hot loop: no predicated loads in the inner loops.
+
+// per-lane offsets of elements e = lane + 64 q (clamped to the last one) in a node's xth block
+template <int kNQ>
+__device__ __forceinline__ void xth_offsets(const ChebSp& a, int lane, int (&xo)[kNQ]) {
+  const int skip = (a.K - 1) * a.C;
+#pragma unroll
+  for (int q = 0; q < kNQ; ++q) {
+    const int e = min(lane + 64 * q, a.CT - 1);
+    xo[q] = e + (e / a.C) * skip;
+  }
+}
 
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
@@ -33,6 +47,9 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   float acc[kNQ];
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) acc[q] = 0.f;
+  int xo[kNQ];
+  xth_offsets<kNQ>(a, lane, xo);
+  const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csc_ptr[j], p1 = a.csc_ptr[j + 1];
   for (int k = 0; k < a.K; ++k) {
     const float* Pk = a.P + ((int64_t)b * a.K + k) * NN;
@@ -41,9 +58,9 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
       const int i = a.csc_row[p];
       const int64_t o = (int64_t)i * a.N + j;
       const float w = Tk[o] * Pk[o];
-      const float* xr = a.xth + (((int64_t)b * a.N + i) * a.K + k) * a.CT;
+      const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
 #pragma unroll
-      for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, xr[min(lane + 64 * q, a.CT - 1)], acc[q]);
+      for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, xr[xo[q]], acc[q]);
     }
   }
   float* orow = a.out + ((int64_t)b * a.N + j) * a.CT;
@@ -68,15 +85,18 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
     const int e = lane + 64 * q;
     g[q] = e < a.CT ? grow[e] : 0.f;
   }
+  int xo[kNQ];
+  xth_offsets<kNQ>(a, lane, xo);
+  const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csc_ptr[j], p1 = a.csc_ptr[j + 1];
   for (int k = 0; k < a.K; ++k) {
     float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
     for (int p = p0; p < p1; ++p) {
       const int i = a.csc_row[p];
-      const float* xr = a.xth + (((int64_t)b * a.N + i) * a.K + k) * a.CT;
+      const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
       float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], xr[min(lane + 64 * q, a.CT - 1)], s);
+      for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], xr[xo[q]], s);
       s = wave_sum(s);
       if (lane == 0) dWk[(int64_t)i * a.N + j] = s;
     }
@@ -90,6 +110,9 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), i = (int)(wv % a.N);
   const int64_t NN = (int64_t)a.N * a.N;
+  int xo[kNQ];
+  xth_offsets<kNQ>(a, lane, xo);
+  const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csr_ptr[i], p1 = a.csr_ptr[i + 1];
   for (int k = 0; k < a.K; ++k) {
     const float* Pk = a.P + ((int64_t)b * a.K + k) * NN;
@@ -105,11 +128,11 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
 #pragma unroll
       for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, gr[min(lane + 64 * q, a.CT - 1)], acc[q]);
     }
-    float* dr = a.dxth + (((int64_t)b * a.N + i) * a.K + k) * a.CT;
+    float* dr = a.dxth + ((int64_t)b * a.N + i) * KCT + k * a.C;
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
       const int e = lane + 64 * q;
-      if (e < a.CT) dr[e] = acc[q];
+      if (e < a.CT) dr[xo[q]] = acc[q];
     }
   }
 }

@@ -471,10 +471,12 @@ __global__ __launch_bounds__(256) void cheb_mask_grad_kernel(ChebSm a) {
 // =====================================================================================
 // One workgroup per (b,n) row at a time (grid-stride over rows), threads over the row's
 // elements with 32-bit index math (no 64-bit division in the element loop).
+// conv[q] rows are (t, o) (the conv GEMM's row-major output), G rows (c, s).
 __global__ __launch_bounds__(256) void gate_fwd_kernel(GateArgs a) {
   const int S = 3 * a.T - 12;
   const int E = a.C * S;
   const int T0 = a.T - 2, T1 = a.T - 4;
+  const int C2 = 2 * a.C;
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     float* grow = a.G + bn * E;
     for (int e = threadIdx.x; e < E; e += 256) {
@@ -482,15 +484,18 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(GateArgs a) {
       const int gi = s < T0 ? 0 : (s < T0 + T1 ? 1 : 2);
       const int t = gi == 0 ? s : (gi == 1 ? s - T0 : s - T0 - T1);
       const int Tg = a.T - 2 - 2 * gi;
-      const float* cv = a.conv[gi] + bn * 2 * a.C * Tg;
-      const float p = cv[c * Tg + t];
-      const float q = cv[(a.C + c) * Tg + t];
+      const float* cv = a.conv[gi] + bn * C2 * Tg + t * C2;
+      const float p = cv[c];
+      const float q = cv[a.C + c];
       grow[e] = tanhf(p) * (1.f / (1.f + __expf(-q)));
     }
   }
 }
+// dconv_pad[q] rows are (t', o), t' in [0, T+ks-1): the conv gradient at t = t'-(ks-1),
+// zero outside [0, Tg) — the padding the transposed convolution GEMM reads in place.
 __global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a) {
   const int S = 3 * a.T - 12;
+  const int C2 = 2 * a.C;
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
 #pragma unroll
     for (int gi = 0; gi < 3; ++gi) {
@@ -498,24 +503,40 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a) {
       const int Tg = a.T - ks + 1;
       const int Lp = a.T + ks - 1;
       const int off = gi == 0 ? 0 : (gi == 1 ? a.T - 2 : 2 * a.T - 6);
-      const int E = 2 * a.C * Lp;
+      const int E = C2 * Lp;
       float* orow = a.dconv_pad[gi] + bn * E;
-      const float* cv = a.conv[gi] + bn * 2 * a.C * Tg;
+      const float* cv = a.conv[gi] + bn * C2 * Tg;
       const float* dgr = a.dG + bn * a.C * S + off;
       for (int e = threadIdx.x; e < E; e += 256) {
-        const int o = e / Lp, l = e - o * Lp;
-        const int t = l - (ks - 1);
+        const int tp = e / C2, o = e - tp * C2;
+        const int t = tp - (ks - 1);
         float v = 0.f;
         if (t >= 0 && t < Tg) {
           const int c = o < a.C ? o : o - a.C;
-          const float p = cv[c * Tg + t];
-          const float q = cv[(a.C + c) * Tg + t];
+          const float p = cv[t * C2 + c];
+          const float q = cv[t * C2 + a.C + c];
           const float dg = dgr[c * S + t];
           const float th = tanhf(p), sg = 1.f / (1.f + __expf(-q));
           v = o < a.C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
         }
         orow[e] = v;
       }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gtu_weights_kernel(GtuWeights a) {
+  const int C = a.C, C2 = 2 * C;
+  for (int q = 0; q < 3; ++q) {
+    const int ks = 3 + 2 * q;
+    const int n = C2 * C * ks;
+    const float* w = a.w[q];
+    float* o = a.perm[q];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+      // source w[oc][c][j], i = (oc*C + c)*ks + j
+      const int j = i % ks, r = i / ks, c = r % C, oc = r / C;
+      if (a.mode == 0) o[(oc * ks + j) * C + c] = w[i];
+      else o[((ks - 1 - j) * C2 + oc) * C + c] = w[i];
     }
   }
 }
@@ -543,7 +564,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
       tco = fmaxf(tc, 0.f);
       xres = a.res_w[c] * a.x[bn * T + t] + a.res_b[c];
     } else {
-      tco = fmaxf(a.X[o] + tc, 0.f);
+      tco = fmaxf(a.X[base + t * C + c] + tc, 0.f);  // X rows are (t, c)
       xres = a.x[o];
     }
     const float r = fmaxf(xres + tco, 0.f);
@@ -602,13 +623,14 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(TailArgs a) {
     float dtc = dtco;
     if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
     a.dtc[o] = dtc;
+    const int c = e / T;
     if (a.first) {
-      a.dX[o] = 0.f;
+      a.dX[base + t * C + c] = 0.f;
       a.rcontrib[o] = dr * a.x[bn * T + t];  // d residual_conv.weight contributions
       a.dres[o] = dr;                         // d residual_conv.bias contributions
       dxh[e] = dr;                            // reuse LDS for the channel reduction below
     } else {
-      a.dX[o] = dtco;
+      a.dX[base + t * C + c] = dtco;  // dX rows are (t, c), like X
       a.dx[o] = dr;
     }
   }
@@ -788,6 +810,12 @@ int op_cheb_mask_grad(const ChebSm& a, hipStream_t st) {
 
 int op_gate_fwd(const GateArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(gate_fwd_kernel, dim3((unsigned)std::min<int64_t>(a.BN, 4096)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+int op_gtu_weights(const GtuWeights& a, hipStream_t st) {
+  hipLaunchKernelGGL(gtu_weights_kernel, dim3((unsigned)std::max<int64_t>(1, cdiv64(2LL * a.C * a.C * 7, 256))),
+                     dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -55,17 +55,26 @@ struct ColsumArgs {
   float* part = nullptr; int P = 1; int OL = 1;
 };
 
+// GTU conv weights (2C, C, 1, ks) re-laid for single-level GEMM k maps:
+//   mode 0: perm[o][j][c] = w[o][c][j]            (forward: k = (j, c))
+//   mode 1: perm[j'][o][c] = w[o][c][ks-1-j']     (transposed conv: k = (j', o))
+struct GtuWeights {
+  int C = 0, mode = 0;
+  const float* w[3] = {};
+  float* perm[3] = {};
+};
+
 struct GateArgs {
   int64_t BN = 0; int C = 0, T = 0;
-  const float* conv[3] = {};      // [bn][2C][T-ks+1]
+  const float* conv[3] = {};      // [bn][T-ks+1][2C]
   float* G = nullptr;             // [bn][C][3T-12]
   const float* dG = nullptr;
-  float* dconv_pad[3] = {};       // [bn][2C][T+ks-1]
+  float* dconv_pad[3] = {};       // [bn][T+ks-1][2C]
 };
 
 struct TailArgs {
   int64_t BN = 0; int C = 0, T = 0; int first = 0;
-  const float* X = nullptr;       // cheb output (B,N,C,T)
+  const float* X = nullptr;       // cheb output (B,N,T,C)
   const float* tc = nullptr;      // fcmy output (B,N,C,T)
   const float* x = nullptr;       // block input (B,N,F,T)
   const float* res_w = nullptr; const float* res_b = nullptr;
@@ -89,16 +98,16 @@ struct PackTheta {
 
 // sparse Chebyshev aggregation over the union support of T_0..T_{K-1} (cheb_sparse.hip)
 struct ChebSp {
-  int B = 0, N = 0, K = 0, CT = 0;
+  int B = 0, N = 0, K = 0, CT = 0, C = 0;   // element e of a C*T row = (t, c), e = t*C + c
   const int* csc_ptr = nullptr; const int* csc_row = nullptr;  // column j -> source rows i
   const int* csr_ptr = nullptr; const int* csr_col = nullptr;  // row i -> destination columns j
   const float* cheb = nullptr;   // (K,N,N)
   const float* P = nullptr;      // (B,K,N,N) column softmax
-  const float* xth = nullptr;    // (B,N,K,CT)
-  float* out = nullptr;          // (B,N,CT)  fwd (ReLU applied)
-  const float* g = nullptr;      // (B,N,CT)  bwd: d(pre-ReLU out)
+  const float* xth = nullptr;    // (B,N,T,K,C)
+  float* out = nullptr;          // (B,N,T,C)  fwd (ReLU applied)
+  const float* g = nullptr;      // (B,N,T,C)  bwd: d(pre-ReLU out)
   float* dW = nullptr;           // (B,K,N,N) bwd: written on the support only
-  float* dxth = nullptr;         // (B,N,K,CT) bwd
+  float* dxth = nullptr;         // (B,N,T,K,C) bwd
 };
 bool cheb_sparse_ok(int CT);
 int op_cheb_spmm_fwd(const ChebSp& a, hipStream_t st);
@@ -124,6 +133,7 @@ int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st);
 int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st);
 int op_cheb_mask_grad(const ChebSm& a, hipStream_t st);
 int op_gate_fwd(const GateArgs& a, hipStream_t st);
+int op_gtu_weights(const GtuWeights& a, hipStream_t st);
 int op_gate_bwd(const GateArgs& a, hipStream_t st);
 int op_tail_fwd(const TailArgs& a, hipStream_t st);
 int op_tail_bwd(const TailArgs& a, hipStream_t st);
