@@ -104,9 +104,11 @@ constexpr size_t kPart = size_t(2) << 20;      // floats (8 MB) for column-sum p
 
 struct Scratch {
   float *Wp, *thcat, *tc, *gemm_ws, *part, *Wg[3];
-  // bwd
-  float *dtc, *dX, *gpre, *gcon, *bcon, *dG, *dconv[3], *dW, *dxth, *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dctx,
-      *dqkv, *dscore, *du_et;
+  // bwd (the *_side workspaces belong to the side stream; gcon_* / bcon_* / dres_t are
+  // per-stage so the side stream's reductions never race a later main-chain write)
+  float *gemm_ws_side, *part_side;
+  float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dG, *dconv[3], *dW, *dxth,
+      *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dctx, *dqkv, *dscore, *du_et;
 };
 
 Scratch plan_scratch(const Dims& m, Arena& a) {
@@ -120,10 +122,15 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.dtc = a.take(m.BN * m.CT);
   s.dX = a.take(m.BN * m.CT);
   s.gpre = a.take(m.BN * m.CT);
-  // LN / tail gamma & beta contributions: largest of (B*N*C*T, B*N*D, B*F*T*N)
-  int64_t con = std::max(m.BN * m.CT, std::max(m.BN * m.D, m.BFT * m.N));
-  s.gcon = a.take(con);
-  s.bcon = a.take(con);
+  s.gemm_ws_side = a.take(kGemmWs);
+  s.part_side = a.take(kPart);
+  s.gcon_t = a.take(m.BN * m.CT);
+  s.bcon_t = a.take(m.BN * m.CT);
+  s.dres_t = a.take(m.BN * m.CT);
+  s.gcon_s = a.take(m.BN * m.D);
+  s.bcon_s = a.take(m.BN * m.D);
+  s.gcon_a = a.take(m.BFT * m.N);
+  s.gcon_e = m.first ? a.take((int64_t)m.B * m.T * m.N) : nullptr;
   s.dG = a.take(m.BN * m.C * m.S);
   for (int g = 0; g < 3; ++g) s.dconv[g] = a.take(m.BN * 2 * m.C * m.Lp[g]);
   s.dW = a.take((int64_t)m.B * m.K * m.NN);
@@ -501,6 +508,41 @@ struct Fwd {
 // ------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------
+// The backward has two dependency chains: the data gradients (dx -> ... -> d_x, each step
+// needing the previous) and the parameter gradients (weight GEMMs, bias / gamma / beta
+// column sums, split-K folds), which only read values the data chain has produced. The
+// second chain runs on a side stream (lowest priority) forked from the caller's stream
+// by events, so its kernels fill the CUs the small data-chain kernels leave idle; it has
+// its own GEMM / reduction workspaces and its inputs are never overwritten by the main
+// chain afterwards (buffers that would be are given their own allocation). One join at
+// the end. DSTAGNN_SIDE_STREAM=0 runs everything on the caller's stream.
+struct SideStream {
+  hipStream_t side = nullptr;
+  hipEvent_t ev[64] = {};
+  int next = 0;
+  bool ok = false;
+};
+
+SideStream* side_stream_for_device() {
+  static std::mutex mu;
+  static SideStream cache[64];
+  static const bool enabled = !getenv("DSTAGNN_SIDE_STREAM") || atoi(getenv("DSTAGNN_SIDE_STREAM")) != 0;
+  if (!enabled) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  SideStream& s = cache[dev];
+  if (!s.ok) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
+    if (hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
+    for (auto& e : s.ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    s.ok = true;
+  }
+  return &s;
+}
+
 struct Bwd {
   const Dims& m;
   const dstagnn_block_dims& d;
@@ -515,13 +557,27 @@ struct Bwd {
   SaveBufs& s;
   Scratch& w;
   hipStream_t st;
+  SideStream* ss = nullptr;
+  hipStream_t sd = nullptr;  // side stream (== st when disabled)
 
-  int colsum(const float* in, const float* in2, int64_t A, int O, int I, float* out) {
-    (void)in2;
-    if (!out) return 0;
-    return op_colsum(in, A, O, I, out, 1, 0.f, w.part, kPart, st);
+  int event_pair(hipStream_t from, hipStream_t to) {
+    if (from == to) return 0;
+    hipEvent_t e = ss->ev[ss->next];
+    ss->next = (ss->next + 1) % 64;
+    hipError_t r = hipEventRecord(e, from);
+    if (r == hipSuccess) r = hipStreamWaitEvent(to, e, 0);
+    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
+    return 0;
   }
-  // several same-shape column sums in one launch pair; null outputs are skipped
+  int fork() { return event_pair(st, sd); }  // side sees everything the main chain issued so far
+  int join() { return event_pair(sd, st); }  // main waits for everything issued on the side
+
+  int colsum_on(hipStream_t q, const float* in, int64_t A, int O, int I, float* out) {
+    if (!out) return 0;
+    float* part = q == st ? w.part : w.part_side;
+    return op_colsum(in, A, O, I, out, 1, 0.f, part, kPart, q);
+  }
+  // several same-shape column sums in one launch pair (side stream); null outputs skipped
   int colsums(std::initializer_list<std::pair<const float*, float*>> io, int64_t A, int O, int I) {
     const float* ins[4];
     float* outs[4];
@@ -529,9 +585,10 @@ struct Bwd {
     for (const auto& q : io)
       if (q.second && n < 4) { ins[n] = q.first; outs[n] = q.second; ++n; }
     if (!n) return 0;
-    return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, w.part, kPart, st);
+    return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, sd == st ? w.part : w.part_side, kPart, sd);
   }
   int gemm(const Gemm& g) { return run_gemm(g, w.gemm_ws, kGemmWs, st); }
+  int sgemm(const Gemm& g) { return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd); }
 
   int stage_tail() {
     TailArgs t;
@@ -539,12 +596,9 @@ struct Bwd {
     t.X = s.X; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
     if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
     t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c;
-    t.dout = dout; t.gcontrib = w.gcon; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
-    t.rcontrib = w.bcon; t.dres = w.gpre;  // gpre reused as scratch until the cheb stage
+    t.dout = dout; t.gcontrib = w.gcon_t; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
+    t.rcontrib = w.bcon_t; t.dres = w.dres_t;
     DS_TRY(op_tail_bwd(t, st));
-    DS_TRY(colsums({{w.gcon, gd.ln_g}, {dout, gd.ln_b}, {w.bcon, m.first ? gd.res_w : nullptr},
-                    {w.gpre, m.first ? gd.res_b : nullptr}}, m.BN, m.C, m.T));
-    // fcmy backward
     {
       Gemm g;  // dG = dtc @ W
       g.M = (int)(m.BN * m.C); g.N = (int)m.S; g.K = m.T;
@@ -553,16 +607,20 @@ struct Bwd {
       g.C = w.dG; g.cm = idx1(m.S); g.cn = idx1(1);
       DS_TRY(gemm(g));
     }
+    // --- side: LN / residual / fcmy parameter gradients
+    DS_TRY(fork());
+    DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {dout, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
+                    {w.dres_t, m.first ? gd.res_b : nullptr}}, m.BN, m.C, m.T));
     if (gd.fcmy_w) {
       Gemm g;  // dW[t,s] = sum_r dtc[r,t] G[r,s]
       g.M = m.T; g.N = (int)m.S; g.K = (int)(m.BN * m.C);
       g.A = w.dtc; g.am = idx1(1); g.ak = idx1(m.T);
       g.B = s.G; g.bk = idx1(m.S); g.bn = idx1(1);
       g.C = gd.fcmy_w; g.cm = idx1(m.S); g.cn = idx1(1);
-      DS_TRY(gemm(g));
+      DS_TRY(sgemm(g));
     }
-    DS_TRY(colsum(w.dtc, nullptr, m.BN * m.C, m.T, 1, gd.fcmy_b));
-    // gates
+    DS_TRY(colsum_on(sd, w.dtc, m.BN * m.C, m.T, 1, gd.fcmy_b));
+    // --- main: gates, then per GTU the transposed convolution; side: its weight / bias grads
     GateArgs ga;
     ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
     for (int q = 0; q < 3; ++q) { ga.conv[q] = s.conv[q]; ga.dconv_pad[q] = w.dconv[q]; }
@@ -574,6 +632,7 @@ struct Bwd {
       for (int q = 0; q < 3; ++q) { gw.w[q] = p.gtu_w[q]; gw.perm[q] = w.Wg[q]; }
       DS_TRY(op_gtu_weights(gw, st));
     }
+    DS_TRY(fork());
     for (int q = 0; q < 3; ++q) {
       const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
       const int64_t C2 = 2 * (int64_t)m.C;
@@ -584,9 +643,9 @@ struct Bwd {
         g.A = w.dconv[q]; g.a_off = (ks - 1) * C2; g.am = idx1(1); g.ak = idx2(Tg, C2, cs);
         g.B = s.X; g.bk = idx2(Tg, m.C, m.CT); g.bn = idx1(1);
         g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx2(m.C, ks, 1);
-        DS_TRY(gemm(g));
+        DS_TRY(sgemm(g));
       }
-      DS_TRY(colsum(w.dconv[q], nullptr, m.BN * Lp, (int)C2, 1, gd.gtu_b[q]));
+      DS_TRY(colsum_on(sd, w.dconv[q], m.BN * Lp, (int)C2, 1, gd.gtu_b[q]));
       {
         Gemm g;  // dX[bn,t,c] += sum_{(j',o)} dconv_pad[bn,t+j',o] W[o,c,ks-1-j']
         g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
@@ -603,13 +662,60 @@ struct Bwd {
   int stage_cheb() {
     DS_TRY(op_relu_mask(w.dX, s.X, w.gpre, m.BN * m.CT, st));
     DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, w.thcat, st));
-    ChebGradIO c;
-    c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
-    c.x = x; c.thcat = w.thcat; c.g = &gr; c.sparse = m.sparse; c.P = s.P; c.W = s.W; c.xth = s.xth;
-    c.gpre = w.gpre; c.dx = dx; c.dx_beta = 1.f; c.dz = w.dW; c.dthcat = w.dthcat; c.dmask = gd.mask;
-    c.dxth = w.dxth;
-    DS_TRY(cheb_backward(c, w.gemm_ws, st));
-    DS_TRY(unpack_theta(w.dthcat, m.K, m.F, m.C, gd.theta, st));
+    const int64_t NN = m.NN, KC = m.KC, T = m.T, CT = m.CT, KCT = m.KCT, FT = m.FT;
+    const int B = m.B, N = m.N, K = m.K, C = m.C, F = m.F;
+    if (m.sparse) {
+      hipError_t e = hipMemsetAsync(w.dW, 0, sizeof(float) * (size_t)B * K * NN, st);
+      if (e != hipSuccess) { set_last_error(std::string("memset: ") + hipGetErrorString(e)); return (int)e; }
+      ChebSp sp = make_sp(B, N, K, C, m.T, &gr);
+      sp.P = s.P; sp.xth = s.xth; sp.g = w.gpre; sp.dW = w.dW; sp.dxth = w.dxth;
+      DS_TRY(op_cheb_sddmm_bwd(sp, st));
+      DS_TRY(op_cheb_spmm_t_bwd(sp, st));
+    } else {
+      {
+        Gemm g;  // dW[b,k,i,j] = sum_e xth[b,i,t,k,c] g[b,j,e]
+        g.M = N; g.N = N; g.K = (int)CT; g.batch = B * K;
+        g.A = s.xth; g.am = idx1(KCT); g.ak = idx2(C, 1, KC); g.az = idx2(K, C, N * KCT);
+        g.B = w.gpre; g.bk = idx1(1); g.bn = idx1(CT); g.bz = idx2(K, 0, N * CT);
+        g.C = w.dW; g.cm = idx1(N); g.cn = idx1(1); g.cz = idx1(NN);
+        DS_TRY(gemm(g));
+      }
+      {
+        Gemm g;  // dxth[b,i,t,k,c] = sum_j W[b,k,i,j] g[b,j,e]
+        g.M = N; g.N = (int)CT; g.K = N; g.batch = B * K;
+        g.A = s.W; g.am = idx1(N); g.ak = idx1(1); g.az = idx1(NN);
+        g.B = w.gpre; g.bk = idx1(CT); g.bn = idx1(1); g.bz = idx2(K, 0, N * CT);
+        g.C = w.dxth; g.cm = idx1(KCT); g.cn = idx2(C, 1, KC); g.cz = idx2(K, C, N * KCT);
+        DS_TRY(gemm(g));
+      }
+    }
+    // softmax backward in place: dz = P * (T o dW - colsum(P T o dW))
+    ChebSm sm;
+    sm.B = B; sm.K = K; sm.N = N; sm.apa = gr.adj_pa; sm.cheb = gr.cheb; sm.P = s.P;
+    sm.dW = w.dW; sm.dz = w.dW;
+    for (int k = 0; k < K; ++k) sm.dmask[k] = gd.mask[k];
+    DS_TRY(op_cheb_softmax_bwd(sm, st));
+    // --- side: mask and Theta gradients
+    DS_TRY(fork());
+    DS_TRY(op_cheb_mask_grad(sm, sd));
+    {
+      Gemm g;  // dTheta_cat[f,(k,c)] = sum_{b,i,t} x[b,i,f,t] dxth[b,i,t,k,c]
+      g.M = F; g.N = (int)KC; g.K = B * N * m.T;
+      g.A = x; g.am = idx1(T); g.ak = idx2(T, 1, FT);
+      g.B = w.dxth; g.bk = idx1(KC); g.bn = idx1(1);
+      g.C = w.dthcat; g.cm = idx1(KC); g.cn = idx1(1);
+      DS_TRY(sgemm(g));
+    }
+    DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sd));
+    {
+      Gemm g;  // dx[b,i,f,t] += sum_{k,c} Theta_k[f,c] dxth[b,i,t,k,c]
+      g.M = B * N * m.T; g.N = F; g.K = (int)KC;
+      g.A = w.dxth; g.am = idx1(KC); g.ak = idx1(1);
+      g.B = w.thcat; g.bk = idx1(1); g.bn = idx1(KC);
+      g.C = dx; g.cm = idx2(T, 1, FT); g.cn = idx1(T);
+      g.beta = 1.f;
+      DS_TRY(gemm(g));
+    }
     return 0;
   }
 
@@ -636,14 +742,15 @@ struct Bwd {
     }
     float* wg[2] = {gd.sat_wq, gd.sat_wk};
     const float* wts[2] = {p.sat_wq, p.sat_wk};
+    DS_TRY(fork());
     for (int q = 0; q < 2; ++q) {
-      if (wg[q]) {  // dW'[n,d] = sum_r dqk[r, q*KD + n] Zd[r,d]
+      if (wg[q]) {  // side: dW'[n,d] = sum_r dqk[r, q*KD + n] Zd[r,d]
         Gemm g;
         g.M = (int)m.KD; g.N = m.D; g.K = (int)m.BN;
         g.A = w.dqk; g.a_off = q * m.KD; g.am = idx1(1); g.ak = idx1(ld);
         g.B = s.Zd; g.bk = idx1(m.D); g.bn = idx1(1);
         g.C = wg[q]; g.cm = idx1(m.D); g.cn = idx1(1);
-        DS_TRY(gemm(g));
+        DS_TRY(sgemm(g));
       }
       Gemm g;  // dZd += dqk[:, q] W'
       g.M = (int)m.BN; g.N = m.D; g.K = (int)m.KD;
@@ -660,26 +767,27 @@ struct Bwd {
       a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s; a.g = p.embS_g;
       if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
       a.dx = w.dY; a.dxrow = idx1(m.D);
-      a.gcontrib = w.gcon; a.bcontrib = w.bcon;
+      a.gcontrib = w.gcon_s; a.bcontrib = w.bcon_s;
       DS_TRY(op_ln_bwd(a, st));
-      DS_TRY(colsums({{w.gcon, gd.embS_g}, {w.bcon, gd.embS_b}}, m.BN, m.D, 1));
-      if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, st));
     }
-    return 0;
-  }
-
-  int stage_preconv() {
-    DS_TRY(colsum(w.dY, nullptr, m.BN, m.D, 1, gd.pre_conv_b));
+    // --- side: EmbedS gamma / beta / pos-embedding grads, pre_conv bias and weight grads
+    DS_TRY(fork());
+    DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}, {w.dY, gd.pre_conv_b}}, m.BN, m.D, 1));
+    if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sd));
     if (gd.pre_conv_w) {
       Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
       g.M = m.D; g.N = (int)m.FT; g.K = (int)m.BN;
       g.A = w.dY; g.am = idx1(1); g.ak = idx1(m.D);
       g.B = s.O; g.bk = idx2(m.N, 1, m.FT * m.N); g.bn = idx1(m.N);
       g.C = w.dWp; g.cm = idx1(m.FT); g.cn = idx1(1);
-      DS_TRY(gemm(g));
+      DS_TRY(sgemm(g));
       // pre_conv.weight[d][t][0][f] = dWp[d][f][t]
-      DS_TRY(op_transpose(w.dWp, gd.pre_conv_w, m.F, m.T, m.D, m.FT, m.FT, 0.f, st));
+      DS_TRY(op_transpose(w.dWp, gd.pre_conv_w, m.F, m.T, m.D, m.FT, m.FT, 0.f, sd));
     }
+    return 0;
+  }
+
+  int stage_preconv() {
     DS_TRY(op_transpose(p.pre_conv_w, w.Wp, m.T, m.F, m.D, m.FT, m.FT, 0.f, st));
     Gemm g;  // dO[b,(f,t),n] = sum_d Wp[d,(f,t)] dY[(b,n),d]
     g.M = (int)m.FT; g.N = (int)m.BN; g.K = m.D;
@@ -697,9 +805,20 @@ struct Bwd {
       a.dy = w.dO; a.dyrow = idx1(N);
       a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat; a.g = p.tat_ln_g;
       a.dx = w.dU; a.dxrow = idx1(N);
-      a.gcontrib = w.gcon; a.bcontrib = nullptr;
+      a.gcontrib = w.gcon_a; a.bcontrib = nullptr;
       DS_TRY(op_ln_bwd(a, st));
-      DS_TRY(colsums({{w.gcon, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
+    }
+    // --- side: TAt LN gamma / beta and fc weight grads (dU is read here, so the main
+    // chain joins the side before accumulating into dU below)
+    DS_TRY(fork());
+    DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
+    if (gd.tat_fc) {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
+      Gemm g;
+      g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
+      g.A = w.dU; g.am = idx1(1); g.ak = idx1(N);
+      g.B = s.ctx; g.bk = idx1(m.HV); g.bn = idx1(1);
+      g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
+      DS_TRY(sgemm(g));
     }
     {  // dctx = dU Wfc
       Gemm g;
@@ -709,23 +828,16 @@ struct Bwd {
       g.C = w.dctx; g.cm = idx1(m.HV); g.cn = idx1(1);
       DS_TRY(gemm(g));
     }
-    if (gd.tat_fc) {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
-      Gemm g;
-      g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
-      g.A = w.dU; g.am = idx1(1); g.ak = idx1(N);
-      g.B = s.ctx; g.bk = idx1(m.HV); g.bn = idx1(1);
-      g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
-      DS_TRY(gemm(g));
-    }
     float* dsc = (d.res_mode == DSTAGNN_RES_FULL && dres) ? dres : w.dscore;
     DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, st));
     if (d.res_mode == DSTAGNN_RES_BCAST && dres)
       DS_TRY(op_sum_middle(w.dscore, m.B, m.F, (int64_t)m.h * m.T * m.T, dres, 0.f, st));
-    // dE = dU + sum_q dqkv_q W_q ;  dW_q = dqkv_q^T E
+    // dE = dU + sum_q dqkv_q W_q ;  dW_q = dqkv_q^T E  (side)
     const float* wts[3] = {p.tat_wq, p.tat_wk, p.tat_wv};
     float* wg[3] = {gd.tat_wq, gd.tat_wk, gd.tat_wv};
     const int64_t cols[3] = {m.HQ, m.HQ, m.HV};
     const int64_t offs[3] = {0, m.HQ, 2 * m.HQ};
+    DS_TRY(fork());
     for (int q = 0; q < 3; ++q) {
       if (wg[q]) {
         Gemm g;
@@ -733,8 +845,11 @@ struct Bwd {
         g.A = w.dqkv; g.a_off = offs[q]; g.am = idx1(1); g.ak = idx1(m.QW);
         g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
         g.C = wg[q]; g.cm = idx1(N); g.cn = idx1(1);
-        DS_TRY(gemm(g));
+        DS_TRY(sgemm(g));
       }
+    }
+    DS_TRY(join());  // the fc weight grad has read dU
+    for (int q = 0; q < 3; ++q) {
       Gemm g;
       g.M = (int)m.BFT; g.N = m.N; g.K = (int)cols[q];
       g.A = w.dqkv; g.a_off = offs[q]; g.am = idx1(m.QW); g.ak = idx1(1);
@@ -750,10 +865,11 @@ struct Bwd {
       a.dy = w.dU; a.dyrow = idx1(N);
       a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et; a.g = p.embT_g;
       a.dx = w.du_et; a.dxrow = idx1(N);
-      a.gcontrib = w.gcon; a.bcontrib = nullptr;
+      a.gcontrib = w.gcon_e; a.bcontrib = nullptr;
       DS_TRY(op_ln_bwd(a, st));
-      DS_TRY(colsums({{w.gcon, gd.embT_g}, {w.dU, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
-      if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, st));
+      DS_TRY(fork());
+      DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dU, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
+      if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sd));
       DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
     } else {
       DS_TRY(op_transpose(w.dU, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
@@ -762,12 +878,14 @@ struct Bwd {
   }
 
   int run() {
+    ss = (st != nullptr || true) ? side_stream_for_device() : nullptr;
+    sd = ss ? ss->side : st;
     DS_TRY(stage_tail());
     DS_TRY(stage_cheb());
     DS_TRY(stage_sat());
     DS_TRY(stage_preconv());
     DS_TRY(stage_tat());
-    return 0;
+    return join();
   }
 };
 
