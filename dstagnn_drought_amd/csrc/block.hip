@@ -59,6 +59,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
 }
 
 struct SaveBufs {
+  float *Wqkv, *Wqk;  // stacked projection weights [Wq; Wk; Wv] (QW, N) and [W_Q'; W_K'] (2KD, D)
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float* conv[3];
   float *G, *tco, *r, *mu_c, *rs_c, *u_et, *mu_et, *rs_et;
@@ -66,6 +67,8 @@ struct SaveBufs {
 
 SaveBufs plan_save(const Dims& m, Arena& a) {
   SaveBufs s;
+  s.Wqkv = a.take(m.QW * m.N);
+  s.Wqk = a.take(2 * m.KD * m.D);
   s.E = a.take(m.BFT * m.N);
   s.qkv = a.take(m.BFT * m.QW);
   s.att = a.take(m.BFT * m.h * m.T);
@@ -106,7 +109,7 @@ struct Scratch {
   float *Wp, *thcat, *tc, *gemm_ws, *part, *Wg[3];
   // bwd (the *_side workspaces belong to the side stream; gcon_* / bcon_* / dres_t are
   // per-stage so the side stream's reductions never race a later main-chain write)
-  float *gemm_ws_side, *part_side;
+  float *gemm_ws_side, *part_side, *dWqkv, *dWqk;
   float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dG, *dconv[3], *dW, *dxth,
       *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dctx, *dqkv, *dscore, *du_et;
 };
@@ -124,6 +127,8 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.gpre = a.take(m.BN * m.CT);
   s.gemm_ws_side = a.take(kGemmWs);
   s.part_side = a.take(kPart);
+  s.dWqkv = a.take(m.QW * m.N);
+  s.dWqk = a.take(2 * m.KD * m.D);
   s.gcon_t = a.take(m.BN * m.CT);
   s.bcon_t = a.take(m.BN * m.CT);
   s.dres_t = a.take(m.BN * m.CT);
@@ -357,16 +362,19 @@ struct Fwd {
     } else {
       DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, N * m.FT, m.FT * N, 0.f, st));
     }
-    // Q | K | V projections  (MultiHeadAttention :92-94)
-    const float* wts[3] = {p.tat_wq, p.tat_wk, p.tat_wv};
-    const int64_t cols[3] = {m.HQ, m.HQ, m.HV};
-    const int64_t offs[3] = {0, m.HQ, 2 * m.HQ};
-    for (int q = 0; q < 3; ++q) {
+    // Q | K | V projections (MultiHeadAttention :92-94) as ONE GEMM over the stacked weights
+    {
+      PackRows pk;
+      pk.n = 3; pk.cols = m.N;
+      pk.src[0] = p.tat_wq; pk.src[1] = p.tat_wk; pk.src[2] = p.tat_wv;
+      pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
+      pk.dst[0] = s.Wqkv;
+      DS_TRY(op_pack_rows(pk, st));
       Gemm g;
-      g.M = (int)m.BFT; g.N = (int)cols[q]; g.K = m.N;
+      g.M = (int)m.BFT; g.N = (int)m.QW; g.K = m.N;
       g.A = s.E; g.am = idx1(N); g.ak = idx1(1);
-      g.B = wts[q]; g.bk = idx1(1); g.bn = idx1(N);
-      g.C = s.qkv; g.c_off = offs[q]; g.cm = idx1(m.QW); g.cn = idx1(1);
+      g.B = s.Wqkv; g.bk = idx1(1); g.bn = idx1(N);
+      g.C = s.qkv; g.cm = idx1(m.QW); g.cn = idx1(1);
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
     DS_TRY(op_tat_fwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, res, d.res_mode, re_at, s.att, s.ctx, st));
@@ -424,13 +432,18 @@ struct Fwd {
       if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
       DS_TRY(op_ln_fwd(a, st));
     }
-    const float* wts[2] = {p.sat_wq, p.sat_wk};
-    for (int q = 0; q < 2; ++q) {  // SMultiHeadAttention W_Q / W_K (:62-63)
+    {  // SMultiHeadAttention W_Q / W_K (:62-63) as ONE GEMM over the stacked weights
+      PackRows pk;
+      pk.n = 2; pk.cols = m.D;
+      pk.src[0] = p.sat_wq; pk.src[1] = p.sat_wk;
+      pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
+      pk.dst[0] = s.Wqk;
+      DS_TRY(op_pack_rows(pk, st));
       Gemm g;
-      g.M = (int)m.BN; g.N = (int)m.KD; g.K = m.D;
+      g.M = (int)m.BN; g.N = (int)(2 * m.KD); g.K = m.D;
       g.A = s.Zd; g.am = idx1(m.D); g.ak = idx1(1);
-      g.B = wts[q]; g.bk = idx1(1); g.bn = idx1(m.D);
-      g.C = s.qk; g.c_off = q * m.KD; g.cm = idx1(2 * m.KD); g.cn = idx1(1);
+      g.B = s.Wqk; g.bk = idx1(1); g.bn = idx1(m.D);
+      g.C = s.qk; g.cm = idx1(2 * m.KD); g.cn = idx1(1);
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
     {  // S'[b,k] = Q'_k K'_k^T / sqrt(dk)  (:19) -> written into P (softmaxed in place)
@@ -740,24 +753,26 @@ struct Bwd {
       g.alpha = sc;
       DS_TRY(gemm(g));
     }
-    float* wg[2] = {gd.sat_wq, gd.sat_wk};
-    const float* wts[2] = {p.sat_wq, p.sat_wk};
     DS_TRY(fork());
-    for (int q = 0; q < 2; ++q) {
-      if (wg[q]) {  // side: dW'[n,d] = sum_r dqk[r, q*KD + n] Zd[r,d]
-        Gemm g;
-        g.M = (int)m.KD; g.N = m.D; g.K = (int)m.BN;
-        g.A = w.dqk; g.a_off = q * m.KD; g.am = idx1(1); g.ak = idx1(ld);
-        g.B = s.Zd; g.bk = idx1(m.D); g.bn = idx1(1);
-        g.C = wg[q]; g.cm = idx1(m.D); g.cn = idx1(1);
-        DS_TRY(sgemm(g));
-      }
-      Gemm g;  // dZd += dqk[:, q] W'
-      g.M = (int)m.BN; g.N = m.D; g.K = (int)m.KD;
-      g.A = w.dqk; g.a_off = q * m.KD; g.am = idx1(ld); g.ak = idx1(1);
-      g.B = wts[q]; g.bk = idx1(m.D); g.bn = idx1(1);
+    if (gd.sat_wq || gd.sat_wk) {  // side: [dW_Q'; dW_K'] = dqk^T Zd, then split
+      Gemm g;
+      g.M = (int)ld; g.N = m.D; g.K = (int)m.BN;
+      g.A = w.dqk; g.am = idx1(1); g.ak = idx1(ld);
+      g.B = s.Zd; g.bk = idx1(m.D); g.bn = idx1(1);
+      g.C = w.dWqk; g.cm = idx1(m.D); g.cn = idx1(1);
+      DS_TRY(sgemm(g));
+      PackRows pk;
+      pk.n = 2; pk.cols = m.D; pk.unpack = 1;
+      pk.src[0] = w.dWqk; pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
+      pk.dst[0] = gd.sat_wq; pk.dst[1] = gd.sat_wk;
+      DS_TRY(op_pack_rows(pk, sd));
+    }
+    {
+      Gemm g;  // dZd = dqk [W_Q'; W_K']
+      g.M = (int)m.BN; g.N = m.D; g.K = (int)ld;
+      g.A = w.dqk; g.am = idx1(ld); g.ak = idx1(1);
+      g.B = s.Wqk; g.bk = idx1(m.D); g.bn = idx1(1);
       g.C = w.dZd; g.cm = idx1(m.D); g.cn = idx1(1);
-      g.beta = q ? 1.f : 0.f;
       DS_TRY(gemm(g));
     }
     {  // EmbedS LN_D backward (dropout mask re-derived from the seed)
@@ -832,28 +847,27 @@ struct Bwd {
     DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, st));
     if (d.res_mode == DSTAGNN_RES_BCAST && dres)
       DS_TRY(op_sum_middle(w.dscore, m.B, m.F, (int64_t)m.h * m.T * m.T, dres, 0.f, st));
-    // dE = dU + sum_q dqkv_q W_q ;  dW_q = dqkv_q^T E  (side)
-    const float* wts[3] = {p.tat_wq, p.tat_wk, p.tat_wv};
-    float* wg[3] = {gd.tat_wq, gd.tat_wk, gd.tat_wv};
-    const int64_t cols[3] = {m.HQ, m.HQ, m.HV};
-    const int64_t offs[3] = {0, m.HQ, 2 * m.HQ};
+    // dE = dU + dqkv [Wq; Wk; Wv] ;  [dWq; dWk; dWv] = dqkv^T E  (side)
     DS_TRY(fork());
-    for (int q = 0; q < 3; ++q) {
-      if (wg[q]) {
-        Gemm g;
-        g.M = (int)cols[q]; g.N = m.N; g.K = (int)m.BFT;
-        g.A = w.dqkv; g.a_off = offs[q]; g.am = idx1(1); g.ak = idx1(m.QW);
-        g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
-        g.C = wg[q]; g.cm = idx1(N); g.cn = idx1(1);
-        DS_TRY(sgemm(g));
-      }
+    if (gd.tat_wq || gd.tat_wk || gd.tat_wv) {
+      Gemm g;
+      g.M = (int)m.QW; g.N = m.N; g.K = (int)m.BFT;
+      g.A = w.dqkv; g.am = idx1(1); g.ak = idx1(m.QW);
+      g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
+      g.C = w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
+      DS_TRY(sgemm(g));
+      PackRows pk;
+      pk.n = 3; pk.cols = m.N; pk.unpack = 1;
+      pk.src[0] = w.dWqkv; pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
+      pk.dst[0] = gd.tat_wq; pk.dst[1] = gd.tat_wk; pk.dst[2] = gd.tat_wv;
+      DS_TRY(op_pack_rows(pk, sd));
     }
     DS_TRY(join());  // the fc weight grad has read dU
-    for (int q = 0; q < 3; ++q) {
+    {
       Gemm g;
-      g.M = (int)m.BFT; g.N = m.N; g.K = (int)cols[q];
-      g.A = w.dqkv; g.a_off = offs[q]; g.am = idx1(m.QW); g.ak = idx1(1);
-      g.B = wts[q]; g.bk = idx1(N); g.bn = idx1(1);
+      g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.QW;
+      g.A = w.dqkv; g.am = idx1(m.QW); g.ak = idx1(1);
+      g.B = s.Wqkv; g.bk = idx1(N); g.bn = idx1(1);
       g.C = w.dU; g.cm = idx1(N); g.cn = idx1(1);
       g.beta = 1.f;
       DS_TRY(gemm(g));

@@ -525,6 +525,18 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void pack_rows_kernel(PackRows a) {
+  int r0 = 0;
+  for (int q = 0; q < a.n; ++q) {
+    const int64_t n = (int64_t)a.rows[q] * a.cols;
+    const float* src = a.unpack ? a.src[0] + (int64_t)r0 * a.cols : a.src[q];
+    float* dst = a.unpack ? a.dst[q] : a.dst[0] + (int64_t)r0 * a.cols;
+    if (dst)
+      for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+    r0 += a.rows[q];
+  }
+}
+
 __global__ __launch_bounds__(256) void gtu_weights_kernel(GtuWeights a) {
   const int C = a.C, C2 = 2 * C;
   for (int q = 0; q < 3; ++q) {
@@ -810,6 +822,14 @@ int op_cheb_mask_grad(const ChebSm& a, hipStream_t st) {
 
 int op_gate_fwd(const GateArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(gate_fwd_kernel, dim3((unsigned)std::min<int64_t>(a.BN, 4096)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+int op_pack_rows(const PackRows& a, hipStream_t st) {
+  if (a.n < 1 || a.n > 8) { set_last_error("pack_rows: 1..8 matrices"); return DSTAGNN_E_ARG; }
+  int64_t mx = 1;
+  for (int q = 0; q < a.n; ++q) mx = std::max<int64_t>(mx, (int64_t)a.rows[q] * a.cols);
+  hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(mx, 256), 1024)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -64,6 +64,15 @@ struct GtuWeights {
   float* perm[3] = {};
 };
 
+// Stack up to 8 row-major matrices (rows_i x cols) into one (sum rows_i) x cols matrix
+// (unpack = 1: the inverse, null destinations skipped) — fuses same-input projections.
+struct PackRows {
+  int n = 0, cols = 0, unpack = 0;
+  int rows[8] = {};
+  const float* src[8] = {};   // pack sources / unpack: src[0] = packed
+  float* dst[8] = {};         // pack: dst[0] = packed / unpack destinations
+};
+
 struct GateArgs {
   int64_t BN = 0; int C = 0, T = 0;
   const float* conv[3] = {};      // [bn][T-ks+1][2C]
@@ -134,6 +143,7 @@ int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st);
 int op_cheb_mask_grad(const ChebSm& a, hipStream_t st);
 int op_gate_fwd(const GateArgs& a, hipStream_t st);
 int op_gtu_weights(const GtuWeights& a, hipStream_t st);
+int op_pack_rows(const PackRows& a, hipStream_t st);
 int op_gate_bwd(const GateArgs& a, hipStream_t st);
 int op_tail_fwd(const TailArgs& a, hipStream_t st);
 int op_tail_bwd(const TailArgs& a, hipStream_t st);
