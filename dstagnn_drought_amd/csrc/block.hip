@@ -59,7 +59,10 @@ Dims mkdims(const dstagnn_block_dims& d) {
 }
 
 struct SaveBufs {
-  float *Wqkv, *Wqk;  // stacked projection weights [Wq; Wk; Wv] (QW, N) and [W_Q'; W_K'] (2KD, D)
+  // parameters re-laid once per forward (side stream) and reused by the backward:
+  // stacked projections [Wq; Wk; Wv] (QW, N) and [W_Q'; W_K'] (2KD, D), pre_conv as
+  // (D, F*T), Theta_cat (F, K*C), GTU conv weights (o, j, c) fwd and (j', o, c) flipped bwd
+  float *Wqkv, *Wqk, *Wp, *thcat, *Wgf[3], *Wgb[3];
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float* conv[3];
   float *G, *tco, *r, *mu_c, *rs_c, *u_et, *mu_et, *rs_et;
@@ -69,6 +72,10 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   SaveBufs s;
   s.Wqkv = a.take(m.QW * m.N);
   s.Wqk = a.take(2 * m.KD * m.D);
+  s.Wp = a.take((int64_t)m.D * m.FT);
+  s.thcat = a.take((int64_t)m.F * m.KC);
+  for (int g = 0; g < 3; ++g) s.Wgf[g] = a.take(2 * (int64_t)m.C * m.C * m.ks[g]);
+  for (int g = 0; g < 3; ++g) s.Wgb[g] = a.take(2 * (int64_t)m.C * m.C * m.ks[g]);
   s.E = a.take(m.BFT * m.N);
   s.qkv = a.take(m.BFT * m.QW);
   s.att = a.take(m.BFT * m.h * m.T);
@@ -106,7 +113,7 @@ constexpr size_t kGemmWs = size_t(8) << 20;   // floats (32 MB) for split-K part
 constexpr size_t kPart = size_t(2) << 20;      // floats (8 MB) for column-sum partials
 
 struct Scratch {
-  float *Wp, *thcat, *tc, *gemm_ws, *part, *Wg[3];
+  float *tc, *gemm_ws, *part;
   // bwd (the *_side workspaces belong to the side stream; gcon_* / bcon_* / dres_t are
   // per-stage so the side stream's reductions never race a later main-chain write)
   float *gemm_ws_side, *part_side, *dWqkv, *dWqk;
@@ -118,9 +125,6 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   Scratch s;
   s.gemm_ws = a.take(kGemmWs);
   s.part = a.take(kPart);
-  s.Wp = a.take((int64_t)m.D * m.FT);
-  s.thcat = a.take((int64_t)m.F * m.KC);
-  for (int g = 0; g < 3; ++g) s.Wg[g] = a.take(2 * (int64_t)m.C * m.C * m.ks[g]);
   s.tc = a.take(m.BN * m.CT);
   s.dtc = a.take(m.BN * m.CT);
   s.dX = a.take(m.BN * m.CT);
@@ -331,195 +335,7 @@ int unpack_theta(const float* thcat, int K, int F, int C, float* const* dtheta, 
 }
 
 // ------------------------------------------------------------------------------
-// forward
-// ------------------------------------------------------------------------------
-struct Fwd {
-  const Dims& m;
-  const dstagnn_block_dims& d;
-  const dstagnn_block_params& p;
-  const dstagnn_graph& gr;
-  const float* x;
-  const float* res;
-  float* out;
-  float* re_at;
-  SaveBufs& s;
-  Scratch& w;
-  hipStream_t st;
-
-  int stage_tat() {
-    const int64_t N = m.N;
-    // E: TAt input (B,F,T,N)
-    if (m.first) {
-      LnFwd a;
-      a.R = m.B * m.T; a.L = m.N;
-      a.src[0].p = x; a.src[0].row = idx2(m.T, 1, (int64_t)m.N * m.T); a.src[0].es = m.T;
-      a.src[1].p = p.embT_pos; a.src[1].row = idx2(m.T, m.N, 0); a.src[1].es = 1;
-      a.nsrc = 2;
-      a.g = p.embT_g; a.b = p.embT_b;
-      a.y = s.E; a.yrow = idx1(N); a.yes = 1;
-      a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et;
-      DS_TRY(op_ln_fwd(a, st));
-    } else {
-      DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, N * m.FT, m.FT * N, 0.f, st));
-    }
-    // Q | K | V projections (MultiHeadAttention :92-94) as ONE GEMM over the stacked weights
-    {
-      PackRows pk;
-      pk.n = 3; pk.cols = m.N;
-      pk.src[0] = p.tat_wq; pk.src[1] = p.tat_wk; pk.src[2] = p.tat_wv;
-      pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
-      pk.dst[0] = s.Wqkv;
-      DS_TRY(op_pack_rows(pk, st));
-      Gemm g;
-      g.M = (int)m.BFT; g.N = (int)m.QW; g.K = m.N;
-      g.A = s.E; g.am = idx1(N); g.ak = idx1(1);
-      g.B = s.Wqkv; g.bk = idx1(1); g.bn = idx1(N);
-      g.C = s.qkv; g.cm = idx1(m.QW); g.cn = idx1(1);
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
-    }
-    DS_TRY(op_tat_fwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, res, d.res_mode, re_at, s.att, s.ctx, st));
-    // fc (:99)
-    {
-      Gemm g;
-      g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.HV;
-      g.A = s.ctx; g.am = idx1(m.HV); g.ak = idx1(1);
-      g.B = p.tat_fc; g.bk = idx1(1); g.bn = idx1(m.HV);
-      g.C = s.u_tat; g.cm = idx1(N); g.cn = idx1(1);
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
-    }
-    // LN_N(fc + E) (:100)
-    {
-      LnFwd a;
-      a.R = (int)m.BFT; a.L = m.N;
-      a.src[0].p = s.u_tat; a.src[0].row = idx1(N);
-      a.src[1].p = s.E; a.src[1].row = idx1(N);
-      a.nsrc = 2;
-      a.g = p.tat_ln_g; a.b = p.tat_ln_b;
-      a.y = s.O; a.yrow = idx1(N);
-      a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat;
-      DS_TRY(op_ln_fwd(a, st));
-    }
-    return 0;
-  }
-
-  Gemm preconv_gemm() {
-    Gemm g;  // u_s[(b,n), d] = bias[d] + sum_{(f,t)} O[b,f,t,n] Wp[d,(f,t)]
-    g.M = (int)m.BN; g.N = m.D; g.K = (int)m.FT;
-    g.A = s.O; g.am = idx2(m.N, 1, m.FT * m.N); g.ak = idx1(m.N);
-    g.B = w.Wp; g.bk = idx1(1); g.bn = idx1(m.FT);
-    g.C = s.u_s; g.cm = idx1(m.D); g.cn = idx1(1);
-    g.bias = p.pre_conv_b;
-    g.hot = 1;
-    return g;
-  }
-
-  int stage_preconv() {
-    // Wp[d][f][t] = pre_conv.weight[d][t][0][f]
-    DS_TRY(op_transpose(p.pre_conv_w, w.Wp, m.T, m.F, m.D, m.FT, m.FT, 0.f, st));
-    return run_gemm(preconv_gemm(), w.gemm_ws, kGemmWs, st);
-  }
-
-  int stage_sat() {
-    {  // EmbedS LN_D(y + pos) + dropout (:233-234)
-      LnFwd a;
-      a.R = (int)m.BN; a.L = m.D;
-      a.src[0].p = s.u_s; a.src[0].row = idx1(m.D);
-      a.src[1].p = p.embS_pos; a.src[1].row = idx2(m.N, m.D, 0);
-      a.nsrc = 2;
-      a.g = p.embS_g; a.b = p.embS_b;
-      a.y = s.Zd; a.yrow = idx1(m.D);
-      a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s;
-      if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
-      DS_TRY(op_ln_fwd(a, st));
-    }
-    {  // SMultiHeadAttention W_Q / W_K (:62-63) as ONE GEMM over the stacked weights
-      PackRows pk;
-      pk.n = 2; pk.cols = m.D;
-      pk.src[0] = p.sat_wq; pk.src[1] = p.sat_wk;
-      pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
-      pk.dst[0] = s.Wqk;
-      DS_TRY(op_pack_rows(pk, st));
-      Gemm g;
-      g.M = (int)m.BN; g.N = (int)(2 * m.KD); g.K = m.D;
-      g.A = s.Zd; g.am = idx1(m.D); g.ak = idx1(1);
-      g.B = s.Wqk; g.bk = idx1(1); g.bn = idx1(m.D);
-      g.C = s.qk; g.cm = idx1(2 * m.KD); g.cn = idx1(1);
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
-    }
-    {  // S'[b,k] = Q'_k K'_k^T / sqrt(dk)  (:19) -> written into P (softmaxed in place)
-      Gemm g;
-      g.M = m.N; g.N = m.N; g.K = m.dk; g.batch = m.B * m.K;
-      g.A = s.qk; g.am = idx1(2 * m.KD); g.ak = idx1(1); g.az = idx2(m.K, m.dk, m.N * 2 * m.KD);
-      g.B = s.qk; g.b_off = m.KD; g.bk = idx1(1); g.bn = idx1(2 * m.KD); g.bz = idx2(m.K, m.dk, m.N * 2 * m.KD);
-      g.C = s.P; g.cm = idx1(m.N); g.cn = idx1(1); g.cz = idx1(m.NN);
-      g.alpha = 1.f / sqrtf((float)m.dk);
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
-    }
-    return 0;
-  }
-
-  int stage_cheb() {
-    DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, w.thcat, st));
-    ChebIO c;
-    c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
-    c.x = x; c.S = s.P; c.mask = p.mask; c.g = &gr; c.sparse = m.sparse; c.thcat = w.thcat;
-    c.P = s.P; c.W = s.W; c.xth = s.xth; c.X = s.X;
-    return cheb_forward(c, w.gemm_ws, st);
-  }
-
-  int stage_tail() {
-    {  // GTU conv weights re-laid (o, j, c) so the im2col k map is single-level
-      GtuWeights gw;
-      gw.C = m.C; gw.mode = 0;
-      for (int q = 0; q < 3; ++q) { gw.w[q] = p.gtu_w[q]; gw.perm[q] = w.Wg[q]; }
-      DS_TRY(op_gtu_weights(gw, st));
-    }
-    for (int q = 0; q < 3; ++q) {  // GTU convs (:190) as implicit-im2col GEMMs
-      // conv[(bn,t), o] = b[o] + sum_{(j,c)} X[bn, t+j, c] W[o,c,j]; with X rows (t,c) the
-      // window (j, c) is one contiguous run of ks*C floats
-      const int ks = m.ks[q], Tg = m.Tg[q];
-      Gemm g;
-      g.M = (int)(m.BN * Tg); g.N = 2 * m.C; g.K = m.C * ks;
-      g.A = s.X; g.am = idx2(Tg, m.C, m.CT); g.ak = idx1(1);
-      g.B = w.Wg[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);
-      g.C = s.conv[q]; g.cm = idx1(2 * m.C); g.cn = idx1(1);
-      g.bias = p.gtu_b[q];
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
-    }
-    GateArgs ga;
-    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
-    for (int q = 0; q < 3; ++q) ga.conv[q] = s.conv[q];
-    ga.G = s.G;
-    DS_TRY(op_gate_fwd(ga, st));
-    {  // fcmy (:243)
-      Gemm g;
-      g.M = (int)(m.BN * m.C); g.N = m.T; g.K = (int)m.S;
-      g.A = s.G; g.am = idx1(m.S); g.ak = idx1(1);
-      g.B = p.fcmy_w; g.bk = idx1(1); g.bn = idx1(m.S);
-      g.C = w.tc; g.cm = idx1(m.T); g.cn = idx1(1);
-      g.bias = p.fcmy_b;
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
-    }
-    TailArgs t;
-    t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
-    t.X = s.X; t.tc = w.tc; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
-    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
-    t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c; t.out = out;
-    return op_tail_fwd(t, st);
-  }
-
-  int run() {
-    DS_TRY(stage_tat());
-    DS_TRY(stage_preconv());
-    DS_TRY(stage_sat());
-    DS_TRY(stage_cheb());
-    DS_TRY(stage_tail());
-    return 0;
-  }
-};
-
-// ------------------------------------------------------------------------------
-// backward
+// side stream
 // ------------------------------------------------------------------------------
 // The backward has two dependency chains: the data gradients (dx -> ... -> d_x, each step
 // needing the previous) and the parameter gradients (weight GEMMs, bias / gamma / beta
@@ -556,6 +372,234 @@ SideStream* side_stream_for_device() {
   return &s;
 }
 
+// fork / join between the caller's stream and the side stream (no-ops when disabled)
+struct Streams {
+  hipStream_t st = nullptr, sd = nullptr;
+  SideStream* ss = nullptr;
+  void init(hipStream_t main) {
+    st = main;
+    ss = side_stream_for_device();
+    sd = ss ? ss->side : st;
+  }
+  int event_pair(hipStream_t from, hipStream_t to) {
+    if (from == to) return 0;
+    hipEvent_t e = ss->ev[ss->next];
+    ss->next = (ss->next + 1) % 64;
+    hipError_t r = hipEventRecord(e, from);
+    if (r == hipSuccess) r = hipStreamWaitEvent(to, e, 0);
+    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
+    return 0;
+  }
+  int fork() { return event_pair(st, sd); }  // side sees everything the main chain issued so far
+  int join() { return event_pair(sd, st); }  // main waits for everything issued on the side
+};
+
+// ------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------
+struct Fwd {
+  const Dims& m;
+  const dstagnn_block_dims& d;
+  const dstagnn_block_params& p;
+  const dstagnn_graph& gr;
+  const float* x;
+  const float* res;
+  float* out;
+  float* re_at;
+  SaveBufs& s;
+  Scratch& w;
+  hipStream_t st;
+  Streams ks;
+
+  int stage_tat() {
+    const int64_t N = m.N;
+    // E: TAt input (B,F,T,N)
+    if (m.first) {
+      LnFwd a;
+      a.R = m.B * m.T; a.L = m.N;
+      a.src[0].p = x; a.src[0].row = idx2(m.T, 1, (int64_t)m.N * m.T); a.src[0].es = m.T;
+      a.src[1].p = p.embT_pos; a.src[1].row = idx2(m.T, m.N, 0); a.src[1].es = 1;
+      a.nsrc = 2;
+      a.g = p.embT_g; a.b = p.embT_b;
+      a.y = s.E; a.yrow = idx1(N); a.yes = 1;
+      a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et;
+      DS_TRY(op_ln_fwd(a, st));
+    } else {
+      DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, N * m.FT, m.FT * N, 0.f, st));
+    }
+    // Q | K | V projections (MultiHeadAttention :92-94) as ONE GEMM over the stacked weights
+    DS_TRY(ks.join());  // the re-laid parameters (stage_params, side stream)
+    {
+      Gemm g;
+      g.M = (int)m.BFT; g.N = (int)m.QW; g.K = m.N;
+      g.A = s.E; g.am = idx1(N); g.ak = idx1(1);
+      g.B = s.Wqkv; g.bk = idx1(1); g.bn = idx1(N);
+      g.C = s.qkv; g.cm = idx1(m.QW); g.cn = idx1(1);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    DS_TRY(op_tat_fwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, res, d.res_mode, re_at, s.att, s.ctx, st));
+    // fc (:99)
+    {
+      Gemm g;
+      g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.HV;
+      g.A = s.ctx; g.am = idx1(m.HV); g.ak = idx1(1);
+      g.B = p.tat_fc; g.bk = idx1(1); g.bn = idx1(m.HV);
+      g.C = s.u_tat; g.cm = idx1(N); g.cn = idx1(1);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    // LN_N(fc + E) (:100)
+    {
+      LnFwd a;
+      a.R = (int)m.BFT; a.L = m.N;
+      a.src[0].p = s.u_tat; a.src[0].row = idx1(N);
+      a.src[1].p = s.E; a.src[1].row = idx1(N);
+      a.nsrc = 2;
+      a.g = p.tat_ln_g; a.b = p.tat_ln_b;
+      a.y = s.O; a.yrow = idx1(N);
+      a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat;
+      DS_TRY(op_ln_fwd(a, st));
+    }
+    return 0;
+  }
+
+  Gemm preconv_gemm() {
+    Gemm g;  // u_s[(b,n), d] = bias[d] + sum_{(f,t)} O[b,f,t,n] Wp[d,(f,t)]
+    g.M = (int)m.BN; g.N = m.D; g.K = (int)m.FT;
+    g.A = s.O; g.am = idx2(m.N, 1, m.FT * m.N); g.ak = idx1(m.N);
+    g.B = s.Wp; g.bk = idx1(1); g.bn = idx1(m.FT);
+    g.C = s.u_s; g.cm = idx1(m.D); g.cn = idx1(1);
+    g.bias = p.pre_conv_b;
+    g.hot = 1;
+    return g;
+  }
+
+  int stage_preconv() { return run_gemm(preconv_gemm(), w.gemm_ws, kGemmWs, st); }
+
+  // every parameter re-layout, on the side stream while the main chain starts
+  int stage_params() {
+    DS_TRY(ks.fork());
+    hipStream_t q = ks.sd;
+    {
+      PackRows pk;
+      pk.n = 3; pk.cols = m.N;
+      pk.src[0] = p.tat_wq; pk.src[1] = p.tat_wk; pk.src[2] = p.tat_wv;
+      pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
+      pk.dst[0] = s.Wqkv;
+      DS_TRY(op_pack_rows(pk, q));
+    }
+    {
+      PackRows pk;
+      pk.n = 2; pk.cols = m.D;
+      pk.src[0] = p.sat_wq; pk.src[1] = p.sat_wk;
+      pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
+      pk.dst[0] = s.Wqk;
+      DS_TRY(op_pack_rows(pk, q));
+    }
+    // Wp[d][f][t] = pre_conv.weight[d][t][0][f]
+    DS_TRY(op_transpose(p.pre_conv_w, s.Wp, m.T, m.F, m.D, m.FT, m.FT, 0.f, q));
+    DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, s.thcat, q));
+    GtuWeights gw;
+    gw.C = m.C;
+    for (int g = 0; g < 3; ++g) { gw.w[g] = p.gtu_w[g]; gw.perm[g] = s.Wgf[g]; }
+    gw.mode = 0;
+    DS_TRY(op_gtu_weights(gw, q));
+    for (int g = 0; g < 3; ++g) gw.perm[g] = s.Wgb[g];
+    gw.mode = 1;
+    DS_TRY(op_gtu_weights(gw, q));
+    return 0;
+  }
+
+  int stage_sat() {
+    {  // EmbedS LN_D(y + pos) + dropout (:233-234)
+      LnFwd a;
+      a.R = (int)m.BN; a.L = m.D;
+      a.src[0].p = s.u_s; a.src[0].row = idx1(m.D);
+      a.src[1].p = p.embS_pos; a.src[1].row = idx2(m.N, m.D, 0);
+      a.nsrc = 2;
+      a.g = p.embS_g; a.b = p.embS_b;
+      a.y = s.Zd; a.yrow = idx1(m.D);
+      a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s;
+      if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
+      DS_TRY(op_ln_fwd(a, st));
+    }
+    {  // SMultiHeadAttention W_Q / W_K (:62-63) as ONE GEMM over the stacked weights
+      Gemm g;
+      g.M = (int)m.BN; g.N = (int)(2 * m.KD); g.K = m.D;
+      g.A = s.Zd; g.am = idx1(m.D); g.ak = idx1(1);
+      g.B = s.Wqk; g.bk = idx1(1); g.bn = idx1(m.D);
+      g.C = s.qk; g.cm = idx1(2 * m.KD); g.cn = idx1(1);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    {  // S'[b,k] = Q'_k K'_k^T / sqrt(dk)  (:19) -> written into P (softmaxed in place)
+      Gemm g;
+      g.M = m.N; g.N = m.N; g.K = m.dk; g.batch = m.B * m.K;
+      g.A = s.qk; g.am = idx1(2 * m.KD); g.ak = idx1(1); g.az = idx2(m.K, m.dk, m.N * 2 * m.KD);
+      g.B = s.qk; g.b_off = m.KD; g.bk = idx1(1); g.bn = idx1(2 * m.KD); g.bz = idx2(m.K, m.dk, m.N * 2 * m.KD);
+      g.C = s.P; g.cm = idx1(m.N); g.cn = idx1(1); g.cz = idx1(m.NN);
+      g.alpha = 1.f / sqrtf((float)m.dk);
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    return 0;
+  }
+
+  int stage_cheb() {
+    ChebIO c;
+    c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
+    c.x = x; c.S = s.P; c.mask = p.mask; c.g = &gr; c.sparse = m.sparse; c.thcat = s.thcat;
+    c.P = s.P; c.W = s.W; c.xth = s.xth; c.X = s.X;
+    return cheb_forward(c, w.gemm_ws, st);
+  }
+
+  int stage_tail() {
+    for (int q = 0; q < 3; ++q) {  // GTU convs (:190) as implicit-im2col GEMMs
+      // conv[(bn,t), o] = b[o] + sum_{(j,c)} X[bn, t+j, c] W[o,c,j]; with X rows (t,c) the
+      // window (j, c) is one contiguous run of ks*C floats
+      const int ks = m.ks[q], Tg = m.Tg[q];
+      Gemm g;
+      g.M = (int)(m.BN * Tg); g.N = 2 * m.C; g.K = m.C * ks;
+      g.A = s.X; g.am = idx2(Tg, m.C, m.CT); g.ak = idx1(1);
+      g.B = s.Wgf[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);  // re-laid (o, j, c)
+      g.C = s.conv[q]; g.cm = idx1(2 * m.C); g.cn = idx1(1);
+      g.bias = p.gtu_b[q];
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    GateArgs ga;
+    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
+    for (int q = 0; q < 3; ++q) ga.conv[q] = s.conv[q];
+    ga.G = s.G;
+    DS_TRY(op_gate_fwd(ga, st));
+    {  // fcmy (:243)
+      Gemm g;
+      g.M = (int)(m.BN * m.C); g.N = m.T; g.K = (int)m.S;
+      g.A = s.G; g.am = idx1(m.S); g.ak = idx1(1);
+      g.B = p.fcmy_w; g.bk = idx1(1); g.bn = idx1(m.S);
+      g.C = w.tc; g.cm = idx1(m.T); g.cn = idx1(1);
+      g.bias = p.fcmy_b;
+      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+    }
+    TailArgs t;
+    t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
+    t.X = s.X; t.tc = w.tc; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
+    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
+    t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c; t.out = out;
+    return op_tail_fwd(t, st);
+  }
+
+  int run() {
+    ks.init(st);
+    DS_TRY(stage_params());
+    DS_TRY(stage_tat());
+    DS_TRY(stage_preconv());
+    DS_TRY(stage_sat());
+    DS_TRY(stage_cheb());
+    DS_TRY(stage_tail());
+    return 0;
+  }
+};
+
+// ------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------
 struct Bwd {
   const Dims& m;
   const dstagnn_block_dims& d;
@@ -570,20 +614,10 @@ struct Bwd {
   SaveBufs& s;
   Scratch& w;
   hipStream_t st;
-  SideStream* ss = nullptr;
+  Streams ks;
   hipStream_t sd = nullptr;  // side stream (== st when disabled)
-
-  int event_pair(hipStream_t from, hipStream_t to) {
-    if (from == to) return 0;
-    hipEvent_t e = ss->ev[ss->next];
-    ss->next = (ss->next + 1) % 64;
-    hipError_t r = hipEventRecord(e, from);
-    if (r == hipSuccess) r = hipStreamWaitEvent(to, e, 0);
-    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
-    return 0;
-  }
-  int fork() { return event_pair(st, sd); }  // side sees everything the main chain issued so far
-  int join() { return event_pair(sd, st); }  // main waits for everything issued on the side
+  int fork() { return ks.fork(); }
+  int join() { return ks.join(); }
 
   int colsum_on(hipStream_t q, const float* in, int64_t A, int O, int I, float* out) {
     if (!out) return 0;
@@ -639,12 +673,6 @@ struct Bwd {
     for (int q = 0; q < 3; ++q) { ga.conv[q] = s.conv[q]; ga.dconv_pad[q] = w.dconv[q]; }
     ga.dG = w.dG;
     DS_TRY(op_gate_bwd(ga, st));
-    {  // flipped conv weights (j', o, c) for the transposed convolution
-      GtuWeights gw;
-      gw.C = m.C; gw.mode = 1;
-      for (int q = 0; q < 3; ++q) { gw.w[q] = p.gtu_w[q]; gw.perm[q] = w.Wg[q]; }
-      DS_TRY(op_gtu_weights(gw, st));
-    }
     DS_TRY(fork());
     for (int q = 0; q < 3; ++q) {
       const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
@@ -663,7 +691,7 @@ struct Bwd {
         Gemm g;  // dX[bn,t,c] += sum_{(j',o)} dconv_pad[bn,t+j',o] W[o,c,ks-1-j']
         g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
         g.A = w.dconv[q]; g.am = idx2(m.T, C2, cs); g.ak = idx1(1);
-        g.B = w.Wg[q]; g.bk = idx1(m.C); g.bn = idx1(1);
+        g.B = s.Wgb[q]; g.bk = idx1(m.C); g.bn = idx1(1);  // flipped (j', o, c)
         g.C = w.dX; g.cm = idx1(m.C); g.cn = idx1(1);
         g.beta = 1.f;
         DS_TRY(gemm(g));
@@ -674,7 +702,6 @@ struct Bwd {
 
   int stage_cheb() {
     DS_TRY(op_relu_mask(w.dX, s.X, w.gpre, m.BN * m.CT, st));
-    DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, w.thcat, st));
     const int64_t NN = m.NN, KC = m.KC, T = m.T, CT = m.CT, KCT = m.KCT, FT = m.FT;
     const int B = m.B, N = m.N, K = m.K, C = m.C, F = m.F;
     if (m.sparse) {
@@ -724,7 +751,7 @@ struct Bwd {
       Gemm g;  // dx[b,i,f,t] += sum_{k,c} Theta_k[f,c] dxth[b,i,t,k,c]
       g.M = B * N * m.T; g.N = F; g.K = (int)KC;
       g.A = w.dxth; g.am = idx1(KC); g.ak = idx1(1);
-      g.B = w.thcat; g.bk = idx1(1); g.bn = idx1(KC);
+      g.B = s.thcat; g.bk = idx1(1); g.bn = idx1(KC);
       g.C = dx; g.cm = idx2(T, 1, FT); g.cn = idx1(T);
       g.beta = 1.f;
       DS_TRY(gemm(g));
@@ -803,10 +830,9 @@ struct Bwd {
   }
 
   int stage_preconv() {
-    DS_TRY(op_transpose(p.pre_conv_w, w.Wp, m.T, m.F, m.D, m.FT, m.FT, 0.f, st));
     Gemm g;  // dO[b,(f,t),n] = sum_d Wp[d,(f,t)] dY[(b,n),d]
     g.M = (int)m.FT; g.N = (int)m.BN; g.K = m.D;
-    g.A = w.Wp; g.am = idx1(1); g.ak = idx1(m.FT);
+    g.A = s.Wp; g.am = idx1(1); g.ak = idx1(m.FT);
     g.B = w.dY; g.bk = idx1(1); g.bn = idx1(m.D);
     g.C = w.dO; g.cm = idx1(m.N); g.cn = idx2(m.N, 1, m.FT * m.N);
     return gemm(g);
@@ -892,8 +918,8 @@ struct Bwd {
   }
 
   int run() {
-    ss = (st != nullptr || true) ? side_stream_for_device() : nullptr;
-    sd = ss ? ss->side : st;
+    ks.init(st);
+    sd = ks.sd;
     DS_TRY(stage_tail());
     DS_TRY(stage_cheb());
     DS_TRY(stage_sat());
