@@ -173,6 +173,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_issue = time.perf_counter() - t0  # host time to issue the steps (launch-bound if ~ elapsed)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -183,7 +184,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
-    log(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step")
+    log(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step (host issue {t_issue / args.steps * 1e3:.3f} ms/step)")
     value = world * B * args.steps / elapsed
 
     # ---- dominant kernel: the pre_conv fwd GEMM (gemm_f32_hot_kernel), HIP events on its stream

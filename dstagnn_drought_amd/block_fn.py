@@ -91,11 +91,64 @@ def use_sparse(graph, meta, T):
     return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= 1024
 
 
+_SIZES = {}
+
+
 def workspace_sizes(dims):
-    lib = _lib.load()
-    sv, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
-    _lib.check(lib.dstagnn_block_sizes(ctypes.byref(dims), ctypes.byref(sv), ctypes.byref(sc)), "dstagnn_block_sizes")
-    return sv.value, sc.value
+    key = bytes(dims)
+    r = _SIZES.get(key)
+    if r is None:
+        lib = _lib.load()
+        sv, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
+        _lib.check(lib.dstagnn_block_sizes(ctypes.byref(dims), ctypes.byref(sv), ctypes.byref(sc)),
+                   "dstagnn_block_sizes")
+        r = _SIZES[key] = (sv.value, sc.value)
+    return r
+
+
+# host-side caches for the per-call argument structs (the block is launch-bound on the host
+# at the benchmark size): keyed by the device pointers they hold
+_PSTRUCT = {}
+_GSTRUCT = {}
+
+
+def _params_struct(names, params):
+    key = (names, tuple(t.data_ptr() for t in params))
+    st = _PSTRUCT.get(key)
+    if st is None:
+        if len(_PSTRUCT) > 64:
+            _PSTRUCT.clear()
+        st = _PSTRUCT[key] = _fill(_lib.BlockParams(), names, params)
+    return st
+
+
+def _graph_struct_cached(graph):
+    key = tuple((k, v.data_ptr(), v.numel()) for k, v in graph.items() if v is not None)
+    st = _GSTRUCT.get(key)
+    if st is None:
+        if len(_GSTRUCT) > 64:
+            _GSTRUCT.clear()
+        st = _GSTRUCT[key] = graph_struct(graph)
+    return st
+
+
+_GLAYOUT = {}
+
+
+def _grad_layout(names, params, first):
+    """Offsets of every used parameter's gradient in one flat buffer (256-B aligned slots)."""
+    key = (names, tuple(tuple(t.shape) for t in params), first)
+    lay = _GLAYOUT.get(key)
+    if lay is None:
+        offs, total = [], 0
+        for n, t in zip(names, params):
+            if first or not n.startswith(UNUSED_INNER):
+                offs.append(total)
+                total += (t.numel() + 63) // 64 * 64
+            else:
+                offs.append(None)
+        lay = _GLAYOUT[key] = (offs, total)
+    return lay
 
 
 class DSTAGNNBlockFunction(torch.autograd.Function):
@@ -116,8 +169,8 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
         out = torch.empty(B, N, meta["C"], T, dtype=torch.float32, device=dev)
         re_at = torch.empty(B, F, meta["n_heads"], T, T, dtype=torch.float32, device=dev)
-        p = _fill(_lib.BlockParams(), names, params)
-        g = graph_struct(graph)
+        p = _params_struct(names, params)
+        g = _graph_struct_cached(graph)
         rc = lib.dstagnn_block_forward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
                                        _lib.ptr(ra), _lib.ptr(out), _lib.ptr(re_at), _lib.ptr(save), sv,
                                        _lib.ptr(scratch), sc, _lib.stream_handle(dev))
@@ -139,13 +192,14 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         d_out = d_out.contiguous()
         d_re_at = d_re_at.contiguous() if d_re_at is not None else None
         first = dims.F == 1
-        grads = []
-        for n, t in zip(names, params):
-            used = first or not n.startswith(UNUSED_INNER)
-            grads.append(torch.empty_like(t) if used else None)
+        # every parameter gradient is a view of ONE flat buffer: one allocation per
+        # backward instead of one per parameter (autograd adopts the views as .grad)
+        offs, total = _grad_layout(names, params, first)
+        flat = torch.empty(total, dtype=torch.float32, device=dev)
+        grads = [None if o is None else flat[o:o + t.numel()].view(t.shape) for o, t in zip(offs, params)]
         gs = _fill(_lib.BlockGrads(), names, grads)
-        p = _fill(_lib.BlockParams(), names, params)
-        g = graph_struct(ctx.graph)
+        p = _params_struct(names, params)
+        g = _graph_struct_cached(ctx.graph)
         d_x = torch.empty_like(x)
         d_ra = torch.empty_like(ra) if mode != _lib.RES_NONE else None
         sv, sc = ctx.sizes

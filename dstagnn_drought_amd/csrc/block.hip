@@ -14,7 +14,10 @@
 #include <string>
 
 #include "common.hpp"
+#include <chrono>
+#include <cstdio>
 #include <initializer_list>
+#include <map>
 #include <utility>
 #include "ops.hpp"
 
@@ -118,7 +121,7 @@ struct Scratch {
   // per-stage so the side stream's reductions never race a later main-chain write)
   float *gemm_ws_side, *part_side, *dWqkv, *dWqk;
   float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dG, *dconv[3], *dW, *dxth,
-      *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dctx, *dqkv, *dscore, *du_et;
+      *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dE, *dctx, *dqkv, *dscore, *du_et;
 };
 
 Scratch plan_scratch(const Dims& m, Arena& a) {
@@ -151,6 +154,7 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.dWp = a.take((int64_t)m.D * m.FT);
   s.dO = a.take(m.BFT * m.N);
   s.dU = a.take(m.BFT * m.N);
+  s.dE = a.take(m.BFT * m.N);
   s.dctx = a.take(m.BFT * m.HV);
   s.dqkv = a.take(m.BFT * m.QW);
   s.dscore = a.take(m.BFT * m.h * m.T);
@@ -334,6 +338,30 @@ int unpack_theta(const float* thcat, int K, int F, int C, float* const* dtheta, 
   return op_pack_theta(a, st);
 }
 
+// host-side issue timing per stage (DSTAGNN_HOST_PROFILE=1): accumulates and prints
+// the mean every 100 calls to stderr
+struct HostTimer {
+  bool on;
+  const char* tag;
+  std::chrono::steady_clock::time_point t;
+  static std::map<std::string, std::pair<double, long>>& acc() {
+    static std::map<std::string, std::pair<double, long>> a;
+    return a;
+  }
+  HostTimer(bool on_, const char* tag_) : on(on_), tag(tag_) {
+    if (on) t = std::chrono::steady_clock::now();
+  }
+  void lap(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    auto& e = acc()[std::string(tag) + "." + what];
+    e.first += std::chrono::duration<double, std::micro>(now - t).count();
+    e.second += 1;
+    t = now;
+    if (e.second % 100 == 0) fprintf(stderr, "[host] %s.%s %.1f us\n", tag, what, e.first / e.second);
+  }
+};
+
 // ------------------------------------------------------------------------------
 // side stream
 // ------------------------------------------------------------------------------
@@ -410,6 +438,7 @@ struct Fwd {
   Scratch& w;
   hipStream_t st;
   Streams ks;
+  bool params_forked = false;
 
   int stage_tat() {
     const int64_t N = m.N;
@@ -428,7 +457,7 @@ struct Fwd {
       DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, N * m.FT, m.FT * N, 0.f, st));
     }
     // Q | K | V projections (MultiHeadAttention :92-94) as ONE GEMM over the stacked weights
-    DS_TRY(ks.join());  // the re-laid parameters (stage_params, side stream)
+    if (params_forked) DS_TRY(ks.join());  // the re-laid parameters (stage_params on the side stream)
     {
       Gemm g;
       g.M = (int)m.BFT; g.N = (int)m.QW; g.K = m.N;
@@ -477,8 +506,12 @@ struct Fwd {
 
   // every parameter re-layout, on the side stream while the main chain starts
   int stage_params() {
-    DS_TRY(ks.fork());
-    hipStream_t q = ks.sd;
+    // on the caller's stream by default: the fork/join pair costs more host time (~15 us)
+    // than these six small launches cost GPU time; DSTAGNN_PARAMS_SIDE=1 moves them
+    static const bool on_side = getenv("DSTAGNN_PARAMS_SIDE") && atoi(getenv("DSTAGNN_PARAMS_SIDE")) != 0;
+    if (on_side) DS_TRY(ks.fork());
+    params_forked = on_side;
+    hipStream_t q = on_side ? ks.sd : st;
     {
       PackRows pk;
       pk.n = 3; pk.cols = m.N;
@@ -586,13 +619,21 @@ struct Fwd {
   }
 
   int run() {
+    static const bool prof = getenv("DSTAGNN_HOST_PROFILE") != nullptr;
+    HostTimer ht(prof, "fwd");
     ks.init(st);
     DS_TRY(stage_params());
+    ht.lap("params");
     DS_TRY(stage_tat());
+    ht.lap("tat");
     DS_TRY(stage_preconv());
+    ht.lap("preconv");
     DS_TRY(stage_sat());
+    ht.lap("sat");
     DS_TRY(stage_cheb());
+    ht.lap("cheb");
     DS_TRY(stage_tail());
+    ht.lap("tail");
     return 0;
   }
 };
@@ -654,7 +695,12 @@ struct Bwd {
       g.C = w.dG; g.cm = idx1(m.S); g.cn = idx1(1);
       DS_TRY(gemm(g));
     }
-    // --- side: LN / residual / fcmy parameter gradients
+    GateArgs ga;
+    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
+    for (int q = 0; q < 3; ++q) { ga.conv[q] = s.conv[q]; ga.dconv_pad[q] = w.dconv[q]; }
+    ga.dG = w.dG;
+    DS_TRY(op_gate_bwd(ga, st));
+    // --- side: LN / residual / fcmy / GTU parameter gradients (one fork)
     DS_TRY(fork());
     DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {dout, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
                     {w.dres_t, m.first ? gd.res_b : nullptr}}, m.BN, m.C, m.T));
@@ -667,13 +713,6 @@ struct Bwd {
       DS_TRY(sgemm(g));
     }
     DS_TRY(colsum_on(sd, w.dtc, m.BN * m.C, m.T, 1, gd.fcmy_b));
-    // --- main: gates, then per GTU the transposed convolution; side: its weight / bias grads
-    GateArgs ga;
-    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
-    for (int q = 0; q < 3; ++q) { ga.conv[q] = s.conv[q]; ga.dconv_pad[q] = w.dconv[q]; }
-    ga.dG = w.dG;
-    DS_TRY(op_gate_bwd(ga, st));
-    DS_TRY(fork());
     for (int q = 0; q < 3; ++q) {
       const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
       const int64_t C2 = 2 * (int64_t)m.C;
@@ -780,20 +819,6 @@ struct Bwd {
       g.alpha = sc;
       DS_TRY(gemm(g));
     }
-    DS_TRY(fork());
-    if (gd.sat_wq || gd.sat_wk) {  // side: [dW_Q'; dW_K'] = dqk^T Zd, then split
-      Gemm g;
-      g.M = (int)ld; g.N = m.D; g.K = (int)m.BN;
-      g.A = w.dqk; g.am = idx1(1); g.ak = idx1(ld);
-      g.B = s.Zd; g.bk = idx1(m.D); g.bn = idx1(1);
-      g.C = w.dWqk; g.cm = idx1(m.D); g.cn = idx1(1);
-      DS_TRY(sgemm(g));
-      PackRows pk;
-      pk.n = 2; pk.cols = m.D; pk.unpack = 1;
-      pk.src[0] = w.dWqk; pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
-      pk.dst[0] = gd.sat_wq; pk.dst[1] = gd.sat_wk;
-      DS_TRY(op_pack_rows(pk, sd));
-    }
     {
       Gemm g;  // dZd = dqk [W_Q'; W_K']
       g.M = (int)m.BN; g.N = m.D; g.K = (int)ld;
@@ -812,8 +837,21 @@ struct Bwd {
       a.gcontrib = w.gcon_s; a.bcontrib = w.bcon_s;
       DS_TRY(op_ln_bwd(a, st));
     }
-    // --- side: EmbedS gamma / beta / pos-embedding grads, pre_conv bias and weight grads
+    // --- side: SAt projection, EmbedS gamma / beta / pos-embedding, pre_conv bias and weight grads
     DS_TRY(fork());
+    if (gd.sat_wq || gd.sat_wk) {  // side: [dW_Q'; dW_K'] = dqk^T Zd, then split
+      Gemm g;
+      g.M = (int)ld; g.N = m.D; g.K = (int)m.BN;
+      g.A = w.dqk; g.am = idx1(1); g.ak = idx1(ld);
+      g.B = s.Zd; g.bk = idx1(m.D); g.bn = idx1(1);
+      g.C = w.dWqk; g.cm = idx1(m.D); g.cn = idx1(1);
+      DS_TRY(sgemm(g));
+      PackRows pk;
+      pk.n = 2; pk.cols = m.D; pk.unpack = 1;
+      pk.src[0] = w.dWqk; pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
+      pk.dst[0] = gd.sat_wq; pk.dst[1] = gd.sat_wk;
+      DS_TRY(op_pack_rows(pk, sd));
+    }
     DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}, {w.dY, gd.pre_conv_b}}, m.BN, m.D, 1));
     if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sd));
     if (gd.pre_conv_w) {
@@ -849,17 +887,11 @@ struct Bwd {
       a.gcontrib = w.gcon_a; a.bcontrib = nullptr;
       DS_TRY(op_ln_bwd(a, st));
     }
-    // --- side: TAt LN gamma / beta and fc weight grads (dU is read here, so the main
-    // chain joins the side before accumulating into dU below)
-    DS_TRY(fork());
-    DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
-    if (gd.tat_fc) {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
-      Gemm g;
-      g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
-      g.A = w.dU; g.am = idx1(1); g.ak = idx1(N);
-      g.B = s.ctx; g.bk = idx1(m.HV); g.bn = idx1(1);
-      g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
-      DS_TRY(sgemm(g));
+    // dE starts as a copy of dU: the side stream's fc weight grad keeps reading dU while the
+    // main chain accumulates the projection terms into dE (no mid-stage join)
+    {
+      hipError_t e = hipMemcpyAsync(w.dE, w.dU, sizeof(float) * (size_t)(m.BFT * N), hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) { set_last_error(std::string("memcpy: ") + hipGetErrorString(e)); return (int)e; }
     }
     {  // dctx = dU Wfc
       Gemm g;
@@ -873,9 +905,18 @@ struct Bwd {
     DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, st));
     if (d.res_mode == DSTAGNN_RES_BCAST && dres)
       DS_TRY(op_sum_middle(w.dscore, m.B, m.F, (int64_t)m.h * m.T * m.T, dres, 0.f, st));
-    // dE = dU + dqkv [Wq; Wk; Wv] ;  [dWq; dWk; dWv] = dqkv^T E  (side)
+    // --- side: TAt LN gamma / beta, fc and Q|K|V weight grads (one fork)
     DS_TRY(fork());
-    if (gd.tat_wq || gd.tat_wk || gd.tat_wv) {
+    DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
+    if (gd.tat_fc) {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
+      Gemm g;
+      g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
+      g.A = w.dU; g.am = idx1(1); g.ak = idx1(N);
+      g.B = s.ctx; g.bk = idx1(m.HV); g.bn = idx1(1);
+      g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
+      DS_TRY(sgemm(g));
+    }
+    if (gd.tat_wq || gd.tat_wk || gd.tat_wv) {  // [dWq; dWk; dWv] = dqkv^T E
       Gemm g;
       g.M = (int)m.QW; g.N = m.N; g.K = (int)m.BFT;
       g.A = w.dqkv; g.am = idx1(1); g.ak = idx1(m.QW);
@@ -888,13 +929,12 @@ struct Bwd {
       pk.dst[0] = gd.tat_wq; pk.dst[1] = gd.tat_wk; pk.dst[2] = gd.tat_wv;
       DS_TRY(op_pack_rows(pk, sd));
     }
-    DS_TRY(join());  // the fc weight grad has read dU
-    {
+    {  // dE = dU + dqkv [Wq; Wk; Wv]
       Gemm g;
       g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.QW;
       g.A = w.dqkv; g.am = idx1(m.QW); g.ak = idx1(1);
       g.B = s.Wqkv; g.bk = idx1(N); g.bn = idx1(1);
-      g.C = w.dU; g.cm = idx1(N); g.cn = idx1(1);
+      g.C = w.dE; g.cm = idx1(N); g.cn = idx1(1);
       g.beta = 1.f;
       DS_TRY(gemm(g));
     }
@@ -902,30 +942,40 @@ struct Bwd {
     if (m.first) {
       LnBwd a;
       a.R = m.B * m.T; a.L = m.N;
-      a.dy = w.dU; a.dyrow = idx1(N);
+      a.dy = w.dE; a.dyrow = idx1(N);
       a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et; a.g = p.embT_g;
       a.dx = w.du_et; a.dxrow = idx1(N);
       a.gcontrib = w.gcon_e; a.bcontrib = nullptr;
       DS_TRY(op_ln_bwd(a, st));
       DS_TRY(fork());
-      DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dU, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
+      DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dE, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
       if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sd));
       DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
     } else {
-      DS_TRY(op_transpose(w.dU, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
+      DS_TRY(op_transpose(w.dE, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
     }
     return 0;
   }
 
   int run() {
+    static const bool prof = getenv("DSTAGNN_HOST_PROFILE") != nullptr;
+    HostTimer ht(prof, "bwd");
     ks.init(st);
     sd = ks.sd;
+    ht.lap("init");
     DS_TRY(stage_tail());
+    ht.lap("tail");
     DS_TRY(stage_cheb());
+    ht.lap("cheb");
     DS_TRY(stage_sat());
+    ht.lap("sat");
     DS_TRY(stage_preconv());
+    ht.lap("preconv");
     DS_TRY(stage_tat());
-    return join();
+    ht.lap("tat");
+    DS_TRY(join());
+    ht.lap("join");
+    return 0;
   }
 };
 

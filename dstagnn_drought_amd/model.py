@@ -189,11 +189,32 @@ class DSTAGNN_block(nn.Module):
         meta = dict(self.meta)
         meta["train"] = bool(self.training)
         meta["seed"] = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
-        names, params = zip(*self.named_parameters())
-        graph = self.cheb_conv_SAt.graph(self.adj_pa)
-        if not self.sparse_cheb:
-            graph = {"cheb": graph["cheb"], "adj_pa": graph["adj_pa"]}
+        names, params = self._param_list()
+        graph = self._graph()
         return DSTAGNNBlockFunction.apply(meta, names, x.float(), res_att, graph, *params)
+
+    # host-side caches (the launch path is host-bound at these sizes): the parameter list
+    # (Parameter objects survive .to()/.cuda()) and the graph dict (rebuilt when a buffer
+    # is replaced, e.g. by .to())
+    def _param_list(self):
+        c = self.__dict__.get("_plist")
+        if c is None or len(c[1]) != sum(1 for _ in self.parameters()):
+            names, params = zip(*self.named_parameters())
+            c = (tuple(names), tuple(params))
+            self.__dict__["_plist"] = c
+        return c
+
+    def _graph(self):
+        cc = self.cheb_conv_SAt
+        key = (id(cc.cheb_stack), id(self.adj_pa), id(cc.csc_row), bool(self.sparse_cheb))
+        c = self.__dict__.get("_gcache")
+        if c is None or c[0] != key:
+            graph = cc.graph(self.adj_pa)
+            if not self.sparse_cheb:
+                graph = {"cheb": graph["cheb"], "adj_pa": graph["adj_pa"]}
+            c = (key, graph)
+            self.__dict__["_gcache"] = c
+        return c[1]
 
 
 class DSTAGNN_submodule(nn.Module):
