@@ -325,12 +325,6 @@ int cheb_backward(const ChebGradIO& c, float* ws, hipStream_t st) {
   return 0;
 }
 
-int pack_theta(const float* const* theta, int K, int F, int C, float* thcat, hipStream_t st) {
-  PackTheta a;
-  a.K = K; a.F = F; a.C = C; a.unpack = 0; a.cat_out = thcat;
-  for (int k = 0; k < K; ++k) a.src[k] = theta[k];
-  return op_pack_theta(a, st);
-}
 int unpack_theta(const float* thcat, int K, int F, int C, float* const* dtheta, hipStream_t st) {
   PackTheta a;
   a.K = K; a.F = F; a.C = C; a.unpack = 1; a.cat_in = thcat;
@@ -512,33 +506,25 @@ struct Fwd {
     if (on_side) DS_TRY(ks.fork());
     params_forked = on_side;
     hipStream_t q = on_side ? ks.sd : st;
-    {
-      PackRows pk;
-      pk.n = 3; pk.cols = m.N;
-      pk.src[0] = p.tat_wq; pk.src[1] = p.tat_wk; pk.src[2] = p.tat_wv;
-      pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
-      pk.dst[0] = s.Wqkv;
-      DS_TRY(op_pack_rows(pk, q));
+    ParamPrep pp;
+    auto add = [&](int kind, const float* src, float* dst, int64_t n, int p0 = 0, int p1 = 0, int p2 = 0,
+                   int64_t off = 0) {
+      PrepSeg& g = pp.seg[pp.nseg++];
+      g.kind = kind; g.src = src; g.dst = dst; g.n = n; g.p0 = p0; g.p1 = p1; g.p2 = p2; g.dst_off = off;
+    };
+    add(0, p.tat_wq, s.Wqkv, m.HQ * m.N, 0, 0, 0, 0);
+    add(0, p.tat_wk, s.Wqkv, m.HQ * m.N, 0, 0, 0, m.HQ * m.N);
+    add(0, p.tat_wv, s.Wqkv, m.HV * m.N, 0, 0, 0, 2 * m.HQ * m.N);
+    add(0, p.sat_wq, s.Wqk, m.KD * m.D, 0, 0, 0, 0);
+    add(0, p.sat_wk, s.Wqk, m.KD * m.D, 0, 0, 0, m.KD * m.D);
+    add(1, p.pre_conv_w, s.Wp, (int64_t)m.D * m.FT, m.F, m.T);  // Wp[d][f][t] = W[d][t][0][f]
+    for (int k = 0; k < m.K; ++k) add(2, p.theta[k], s.thcat, (int64_t)m.F * m.C, m.C, (int)m.KC, k);
+    for (int g = 0; g < 3; ++g) {
+      const int64_t n = 2 * (int64_t)m.C * m.C * m.ks[g];
+      add(3, p.gtu_w[g], s.Wgf[g], n, m.C, m.ks[g]);
+      add(4, p.gtu_w[g], s.Wgb[g], n, m.C, m.ks[g]);
     }
-    {
-      PackRows pk;
-      pk.n = 2; pk.cols = m.D;
-      pk.src[0] = p.sat_wq; pk.src[1] = p.sat_wk;
-      pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
-      pk.dst[0] = s.Wqk;
-      DS_TRY(op_pack_rows(pk, q));
-    }
-    // Wp[d][f][t] = pre_conv.weight[d][t][0][f]
-    DS_TRY(op_transpose(p.pre_conv_w, s.Wp, m.T, m.F, m.D, m.FT, m.FT, 0.f, q));
-    DS_TRY(pack_theta(p.theta, m.K, m.F, m.C, s.thcat, q));
-    GtuWeights gw;
-    gw.C = m.C;
-    for (int g = 0; g < 3; ++g) { gw.w[g] = p.gtu_w[g]; gw.perm[g] = s.Wgf[g]; }
-    gw.mode = 0;
-    DS_TRY(op_gtu_weights(gw, q));
-    for (int g = 0; g < 3; ++g) gw.perm[g] = s.Wgb[g];
-    gw.mode = 1;
-    DS_TRY(op_gtu_weights(gw, q));
+    DS_TRY(op_param_prep(pp, q));
     return 0;
   }
 
@@ -733,6 +719,7 @@ struct Bwd {
         g.B = s.Wgb[q]; g.bk = idx1(m.C); g.bn = idx1(1);  // flipped (j', o, c)
         g.C = w.dX; g.cm = idx1(m.C); g.cn = idx1(1);
         g.beta = 1.f;
+        if (q == 2) { g.Cout = w.gpre; g.emask = s.X; }  // fused ReLU backward of the cheb output
         DS_TRY(gemm(g));
       }
     }
@@ -740,12 +727,12 @@ struct Bwd {
   }
 
   int stage_cheb() {
-    DS_TRY(op_relu_mask(w.dX, s.X, w.gpre, m.BN * m.CT, st));
+    // gpre = dX * (X > 0) was written by the last transposed-conv GEMM's epilogue
     const int64_t NN = m.NN, KC = m.KC, T = m.T, CT = m.CT, KCT = m.KCT, FT = m.FT;
     const int B = m.B, N = m.N, K = m.K, C = m.C, F = m.F;
     if (m.sparse) {
-      hipError_t e = hipMemsetAsync(w.dW, 0, sizeof(float) * (size_t)B * K * NN, st);
-      if (e != hipSuccess) { set_last_error(std::string("memset: ") + hipGetErrorString(e)); return (int)e; }
+      // dW is written on the support only; the softmax backward reads it only where
+      // T_k != 0 (no memset)
       ChebSp sp = make_sp(B, N, K, C, m.T, &gr);
       sp.P = s.P; sp.xth = s.xth; sp.g = w.gpre; sp.dW = w.dW; sp.dxth = w.dxth;
       DS_TRY(op_cheb_sddmm_bwd(sp, st));

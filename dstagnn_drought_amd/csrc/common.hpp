@@ -220,6 +220,10 @@ struct Gemm {
   float alpha = 1.f, beta = 0.f;
   const float* bias = nullptr; int64_t bias_stride = 1;
   int relu = 0;
+  // optional epilogue extras (same C index maps): write to Cout instead of C, and zero
+  // where emask <= 0 (a fused ReLU backward: d_pre = d_out * (out > 0))
+  const float* emask = nullptr;
+  float* Cout = nullptr;
   int hot = 0;  // 1: launch under the separately named gemm_f32_hot_kernel (profiling tag)
   Gemm() { am = ak = az = bk = bn = bz = cm = cn = cz = idx1(0); }
 };

@@ -49,17 +49,20 @@ struct GemmK {
   const float* bias; int32_t bias_stride;
   int relu;
   float* ws;  // split partials [batch][splitk][M][N]
+  const float* emask;  // optional: zero where emask <= 0 (same maps as C, offset c_off)
+  float* Cout;         // optional: destination instead of C (beta still reads C)
 };
 
 
 __device__ __forceinline__ void epilogue_store(const GemmK& g, int zb, int m, int n, float v) {
-  float* C = g.C + zoff(g.cz, zb);
+  const int64_t zo = zoff(g.cz, zb);
   const int32_t o = koff(g.cm, m) + koff(g.cn, n);
   v *= g.alpha;
-  if (g.beta != 0.f) v += g.beta * C[o];
+  if (g.beta != 0.f) v += g.beta * g.C[zo + o];
   if (g.bias) v += g.bias[n * g.bias_stride];
   if (g.relu) v = fmaxf(v, 0.f);
-  C[o] = v;
+  if (g.emask) v = g.emask[zo + o] > 0.f ? v : 0.f;
+  (g.Cout ? g.Cout : g.C)[zo + o] = v;
 }
 
 struct TileCoord {
@@ -577,6 +580,8 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
     return DSTAGNN_E_SHAPE;
   }
   k.alpha = g.alpha; k.beta = g.beta; k.bias = g.bias; k.bias_stride = (int32_t)g.bias_stride; k.relu = g.relu;
+  k.emask = g.emask ? g.emask + g.c_off : nullptr;
+  k.Cout = g.Cout ? g.Cout + g.c_off : nullptr;
   k.ws = ws;
 
   // optional overrides for tuning sweeps (scripts/gemm_sweep.py)
@@ -599,7 +604,7 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
 
   // split-K when the grid leaves CUs idle and the reduction is long
   int splitk = 1;
-  if (g.K > 0 && blocks < 256 && g.K >= 512 && ws) {
+  if (g.K > 0 && blocks < 128 && g.K >= 512 && ws) {
     int want = (int)std::min<int64_t>(512, cdiv64(512, blocks));
     int maxk = g.K / 128;  // keep >= 128 k per split
     splitk = std::max(1, std::min(want, maxk));

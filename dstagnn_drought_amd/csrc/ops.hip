@@ -437,7 +437,10 @@ __global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
 #pragma unroll 2
     for (int i = g; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
-      c += P[o] * Tk[o] * dW[o];
+      // dW is only defined where some T_k is non-zero (the sparse path writes the
+      // support only, no memset): select, so off-support garbage never propagates
+      const float t = Tk[o];
+      c += P[o] * (t != 0.f ? t * dW[o] : 0.f);
     }
   sm_c[g][cj] = c;
   __syncthreads();
@@ -449,7 +452,8 @@ __global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
 #pragma unroll 2
     for (int i = g; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
-      dz[o] = P[o] * (Tk[o] * dW[o] - c);
+      const float t = Tk[o];
+      dz[o] = P[o] * ((t != 0.f ? t * dW[o] : 0.f) - c);
     }
   }
 }
@@ -537,21 +541,39 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(PackRows a) {
   }
 }
 
-__global__ __launch_bounds__(256) void gtu_weights_kernel(GtuWeights a) {
-  const int C = a.C, C2 = 2 * C;
-  for (int q = 0; q < 3; ++q) {
-    const int ks = 3 + 2 * q;
-    const int n = C2 * C * ks;
-    const float* w = a.w[q];
-    float* o = a.perm[q];
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-      // source w[oc][c][j], i = (oc*C + c)*ks + j
-      const int j = i % ks, r = i / ks, c = r % C, oc = r / C;
-      if (a.mode == 0) o[(oc * ks + j) * C + c] = w[i];
-      else o[((ks - 1 - j) * C2 + oc) * C + c] = w[i];
+// blockIdx.y = segment; grid-stride over the segment's source elements
+__global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
+  const PrepSeg& g = a.seg[blockIdx.y];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.n; i += (int64_t)gridDim.x * 256) {
+    const float v = g.src[i];
+    int64_t o;
+    switch (g.kind) {
+      case 0: o = g.dst_off + i; break;
+      case 1: {  // src (d, t, f) -> dst (d, f, t)
+        const int64_t f = i % g.p0, r = i / g.p0, t = r % g.p1, d = r / g.p1;
+        o = (d * g.p0 + f) * g.p1 + t;
+        break;
+      }
+      case 2: {  // src (f, c) -> dst (f, k*C + c)
+        const int64_t c = i % g.p0, f = i / g.p0;
+        o = f * g.p1 + (int64_t)g.p2 * g.p0 + c;
+        break;
+      }
+      case 3: {  // src (o, c, j) -> dst (o, j, c)
+        const int64_t j = i % g.p1, r = i / g.p1, c = r % g.p0, oc = r / g.p0;
+        o = (oc * g.p1 + j) * g.p0 + c;
+        break;
+      }
+      default: {  // src (o, c, j) -> dst (ks-1-j, o, c)
+        const int64_t j = i % g.p1, r = i / g.p1, c = r % g.p0, oc = r / g.p0;
+        o = ((g.p1 - 1 - j) * 2 * g.p0 + oc) * g.p0 + c;
+        break;
+      }
     }
+    g.dst[o] = v;
   }
 }
+
 
 // =====================================================================================
 // block tail: fcmy dropout, residual, ReLUs and LN over C (one thread per (b,n,t) row)
@@ -825,17 +847,21 @@ int op_gate_fwd(const GateArgs& a, hipStream_t st) {
   DS_CHECK_LAUNCH();
   return 0;
 }
+int op_param_prep(const ParamPrep& a, hipStream_t st) {
+  if (a.nseg <= 0) return 0;
+  if (a.nseg > 24) { set_last_error("param_prep: too many segments"); return DSTAGNN_E_ARG; }
+  int64_t mx = 1;
+  for (int q = 0; q < a.nseg; ++q) mx = std::max<int64_t>(mx, a.seg[q].n);
+  hipLaunchKernelGGL(param_prep_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(mx, 256), 256), (unsigned)a.nseg),
+                     dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
 int op_pack_rows(const PackRows& a, hipStream_t st) {
   if (a.n < 1 || a.n > 8) { set_last_error("pack_rows: 1..8 matrices"); return DSTAGNN_E_ARG; }
   int64_t mx = 1;
   for (int q = 0; q < a.n; ++q) mx = std::max<int64_t>(mx, (int64_t)a.rows[q] * a.cols);
   hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(mx, 256), 1024)), dim3(256), 0, st, a);
-  DS_CHECK_LAUNCH();
-  return 0;
-}
-int op_gtu_weights(const GtuWeights& a, hipStream_t st) {
-  hipLaunchKernelGGL(gtu_weights_kernel, dim3((unsigned)std::max<int64_t>(1, cdiv64(2LL * a.C * a.C * 7, 256))),
-                     dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }

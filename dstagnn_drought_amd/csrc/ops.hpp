@@ -55,15 +55,6 @@ struct ColsumArgs {
   float* part = nullptr; int P = 1; int OL = 1;
 };
 
-// GTU conv weights (2C, C, 1, ks) re-laid for single-level GEMM k maps:
-//   mode 0: perm[o][j][c] = w[o][c][j]            (forward: k = (j, c))
-//   mode 1: perm[j'][o][c] = w[o][c][ks-1-j']     (transposed conv: k = (j', o))
-struct GtuWeights {
-  int C = 0, mode = 0;
-  const float* w[3] = {};
-  float* perm[3] = {};
-};
-
 // Stack up to 8 row-major matrices (rows_i x cols) into one (sum rows_i) x cols matrix
 // (unpack = 1: the inverse, null destinations skipped) — fuses same-input projections.
 struct PackRows {
@@ -71,6 +62,25 @@ struct PackRows {
   int rows[8] = {};
   const float* src[8] = {};   // pack sources / unpack: src[0] = packed
   float* dst[8] = {};         // pack: dst[0] = packed / unpack destinations
+};
+
+// Every per-forward parameter re-layout of the block in ONE launch: a list of segments,
+// each a copy with one of a few index maps (element i of the destination):
+//   0 copy           dst[i] = src[i]                                   (stacked projections)
+//   1 pre_conv       Wp[d][f][t] = W[d][t][0][f]        p0 = F, p1 = T
+//   2 theta          thcat[f][k*C + c] = theta_k[f][c]  p0 = C, p1 = K*C, p2 = k
+//   3 gtu fwd        perm[o][j][c] = w[o][c][j]         p0 = C, p1 = ks
+//   4 gtu bwd        perm[j'][o][c] = w[o][c][ks-1-j']  p0 = C, p1 = ks
+struct PrepSeg {
+  int kind = 0, p0 = 0, p1 = 0, p2 = 0;
+  int64_t n = 0;        // source elements
+  int64_t dst_off = 0;  // kind 0: element offset into dst
+  const float* src = nullptr;
+  float* dst = nullptr;
+};
+struct ParamPrep {
+  int nseg = 0;
+  PrepSeg seg[24];
 };
 
 struct GateArgs {
@@ -142,8 +152,8 @@ int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st);
 int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st);
 int op_cheb_mask_grad(const ChebSm& a, hipStream_t st);
 int op_gate_fwd(const GateArgs& a, hipStream_t st);
-int op_gtu_weights(const GtuWeights& a, hipStream_t st);
 int op_pack_rows(const PackRows& a, hipStream_t st);
+int op_param_prep(const ParamPrep& a, hipStream_t st);
 int op_gate_bwd(const GateArgs& a, hipStream_t st);
 int op_tail_fwd(const TailArgs& a, hipStream_t st);
 int op_tail_bwd(const TailArgs& a, hipStream_t st);
