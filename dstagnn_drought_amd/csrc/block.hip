@@ -116,11 +116,11 @@ constexpr size_t kGemmWs = size_t(8) << 20;   // floats (32 MB) for split-K part
 constexpr size_t kPart = size_t(2) << 20;      // floats (8 MB) for column-sum partials
 
 struct Scratch {
-  float *tc, *gemm_ws, *part;
+  float *gemm_ws, *part;
   // bwd (the *_side workspaces belong to the side stream; gcon_* / bcon_* / dres_t are
   // per-stage so the side stream's reductions never race a later main-chain write)
   float *gemm_ws_side, *part_side, *dWqkv, *dWqk;
-  float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dG, *dconv[3], *dW, *dxth,
+  float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dconv[3], *dW, *dxth,
       *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dE, *dctx, *dqkv, *dscore, *du_et;
 };
 
@@ -128,7 +128,6 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   Scratch s;
   s.gemm_ws = a.take(kGemmWs);
   s.part = a.take(kPart);
-  s.tc = a.take(m.BN * m.CT);
   s.dtc = a.take(m.BN * m.CT);
   s.dX = a.take(m.BN * m.CT);
   s.gpre = a.take(m.BN * m.CT);
@@ -143,7 +142,6 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.bcon_s = a.take(m.BN * m.D);
   s.gcon_a = a.take(m.BFT * m.N);
   s.gcon_e = m.first ? a.take((int64_t)m.B * m.T * m.N) : nullptr;
-  s.dG = a.take(m.BN * m.C * m.S);
   for (int g = 0; g < 3; ++g) s.dconv[g] = a.take(m.BN * 2 * m.C * m.Lp[g]);
   s.dW = a.take((int64_t)m.B * m.K * m.NN);
   s.dxth = a.take(m.BN * m.KCT);
@@ -582,26 +580,14 @@ struct Fwd {
       g.bias = p.gtu_b[q];
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
-    GateArgs ga;
-    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
-    for (int q = 0; q < 3; ++q) ga.conv[q] = s.conv[q];
-    ga.G = s.G;
-    DS_TRY(op_gate_fwd(ga, st));
-    {  // fcmy (:243)
-      Gemm g;
-      g.M = (int)(m.BN * m.C); g.N = m.T; g.K = (int)m.S;
-      g.A = s.G; g.am = idx1(m.S); g.ak = idx1(1);
-      g.B = p.fcmy_w; g.bk = idx1(1); g.bn = idx1(m.S);
-      g.C = w.tc; g.cm = idx1(m.T); g.cn = idx1(1);
-      g.bias = p.fcmy_b;
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
-    }
-    TailArgs t;
+    GtuTailArgs t;  // gates + fcmy + dropout + residual + LN, one workgroup per node
     t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
-    t.X = s.X; t.tc = w.tc; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
+    for (int q = 0; q < 3; ++q) t.conv[q] = s.conv[q];
+    t.fcmy_w = p.fcmy_w; t.fcmy_b = p.fcmy_b;
+    t.X = s.X; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
     if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
-    t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c; t.out = out;
-    return op_tail_fwd(t, st);
+    t.G = s.G; t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c; t.out = out;
+    return op_gtu_tail_fwd(t, st);
   }
 
   int run() {
@@ -665,27 +651,16 @@ struct Bwd {
   int sgemm(const Gemm& g) { return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd); }
 
   int stage_tail() {
-    TailArgs t;
+    GtuTailArgs t;  // LN / residual backward -> dtc -> dG = dtc W -> gates backward, per node
     t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
+    for (int q = 0; q < 3; ++q) { t.conv[q] = s.conv[q]; t.dconv_pad[q] = w.dconv[q]; }
+    t.fcmy_w = p.fcmy_w;
     t.X = s.X; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
     if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
     t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c;
     t.dout = dout; t.gcontrib = w.gcon_t; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
     t.rcontrib = w.bcon_t; t.dres = w.dres_t;
-    DS_TRY(op_tail_bwd(t, st));
-    {
-      Gemm g;  // dG = dtc @ W
-      g.M = (int)(m.BN * m.C); g.N = (int)m.S; g.K = m.T;
-      g.A = w.dtc; g.am = idx1(m.T); g.ak = idx1(1);
-      g.B = p.fcmy_w; g.bk = idx1(m.S); g.bn = idx1(1);
-      g.C = w.dG; g.cm = idx1(m.S); g.cn = idx1(1);
-      DS_TRY(gemm(g));
-    }
-    GateArgs ga;
-    ga.BN = m.BN; ga.C = m.C; ga.T = m.T;
-    for (int q = 0; q < 3; ++q) { ga.conv[q] = s.conv[q]; ga.dconv_pad[q] = w.dconv[q]; }
-    ga.dG = w.dG;
-    DS_TRY(op_gate_bwd(ga, st));
+    DS_TRY(op_gtu_tail_bwd(t, st));
     // --- side: LN / residual / fcmy / GTU parameter gradients (one fork)
     DS_TRY(fork());
     DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {dout, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},

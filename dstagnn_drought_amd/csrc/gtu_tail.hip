@@ -1,0 +1,213 @@
+// gtu_tail.hip — the block's per-node epilogue, fused (gfx950).
+//
+// After the three GTU convolution GEMMs (conv[q] rows (t, o), bias included) everything up
+// to the block output is per node (b, n) and tiny (C*T = 384 values at PEMS08):
+//   gates       G[c, s]  = tanh(P) * sigmoid(Q)          (GTU :190-197, concat over q)
+//   fcmy        tc[c, t] = b[t] + sum_s G[c, s] W[t, s]   (:243, Linear(3T-12 -> T))
+//   dropout, residual, ReLUs, LayerNorm over C            (:244-253)
+// One workgroup per node does all of it from LDS: G is written once (the backward's fcmy
+// weight gradient needs it) and never re-read, tc never leaves the workgroup.  The
+// backward fuses the mirror image: LN / residual backward -> dtc -> dG = dtc W (fcmy) ->
+// the gates' backward into the zero-padded (t', o) rows the transposed-convolution GEMMs
+// read.  Replaces gate_fwd + fcmy GEMM + tail_fwd (3 launches, 2 HBM round trips of G and
+// tc) and tail_bwd + dG GEMM + gate_bwd.
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace {
+
+__device__ __forceinline__ void gate_index(int s, int T, int* gi, int* t) {
+  const int T0 = T - 2, T1 = T - 4;
+  *gi = s < T0 ? 0 : (s < T0 + T1 ? 1 : 2);
+  *t = *gi == 0 ? s : (*gi == 1 ? s - T0 : s - T0 - T1);
+}
+
+__global__ __launch_bounds__(256) void gtu_tail_fwd_kernel(GtuTailArgs a) {
+  extern __shared__ float lds[];
+  const int C = a.C, T = a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
+  float* Gs = lds;           // C*S
+  float* Ws = Gs + C * S;    // T*S
+  float* rl = Ws + T * S;    // CT
+  float* mus = rl + CT;      // T
+  float* rss = mus + T;      // T
+  const int tid = threadIdx.x;
+  for (int e = tid; e < T * S; e += 256) Ws[e] = a.fcmy_w[e];
+  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
+    // gates (G also goes to HBM for the backward's fcmy weight gradient)
+    for (int e = tid; e < C * S; e += 256) {
+      const int c = e / S, s = e - c * S;
+      int gi, t;
+      gate_index(s, T, &gi, &t);
+      const int Tg = T - 2 - 2 * gi;
+      const float* cv = a.conv[gi] + (bn * Tg + t) * C2;
+      const float g = tanhf(cv[c]) * (1.f / (1.f + __expf(-cv[C + c])));
+      Gs[e] = g;
+      a.G[bn * C * S + e] = g;
+    }
+    __syncthreads();
+    // fcmy + dropout + residual + ReLUs; element e = (c, t) of the (C, T) output
+    const int64_t base = bn * CT;
+    for (int e = tid; e < CT; e += 256) {
+      const int c = e / T, t = e - c * T;
+      float tc = a.fcmy_b[t];
+      const float* gr = Gs + c * S;
+      const float* wr = Ws + t * S;
+      for (int s = 0; s < S; ++s) tc = fmaf(gr[s], wr[s], tc);
+      if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+      float tco, xres;
+      if (a.first) {
+        tco = fmaxf(tc, 0.f);
+        xres = a.res_w[c] * a.x[bn * T + t] + a.res_b[c];
+      } else {
+        tco = fmaxf(a.X[base + t * C + c] + tc, 0.f);  // X rows are (t, c)
+        xres = a.x[base + e];
+      }
+      const float r = fmaxf(xres + tco, 0.f);
+      a.tco[base + e] = tco;
+      a.r[base + e] = r;
+      rl[e] = r;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += 256) {
+      float sum = 0.f;
+      for (int c = 0; c < C; ++c) sum += rl[c * T + t];
+      const float mean = sum / C;
+      float var = 0.f;
+      for (int c = 0; c < C; ++c) { const float d = rl[c * T + t] - mean; var += d * d; }
+      const float rs = rsqrtf(var / C + 1e-5f);
+      mus[t] = mean; rss[t] = rs;
+      a.mu[bn * T + t] = mean; a.rs[bn * T + t] = rs;
+    }
+    __syncthreads();
+    for (int e = tid; e < CT; e += 256) {
+      const int c = e / T, t = e - c * T;
+      a.out[base + e] = (rl[e] - mus[t]) * rss[t] * a.ln_g[c] + a.ln_b[c];
+    }
+    __syncthreads();  // LDS reuse by the next node
+  }
+}
+
+__global__ __launch_bounds__(256) void gtu_tail_bwd_kernel(GtuTailArgs a) {
+  extern __shared__ float lds[];
+  const int C = a.C, T = a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
+  float* Ws = lds;            // T*S
+  float* dxh = Ws + T * S;    // CT  (LN dxhat, then dtc)
+  float* xhl = dxh + CT;      // CT
+  float* dGs = xhl + CT;      // C*S
+  float* s1s = dGs + C * S;   // T
+  float* s2s = s1s + T;       // T
+  const int tid = threadIdx.x;
+  for (int e = tid; e < T * S; e += 256) Ws[e] = a.fcmy_w[e];
+  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
+    const int64_t base = bn * CT;
+    const float* mu = a.mu + bn * T;
+    const float* rsv = a.rs + bn * T;
+    // LayerNorm over C backward
+    for (int e = tid; e < CT; e += 256) {
+      const int c = e / T, t = e - c * T;
+      const float dy = a.dout[base + e];
+      const float xh = (a.r[base + e] - mu[t]) * rsv[t];
+      xhl[e] = xh;
+      dxh[e] = dy * a.ln_g[c];
+      a.gcontrib[base + e] = dy * xh;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += 256) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int c = 0; c < C; ++c) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
+      s1s[t] = s1 / C; s2s[t] = s2 / C;
+    }
+    __syncthreads();
+    // ReLUs, residual, dropout: dtc (kept in LDS, dxh reused) and the direct grads
+    for (int e = tid; e < CT; e += 256) {
+      const int c = e / T, t = e - c * T;
+      float dr = rsv[t] * (dxh[e] - s1s[t] - xhl[e] * s2s[t]);
+      dr = a.r[base + e] > 0.f ? dr : 0.f;                 // relu(xres + tco)
+      const float dtco = a.tco[base + e] > 0.f ? dr : 0.f;  // tco = relu(...)
+      float dtc = dtco;
+      if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+      a.dtc[base + e] = dtc;
+      if (a.first) {
+        a.dX[base + t * C + c] = 0.f;
+        a.rcontrib[base + e] = dr * a.x[bn * T + t];
+        a.dres[base + e] = dr;
+        xhl[e] = dr;  // for the residual_conv channel reduction below
+      } else {
+        a.dX[base + t * C + c] = dtco;  // dX rows are (t, c), like X
+        a.dx[base + e] = dr;
+      }
+      dxh[e] = dtc;
+    }
+    __syncthreads();
+    if (a.first) {
+      for (int t = tid; t < T; t += 256) {
+        float sum = 0.f;
+        for (int c = 0; c < C; ++c) sum += a.res_w[c] * xhl[c * T + t];
+        a.dx[bn * T + t] = sum;
+      }
+    }
+    // fcmy backward: dG[c, s] = sum_t dtc[c, t] W[t, s]
+    for (int e = tid; e < C * S; e += 256) {
+      const int c = e / S, s = e - c * S;
+      float g = 0.f;
+      for (int t = 0; t < T; ++t) g = fmaf(dxh[c * T + t], Ws[t * S + s], g);
+      dGs[e] = g;
+    }
+    __syncthreads();
+    // gates backward into the zero-padded (t', o) rows of each GTU
+#pragma unroll
+    for (int gi = 0; gi < 3; ++gi) {
+      const int ks = 3 + 2 * gi;
+      const int Tg = T - ks + 1;
+      const int Lp = T + ks - 1;
+      const int off = gi == 0 ? 0 : (gi == 1 ? T - 2 : 2 * T - 6);
+      const int E = C2 * Lp;
+      float* orow = a.dconv_pad[gi] + bn * E;
+      const float* cv = a.conv[gi] + bn * C2 * Tg;
+      for (int e = tid; e < E; e += 256) {
+        const int tp = e / C2, o = e - tp * C2;
+        const int t = tp - (ks - 1);
+        float v = 0.f;
+        if (t >= 0 && t < Tg) {
+          const int c = o < C ? o : o - C;
+          const float p = cv[t * C2 + c];
+          const float q = cv[t * C2 + C + c];
+          const float dg = dGs[c * S + off + t];
+          const float th = tanhf(p), sg = 1.f / (1.f + __expf(-q));
+          v = o < C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
+        }
+        orow[e] = v;
+      }
+    }
+    __syncthreads();  // LDS reuse by the next node
+  }
+}
+
+size_t fwd_lds(const GtuTailArgs& a) {
+  const int S = 3 * a.T - 12;
+  return sizeof(float) * ((size_t)a.C * S + (size_t)a.T * S + (size_t)a.C * a.T + 2 * (size_t)a.T);
+}
+size_t bwd_lds(const GtuTailArgs& a) {
+  const int S = 3 * a.T - 12;
+  return sizeof(float) * ((size_t)a.T * S + 2 * (size_t)a.C * a.T + (size_t)a.C * S + 2 * (size_t)a.T);
+}
+
+unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 8192); }
+
+}  // namespace
+
+int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
+  const size_t lds = fwd_lds(a);
+  if (lds > 64 * 1024) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  hipLaunchKernelGGL(gtu_tail_fwd_kernel, dim3(node_grid(a.BN)), dim3(256), lds, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
+  const size_t lds = bwd_lds(a);
+  if (lds > 64 * 1024) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  hipLaunchKernelGGL(gtu_tail_bwd_kernel, dim3(node_grid(a.BN)), dim3(256), lds, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}

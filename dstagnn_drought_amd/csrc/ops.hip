@@ -470,64 +470,6 @@ __global__ __launch_bounds__(256) void cheb_mask_grad_kernel(ChebSm a) {
   }
 }
 
-// =====================================================================================
-// GTU gates.  conv_g layout [bn][2C][Tg], Tg = T - ks + 1; Gcat [bn][C][3T-12]
-// =====================================================================================
-// One workgroup per (b,n) row at a time (grid-stride over rows), threads over the row's
-// elements with 32-bit index math (no 64-bit division in the element loop).
-// conv[q] rows are (t, o) (the conv GEMM's row-major output), G rows (c, s).
-__global__ __launch_bounds__(256) void gate_fwd_kernel(GateArgs a) {
-  const int S = 3 * a.T - 12;
-  const int E = a.C * S;
-  const int T0 = a.T - 2, T1 = a.T - 4;
-  const int C2 = 2 * a.C;
-  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
-    float* grow = a.G + bn * E;
-    for (int e = threadIdx.x; e < E; e += 256) {
-      const int c = e / S, s = e - c * S;
-      const int gi = s < T0 ? 0 : (s < T0 + T1 ? 1 : 2);
-      const int t = gi == 0 ? s : (gi == 1 ? s - T0 : s - T0 - T1);
-      const int Tg = a.T - 2 - 2 * gi;
-      const float* cv = a.conv[gi] + bn * C2 * Tg + t * C2;
-      const float p = cv[c];
-      const float q = cv[a.C + c];
-      grow[e] = tanhf(p) * (1.f / (1.f + __expf(-q)));
-    }
-  }
-}
-// dconv_pad[q] rows are (t', o), t' in [0, T+ks-1): the conv gradient at t = t'-(ks-1),
-// zero outside [0, Tg) — the padding the transposed convolution GEMM reads in place.
-__global__ __launch_bounds__(256) void gate_bwd_kernel(GateArgs a) {
-  const int S = 3 * a.T - 12;
-  const int C2 = 2 * a.C;
-  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
-#pragma unroll
-    for (int gi = 0; gi < 3; ++gi) {
-      const int ks = 3 + 2 * gi;
-      const int Tg = a.T - ks + 1;
-      const int Lp = a.T + ks - 1;
-      const int off = gi == 0 ? 0 : (gi == 1 ? a.T - 2 : 2 * a.T - 6);
-      const int E = C2 * Lp;
-      float* orow = a.dconv_pad[gi] + bn * E;
-      const float* cv = a.conv[gi] + bn * C2 * Tg;
-      const float* dgr = a.dG + bn * a.C * S + off;
-      for (int e = threadIdx.x; e < E; e += 256) {
-        const int tp = e / C2, o = e - tp * C2;
-        const int t = tp - (ks - 1);
-        float v = 0.f;
-        if (t >= 0 && t < Tg) {
-          const int c = o < a.C ? o : o - a.C;
-          const float p = cv[t * C2 + c];
-          const float q = cv[t * C2 + a.C + c];
-          const float dg = dgr[c * S + t];
-          const float th = tanhf(p), sg = 1.f / (1.f + __expf(-q));
-          v = o < a.C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
-        }
-        orow[e] = v;
-      }
-    }
-  }
-}
 
 __global__ __launch_bounds__(256) void pack_rows_kernel(PackRows a) {
   int r0 = 0;
@@ -580,103 +522,8 @@ __global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
 // =====================================================================================
 // one workgroup per node (b,n): its C*T elements are contiguous in (B,N,C,T), so every
 // pass is a coalesced sweep; the LN over C (stride T) goes through LDS.
-constexpr int kTailMaxCT = 4096, kTailMaxT = 256;
 
-__global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
-  __shared__ float rl[kTailMaxCT];
-  __shared__ float mus[kTailMaxT], rss[kTailMaxT];
-  const int C = a.C, T = a.T, CT = C * T;
-  const int64_t bn = blockIdx.x;
-  const int64_t base = bn * CT;
-  for (int e = threadIdx.x; e < CT; e += 256) {
-    const int c = e / T, t = e - (e / T) * T;
-    const int64_t o = base + e;
-    float tc = a.tc[o];
-    if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
-    float tco, xres;
-    if (a.first) {
-      tco = fmaxf(tc, 0.f);
-      xres = a.res_w[c] * a.x[bn * T + t] + a.res_b[c];
-    } else {
-      tco = fmaxf(a.X[base + t * C + c] + tc, 0.f);  // X rows are (t, c)
-      xres = a.x[o];
-    }
-    const float r = fmaxf(xres + tco, 0.f);
-    a.tco[o] = tco;
-    a.r[o] = r;
-    rl[e] = r;
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < T; t += 256) {
-    float sum = 0.f;
-    for (int c = 0; c < C; ++c) sum += rl[c * T + t];
-    const float mean = sum / C;
-    float var = 0.f;
-    for (int c = 0; c < C; ++c) { const float d = rl[c * T + t] - mean; var += d * d; }
-    const float rs = rsqrtf(var / C + 1e-5f);
-    mus[t] = mean; rss[t] = rs;
-    a.mu[bn * T + t] = mean; a.rs[bn * T + t] = rs;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < CT; e += 256) {
-    const int c = e / T, t = e - (e / T) * T;
-    a.out[base + e] = (rl[e] - mus[t]) * rss[t] * a.ln_g[c] + a.ln_b[c];
-  }
-}
 
-__global__ __launch_bounds__(256) void tail_bwd_kernel(TailArgs a) {
-  __shared__ float dxh[kTailMaxCT], xhl[kTailMaxCT];
-  __shared__ float s1s[kTailMaxT], s2s[kTailMaxT];
-  const int C = a.C, T = a.T, CT = C * T;
-  const int64_t bn = blockIdx.x;
-  const int64_t base = bn * CT;
-  const float* mu = a.mu + bn * T;
-  const float* rsv = a.rs + bn * T;
-  for (int e = threadIdx.x; e < CT; e += 256) {
-    const int c = e / T, t = e - (e / T) * T;
-    const int64_t o = base + e;
-    const float dy = a.dout[o];
-    const float xh = (a.r[o] - mu[t]) * rsv[t];
-    xhl[e] = xh;
-    dxh[e] = dy * a.ln_g[c];
-    a.gcontrib[o] = dy * xh;
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < T; t += 256) {
-    float s1 = 0.f, s2 = 0.f;
-    for (int c = 0; c < C; ++c) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
-    s1s[t] = s1 / C; s2s[t] = s2 / C;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < CT; e += 256) {
-    const int t = e - (e / T) * T;
-    const int64_t o = base + e;
-    float dr = rsv[t] * (dxh[e] - s1s[t] - xhl[e] * s2s[t]);
-    dr = a.r[o] > 0.f ? dr : 0.f;                    // relu(xres + tco)
-    const float dtco = a.tco[o] > 0.f ? dr : 0.f;      // tco = relu(...)
-    float dtc = dtco;
-    if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)o, a.drop_p);
-    a.dtc[o] = dtc;
-    const int c = e / T;
-    if (a.first) {
-      a.dX[base + t * C + c] = 0.f;
-      a.rcontrib[o] = dr * a.x[bn * T + t];  // d residual_conv.weight contributions
-      a.dres[o] = dr;                         // d residual_conv.bias contributions
-      dxh[e] = dr;                            // reuse LDS for the channel reduction below
-    } else {
-      a.dX[base + t * C + c] = dtco;  // dX rows are (t, c), like X
-      a.dx[o] = dr;
-    }
-  }
-  if (a.first) {
-    __syncthreads();
-    for (int t = threadIdx.x; t < T; t += 256) {
-      float s = 0.f;
-      for (int c = 0; c < C; ++c) s += a.res_w[c] * dxh[c * T + t];
-      a.dx[bn * T + t] = s;
-    }
-  }
-}
 
 // thcat[f][k*C + c] = theta_k[f][c]   (and the inverse for the gradients)
 __global__ __launch_bounds__(256) void pack_theta_kernel(PackTheta a) {
@@ -842,11 +689,6 @@ int op_cheb_mask_grad(const ChebSm& a, hipStream_t st) {
   return 0;
 }
 
-int op_gate_fwd(const GateArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(gate_fwd_kernel, dim3((unsigned)std::min<int64_t>(a.BN, 4096)), dim3(256), 0, st, a);
-  DS_CHECK_LAUNCH();
-  return 0;
-}
 int op_param_prep(const ParamPrep& a, hipStream_t st) {
   if (a.nseg <= 0) return 0;
   if (a.nseg > 24) { set_last_error("param_prep: too many segments"); return DSTAGNN_E_ARG; }
@@ -865,24 +707,7 @@ int op_pack_rows(const PackRows& a, hipStream_t st) {
   DS_CHECK_LAUNCH();
   return 0;
 }
-int op_gate_bwd(const GateArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(gate_bwd_kernel, dim3((unsigned)std::min<int64_t>(a.BN, 4096)), dim3(256), 0, st, a);
-  DS_CHECK_LAUNCH();
-  return 0;
-}
 
-int op_tail_fwd(const TailArgs& a, hipStream_t st) {
-  if (a.C * a.T > kTailMaxCT || a.T > kTailMaxT) { set_last_error("tail: C*T too large"); return DSTAGNN_E_SHAPE; }
-  hipLaunchKernelGGL(tail_fwd_kernel, dim3((unsigned)a.BN), dim3(256), 0, st, a);
-  DS_CHECK_LAUNCH();
-  return 0;
-}
-int op_tail_bwd(const TailArgs& a, hipStream_t st) {
-  if (a.C * a.T > kTailMaxCT || a.T > kTailMaxT) { set_last_error("tail: C*T too large"); return DSTAGNN_E_SHAPE; }
-  hipLaunchKernelGGL(tail_bwd_kernel, dim3((unsigned)a.BN), dim3(256), 0, st, a);
-  DS_CHECK_LAUNCH();
-  return 0;
-}
 
 int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st) {
   hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid1d(n)), dim3(256), 0, st, out, n, seed, which, p);

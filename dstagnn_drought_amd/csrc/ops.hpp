@@ -83,29 +83,31 @@ struct ParamPrep {
   PrepSeg seg[24];
 };
 
-struct GateArgs {
-  int64_t BN = 0; int C = 0, T = 0;
-  const float* conv[3] = {};      // [bn][T-ks+1][2C]
-  float* G = nullptr;             // [bn][C][3T-12]
-  const float* dG = nullptr;
-  float* dconv_pad[3] = {};       // [bn][T+ks-1][2C]
-};
-
-struct TailArgs {
+// fused per-node GTU gates + fcmy + dropout + residual + LayerNorm (gtu_tail.hip)
+struct GtuTailArgs {
   int64_t BN = 0; int C = 0, T = 0; int first = 0;
+  const float* conv[3] = {};      // GTU conv outputs [bn][T-ks+1][2C] (bias included)
+  const float* fcmy_w = nullptr;  // (T, 3T-12)
+  const float* fcmy_b = nullptr;  // (T)
   const float* X = nullptr;       // cheb output (B,N,T,C)
-  const float* tc = nullptr;      // fcmy output (B,N,C,T)
   const float* x = nullptr;       // block input (B,N,F,T)
   const float* res_w = nullptr; const float* res_b = nullptr;
   const float* ln_g = nullptr; const float* ln_b = nullptr;
   float drop_p = 0.f; uint64_t seed = 0;
+  // fwd outputs
+  float* G = nullptr;             // [bn][C][3T-12] (saved for the fcmy weight gradient)
   float* tco = nullptr; float* r = nullptr; float* mu = nullptr; float* rs = nullptr; float* out = nullptr;
   // bwd
   const float* dout = nullptr;
-  float* gcontrib = nullptr;      // dout * xhat
-  float* dtc = nullptr; float* dX = nullptr; float* dx = nullptr;
+  float* gcontrib = nullptr;      // dout * xhat (LN gamma grad contributions)
+  float* dtc = nullptr;           // d fcmy output (B,N,C,T)
+  float* dX = nullptr;            // residual part of d cheb output (B,N,T,C)
+  float* dx = nullptr;            // d block input
   float* rcontrib = nullptr; float* dres = nullptr;  // first block residual_conv grads
+  float* dconv_pad[3] = {};       // [bn][T+ks-1][2C]
 };
+
+
 
 struct PackTheta {
   int K = 0, F = 0, C = 0, unpack = 0;
@@ -151,10 +153,8 @@ int op_relu_mask(const float* g, const float* y, float* out, int64_t n, hipStrea
 int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st);
 int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st);
 int op_cheb_mask_grad(const ChebSm& a, hipStream_t st);
-int op_gate_fwd(const GateArgs& a, hipStream_t st);
 int op_pack_rows(const PackRows& a, hipStream_t st);
+int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st);
+int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st);
 int op_param_prep(const ParamPrep& a, hipStream_t st);
-int op_gate_bwd(const GateArgs& a, hipStream_t st);
-int op_tail_fwd(const TailArgs& a, hipStream_t st);
-int op_tail_bwd(const TailArgs& a, hipStream_t st);
 int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st);
