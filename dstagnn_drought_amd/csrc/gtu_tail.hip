@@ -22,64 +22,114 @@ __device__ __forceinline__ void gate_index(int s, int T, int* gi, int* t) {
   *t = *gi == 0 ? s : (*gi == 1 ? s - T0 : s - T0 - T1);
 }
 
-__global__ __launch_bounds__(256) void gtu_tail_fwd_kernel(GtuTailArgs a) {
+// tanh / sigmoid from one v_exp + one v_rcp each (absolute error ~1e-7, far inside the
+// 1e-4 parity bound) instead of the branchy libm tanhf and an IEEE division
+__device__ __forceinline__ float fast_sigmoid(float x) { return __frcp_rn(1.f + __expf(-x)); }
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
+  return 1.f - 2.f * __frcp_rn(e + 1.f);
+}
+
+// One wave (64 threads) per node: a node's work is a chain of short dependent phases, so
+// what pays is many nodes in flight per CU (up to ~27 single-wave workgroups by LDS), not
+// wide workgroups with block-wide barriers.  Every phase first issues all of a lane's global
+// loads (clamped addresses, chunks of kU elements), then computes and stores: with a global
+// store between two loads the compiler cannot prove they don't alias and would serialise one
+// memory round trip per element.
+constexpr int kNT = 64;
+constexpr int kU = 8;
+
+// KC / KT: compile-time C and T (0 = runtime) so the index divisions fold
+template <int KC, int KT>
+__global__ __launch_bounds__(64) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
-  const int C = a.C, T = a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
+  const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C, CS = C * S;
   float* Gs = lds;           // C*S
-  float* Ws = Gs + C * S;    // T*S
+  float* Ws = Gs + CS;       // T*S
   float* rl = Ws + T * S;    // CT
   float* mus = rl + CT;      // T
   float* rss = mus + T;      // T
   const int tid = threadIdx.x;
-  for (int e = tid; e < T * S; e += 256) Ws[e] = a.fcmy_w[e];
+  for (int e = tid; e < T * S; e += kNT) Ws[e] = a.fcmy_w[e];
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     // gates (G also goes to HBM for the backward's fcmy weight gradient)
-    for (int e = tid; e < C * S; e += 256) {
-      const int c = e / S, s = e - c * S;
-      int gi, t;
-      gate_index(s, T, &gi, &t);
-      const int Tg = T - 2 - 2 * gi;
-      const float* cv = a.conv[gi] + (bn * Tg + t) * C2;
-      const float g = tanhf(cv[c]) * (1.f / (1.f + __expf(-cv[C + c])));
-      Gs[e] = g;
-      a.G[bn * C * S + e] = g;
+    for (int e0 = 0; e0 < CS; e0 += kNT * kU) {
+      float pv[kU], qv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = min(e0 + tid + kNT * u, CS - 1);
+        const int c = e / S, s = e - c * S;
+        int gi, t;
+        gate_index(s, T, &gi, &t);
+        const int Tg = T - 2 - 2 * gi;
+        const float* cv = a.conv[gi] + (bn * Tg + t) * C2;
+        pv[u] = cv[c];
+        qv[u] = cv[C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + tid + kNT * u;
+        if (e < CS) {
+          const float g = fast_tanh(pv[u]) * fast_sigmoid(qv[u]);
+          Gs[e] = g;
+          a.G[bn * CS + e] = g;
+        }
+      }
     }
     __syncthreads();
     // fcmy + dropout + residual + ReLUs; element e = (c, t) of the (C, T) output
     const int64_t base = bn * CT;
-    for (int e = tid; e < CT; e += 256) {
-      const int c = e / T, t = e - c * T;
-      float tc = a.fcmy_b[t];
-      const float* gr = Gs + c * S;
-      const float* wr = Ws + t * S;
-      for (int s = 0; s < S; ++s) tc = fmaf(gr[s], wr[s], tc);
-      if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
-      float tco, xres;
-      if (a.first) {
-        tco = fmaxf(tc, 0.f);
-        xres = a.res_w[c] * a.x[bn * T + t] + a.res_b[c];
-      } else {
-        tco = fmaxf(a.X[base + t * C + c] + tc, 0.f);  // X rows are (t, c)
-        xres = a.x[base + e];
+    for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
+      float xv[kU], Xv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = min(e0 + tid + kNT * u, CT - 1);
+        const int c = e / T, t = e - c * T;
+        if (a.first) {
+          xv[u] = a.x[bn * T + t];
+          Xv[u] = 0.f;
+        } else {
+          xv[u] = a.x[base + e];
+          Xv[u] = a.X[base + t * C + c];  // X rows are (t, c)
+        }
       }
-      const float r = fmaxf(xres + tco, 0.f);
-      a.tco[base + e] = tco;
-      a.r[base + e] = r;
-      rl[e] = r;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + tid + kNT * u;
+        if (e >= CT) continue;
+        const int c = e / T, t = e - c * T;
+        float tc = a.fcmy_b[t];
+        const float* gr = Gs + c * S;
+        const float* wr = Ws + t * S;
+        for (int s = 0; s < S; ++s) tc = fmaf(gr[s], wr[s], tc);
+        if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+        float tco, xres;
+        if (a.first) {
+          tco = fmaxf(tc, 0.f);
+          xres = a.res_w[c] * xv[u] + a.res_b[c];
+        } else {
+          tco = fmaxf(Xv[u] + tc, 0.f);
+          xres = xv[u];
+        }
+        const float r = fmaxf(xres + tco, 0.f);
+        a.tco[base + e] = tco;
+        a.r[base + e] = r;
+        rl[e] = r;
+      }
     }
     __syncthreads();
-    for (int t = tid; t < T; t += 256) {
+    for (int t = tid; t < T; t += kNT) {
       float sum = 0.f;
       for (int c = 0; c < C; ++c) sum += rl[c * T + t];
-      const float mean = sum / C;
+      const float mean = sum * (1.f / C);
       float var = 0.f;
       for (int c = 0; c < C; ++c) { const float d = rl[c * T + t] - mean; var += d * d; }
-      const float rs = rsqrtf(var / C + 1e-5f);
+      const float rs = rsqrtf(var * (1.f / C) + 1e-5f);
       mus[t] = mean; rss[t] = rs;
       a.mu[bn * T + t] = mean; a.rs[bn * T + t] = rs;
     }
     __syncthreads();
-    for (int e = tid; e < CT; e += 256) {
+    for (int e = tid; e < CT; e += kNT) {
       const int c = e / T, t = e - c * T;
       a.out[base + e] = (rl[e] - mus[t]) * rss[t] * a.ln_g[c] + a.ln_b[c];
     }
@@ -87,67 +137,98 @@ __global__ __launch_bounds__(256) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void gtu_tail_bwd_kernel(GtuTailArgs a) {
+template <int KC, int KT>
+__global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
-  const int C = a.C, T = a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
+  const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
   float* Ws = lds;            // T*S
   float* dxh = Ws + T * S;    // CT  (LN dxhat, then dtc)
   float* xhl = dxh + CT;      // CT
-  float* dGs = xhl + CT;      // C*S
+  float* rr = xhl + CT;       // CT  (r, kept for the ReLU masks)
+  float* dGs = rr + CT;       // C*S
   float* s1s = dGs + C * S;   // T
   float* s2s = s1s + T;       // T
   const int tid = threadIdx.x;
-  for (int e = tid; e < T * S; e += 256) Ws[e] = a.fcmy_w[e];
+  for (int e = tid; e < T * S; e += kNT) Ws[e] = a.fcmy_w[e];
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     const int64_t base = bn * CT;
     const float* mu = a.mu + bn * T;
     const float* rsv = a.rs + bn * T;
     // LayerNorm over C backward
-    for (int e = tid; e < CT; e += 256) {
-      const int c = e / T, t = e - c * T;
-      const float dy = a.dout[base + e];
-      const float xh = (a.r[base + e] - mu[t]) * rsv[t];
-      xhl[e] = xh;
-      dxh[e] = dy * a.ln_g[c];
-      a.gcontrib[base + e] = dy * xh;
+    for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
+      float dyv[kU], rv[kU], muv[kU], rsw[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = min(e0 + tid + kNT * u, CT - 1);
+        const int t = e % T;
+        dyv[u] = a.dout[base + e];
+        rv[u] = a.r[base + e];
+        muv[u] = mu[t];
+        rsw[u] = rsv[t];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + tid + kNT * u;
+        if (e >= CT) continue;
+        const int c = e / T;
+        const float xh = (rv[u] - muv[u]) * rsw[u];
+        xhl[e] = xh;
+        rr[e] = rv[u];
+        dxh[e] = dyv[u] * a.ln_g[c];
+        a.gcontrib[base + e] = dyv[u] * xh;
+      }
     }
     __syncthreads();
-    for (int t = tid; t < T; t += 256) {
+    for (int t = tid; t < T; t += kNT) {
       float s1 = 0.f, s2 = 0.f;
       for (int c = 0; c < C; ++c) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
-      s1s[t] = s1 / C; s2s[t] = s2 / C;
+      s1s[t] = s1 * (1.f / C); s2s[t] = s2 * (1.f / C);
     }
     __syncthreads();
     // ReLUs, residual, dropout: dtc (kept in LDS, dxh reused) and the direct grads
-    for (int e = tid; e < CT; e += 256) {
-      const int c = e / T, t = e - c * T;
-      float dr = rsv[t] * (dxh[e] - s1s[t] - xhl[e] * s2s[t]);
-      dr = a.r[base + e] > 0.f ? dr : 0.f;                 // relu(xres + tco)
-      const float dtco = a.tco[base + e] > 0.f ? dr : 0.f;  // tco = relu(...)
-      float dtc = dtco;
-      if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
-      a.dtc[base + e] = dtc;
-      if (a.first) {
-        a.dX[base + t * C + c] = 0.f;
-        a.rcontrib[base + e] = dr * a.x[bn * T + t];
-        a.dres[base + e] = dr;
-        xhl[e] = dr;  // for the residual_conv channel reduction below
-      } else {
-        a.dX[base + t * C + c] = dtco;  // dX rows are (t, c), like X
-        a.dx[base + e] = dr;
+    for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
+      float tcov[kU], xv[kU], rsw[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = min(e0 + tid + kNT * u, CT - 1);
+        const int t = e % T;
+        tcov[u] = a.tco[base + e];
+        xv[u] = a.first ? a.x[bn * T + t] : 0.f;
+        rsw[u] = rsv[t];
       }
-      dxh[e] = dtc;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + tid + kNT * u;
+        if (e >= CT) continue;
+        const int c = e / T, t = e - c * T;
+        float dr = rsw[u] * (dxh[e] - s1s[t] - xhl[e] * s2s[t]);
+        dr = rr[e] > 0.f ? dr : 0.f;                 // relu(xres + tco)
+        const float dtco = tcov[u] > 0.f ? dr : 0.f;  // tco = relu(...)
+        float dtc = dtco;
+        if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+        a.dtc[base + e] = dtc;
+        if (a.first) {
+          a.dX[base + t * C + c] = 0.f;
+          a.rcontrib[base + e] = dr * xv[u];
+          a.dres[base + e] = dr;
+          xhl[e] = dr;  // for the residual_conv channel reduction below
+        } else {
+          a.dX[base + t * C + c] = dtco;  // dX rows are (t, c), like X
+          a.dx[base + e] = dr;
+        }
+        dxh[e] = dtc;
+      }
     }
     __syncthreads();
     if (a.first) {
-      for (int t = tid; t < T; t += 256) {
+      for (int t = tid; t < T; t += kNT) {
         float sum = 0.f;
         for (int c = 0; c < C; ++c) sum += a.res_w[c] * xhl[c * T + t];
         a.dx[bn * T + t] = sum;
       }
     }
     // fcmy backward: dG[c, s] = sum_t dtc[c, t] W[t, s]
-    for (int e = tid; e < C * S; e += 256) {
+    for (int e = tid; e < C * S; e += kNT) {
       const int c = e / S, s = e - c * S;
       float g = 0.f;
       for (int t = 0; t < T; ++t) g = fmaf(dxh[c * T + t], Ws[t * S + s], g);
@@ -164,19 +245,32 @@ __global__ __launch_bounds__(256) void gtu_tail_bwd_kernel(GtuTailArgs a) {
       const int E = C2 * Lp;
       float* orow = a.dconv_pad[gi] + bn * E;
       const float* cv = a.conv[gi] + bn * C2 * Tg;
-      for (int e = tid; e < E; e += 256) {
-        const int tp = e / C2, o = e - tp * C2;
-        const int t = tp - (ks - 1);
-        float v = 0.f;
-        if (t >= 0 && t < Tg) {
+      for (int e0 = 0; e0 < E; e0 += kNT * kU) {
+        float pv[kU], qv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int e = min(e0 + tid + kNT * u, E - 1);
+          const int tp = e / C2, o = e - tp * C2;
+          const int t = min(max(tp - (ks - 1), 0), Tg - 1);
           const int c = o < C ? o : o - C;
-          const float p = cv[t * C2 + c];
-          const float q = cv[t * C2 + C + c];
-          const float dg = dGs[c * S + off + t];
-          const float th = tanhf(p), sg = 1.f / (1.f + __expf(-q));
-          v = o < C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
+          pv[u] = cv[t * C2 + c];
+          qv[u] = cv[t * C2 + C + c];
         }
-        orow[e] = v;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int e = e0 + tid + kNT * u;
+          if (e >= E) continue;
+          const int tp = e / C2, o = e - tp * C2;
+          const int t = tp - (ks - 1);
+          float v = 0.f;
+          if (t >= 0 && t < Tg) {
+            const int c = o < C ? o : o - C;
+            const float dg = dGs[c * S + off + t];
+            const float th = fast_tanh(pv[u]), sg = fast_sigmoid(qv[u]);
+            v = o < C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
+          }
+          orow[e] = v;
+        }
       }
     }
     __syncthreads();  // LDS reuse by the next node
@@ -189,17 +283,20 @@ size_t fwd_lds(const GtuTailArgs& a) {
 }
 size_t bwd_lds(const GtuTailArgs& a) {
   const int S = 3 * a.T - 12;
-  return sizeof(float) * ((size_t)a.T * S + 2 * (size_t)a.C * a.T + (size_t)a.C * S + 2 * (size_t)a.T);
+  return sizeof(float) * ((size_t)a.T * S + 3 * (size_t)a.C * a.T + (size_t)a.C * S + 2 * (size_t)a.T);
 }
 
-unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 8192); }
+unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 65536); }
 
 }  // namespace
 
 int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
   const size_t lds = fwd_lds(a);
   if (lds > 64 * 1024) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-  hipLaunchKernelGGL(gtu_tail_fwd_kernel, dim3(node_grid(a.BN)), dim3(256), lds, st, a);
+  if (a.C == 32 && a.T == 12)
+    hipLaunchKernelGGL((gtu_tail_fwd_kernel<32, 12>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
+  else
+    hipLaunchKernelGGL((gtu_tail_fwd_kernel<0, 0>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -207,7 +304,10 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
 int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
   const size_t lds = bwd_lds(a);
   if (lds > 64 * 1024) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-  hipLaunchKernelGGL(gtu_tail_bwd_kernel, dim3(node_grid(a.BN)), dim3(256), lds, st, a);
+  if (a.C == 32 && a.T == 12)
+    hipLaunchKernelGGL((gtu_tail_bwd_kernel<32, 12>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
+  else
+    hipLaunchKernelGGL((gtu_tail_bwd_kernel<0, 0>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
