@@ -39,18 +39,22 @@ __device__ __forceinline__ float fast_tanh(float x) {
 constexpr int kNT = 64;
 constexpr int kU = 8;
 
-// KC / KT: compile-time C and T (0 = runtime) so the index divisions fold
-template <int KC, int KT>
+// KC / KT: compile-time C and T (0 = runtime) so the index divisions fold.  WL: the fcmy
+// weight (T x 3T-12) staged in LDS; false for long series (GAMBIA T=144: 242 KB), where
+// it is read through L1/L2 instead.
+template <int KC, int KT, bool WL>
 __global__ __launch_bounds__(64) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C, CS = C * S;
-  float* Gs = lds;           // C*S
-  float* Ws = Gs + CS;       // T*S
-  float* rl = Ws + T * S;    // CT
-  float* mus = rl + CT;      // T
-  float* rss = mus + T;      // T
+  float* Gs = lds;                       // C*S
+  float* rl = Gs + CS;                   // CT
+  float* mus = rl + CT;                  // T
+  float* rss = mus + T;                  // T
+  float* Wl = rss + T;                   // T*S (WL only)
+  const float* Ws = WL ? Wl : a.fcmy_w;
   const int tid = threadIdx.x;
-  for (int e = tid; e < T * S; e += kNT) Ws[e] = a.fcmy_w[e];
+  if (WL)
+    for (int e = tid; e < T * S; e += kNT) Wl[e] = a.fcmy_w[e];
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     // gates (G also goes to HBM for the backward's fcmy weight gradient)
     for (int e0 = 0; e0 < CS; e0 += kNT * kU) {
@@ -137,19 +141,21 @@ __global__ __launch_bounds__(64) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   }
 }
 
-template <int KC, int KT>
+template <int KC, int KT, bool WL>
 __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
-  float* Ws = lds;            // T*S
-  float* dxh = Ws + T * S;    // CT  (LN dxhat, then dtc)
+  float* dxh = lds;           // CT  (LN dxhat, then dtc)
   float* xhl = dxh + CT;      // CT
   float* rr = xhl + CT;       // CT  (r, kept for the ReLU masks)
   float* dGs = rr + CT;       // C*S
   float* s1s = dGs + C * S;   // T
   float* s2s = s1s + T;       // T
+  float* Wl = s2s + T;        // T*S (WL only)
+  const float* Ws = WL ? Wl : a.fcmy_w;
   const int tid = threadIdx.x;
-  for (int e = tid; e < T * S; e += kNT) Ws[e] = a.fcmy_w[e];
+  if (WL)
+    for (int e = tid; e < T * S; e += kNT) Wl[e] = a.fcmy_w[e];
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     const int64_t base = bn * CT;
     const float* mu = a.mu + bn * T;
@@ -277,37 +283,46 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   }
 }
 
-size_t fwd_lds(const GtuTailArgs& a) {
-  const int S = 3 * a.T - 12;
-  return sizeof(float) * ((size_t)a.C * S + (size_t)a.T * S + (size_t)a.C * a.T + 2 * (size_t)a.T);
+size_t fwd_lds(const GtuTailArgs& a, bool wl) {
+  const size_t S = 3 * (size_t)a.T - 12;
+  return sizeof(float) * ((size_t)a.C * S + (size_t)a.C * a.T + 2 * (size_t)a.T + (wl ? (size_t)a.T * S : 0));
 }
-size_t bwd_lds(const GtuTailArgs& a) {
-  const int S = 3 * a.T - 12;
-  return sizeof(float) * ((size_t)a.T * S + 3 * (size_t)a.C * a.T + (size_t)a.C * S + 2 * (size_t)a.T);
+size_t bwd_lds(const GtuTailArgs& a, bool wl) {
+  const size_t S = 3 * (size_t)a.T - 12;
+  return sizeof(float) * (3 * (size_t)a.C * a.T + (size_t)a.C * S + 2 * (size_t)a.T + (wl ? (size_t)a.T * S : 0));
 }
 
 unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 65536); }
 
-}  // namespace
+constexpr size_t kLdsMax = 160 * 1024;  // gfx950 LDS per workgroup
 
-int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
-  const size_t lds = fwd_lds(a);
-  if (lds > 64 * 1024) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-  if (a.C == 32 && a.T == 12)
-    hipLaunchKernelGGL((gtu_tail_fwd_kernel<32, 12>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
-  else
-    hipLaunchKernelGGL((gtu_tail_fwd_kernel<0, 0>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
+template <typename K>
+int launch_node_kernel(K kernel, size_t lds, const GtuTailArgs& a, hipStream_t st) {
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) { set_last_error(std::string("gtu_tail LDS: ") + hipGetErrorString(e)); return (int)e; }
+  }
+  hipLaunchKernelGGL(kernel, dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 
+}  // namespace
+
+int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
+  const bool wl = fwd_lds(a, true) <= 32 * 1024;
+  const size_t lds = fwd_lds(a, wl);
+  if (lds > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  if (a.C == 32 && a.T == 12 && wl) return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true>, lds, a, st);
+  if (wl) return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, true>, lds, a, st);
+  return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false>, lds, a, st);
+}
+
 int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
-  const size_t lds = bwd_lds(a);
-  if (lds > 64 * 1024) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-  if (a.C == 32 && a.T == 12)
-    hipLaunchKernelGGL((gtu_tail_bwd_kernel<32, 12>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
-  else
-    hipLaunchKernelGGL((gtu_tail_bwd_kernel<0, 0>), dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
-  DS_CHECK_LAUNCH();
-  return 0;
+  const bool wl = bwd_lds(a, true) <= 32 * 1024;
+  const size_t lds = bwd_lds(a, wl);
+  if (lds > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  if (a.C == 32 && a.T == 12 && wl) return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
+  if (wl) return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, true>, lds, a, st);
+  return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false>, lds, a, st);
 }

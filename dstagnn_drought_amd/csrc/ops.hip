@@ -190,6 +190,76 @@ __global__ __launch_bounds__(256) void tat_bwd_kernel(TatArgs a) {
   }
 }
 
+// Long-series variant (GAMBIA T=144: A and dA together exceed the 160 KB of LDS): only A
+// stays resident.  dV first (needs A), then per column j one thread forms
+// c_j = sum_i A_ij dA_ij and overwrites column j of A with dS (dA recomputed from
+// dctx . V, dv FMAs per element), then dQ / dK from dS.
+__global__ __launch_bounds__(256) void tat_bwd_lowmem_kernel(TatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int T = a.T, dk = a.dk, dv = a.dv;
+  const int dkp = dk + 1, dvp = dv + 1;
+  float* Qs = sm;
+  float* Ks = Qs + T * dkp;
+  float* Vs = Ks + T * dkp;
+  float* dCs = Vs + T * dvp;    // T*dvp
+  float* As = dCs + T * dvp;    // T*T  (A, then dS column by column)
+  const int id = blockIdx.x;
+  const int hd = id % a.h;
+  const int bf = id / a.h;
+  const int ld = 2 * a.h * dk + a.h * dv;
+  const int ldc = a.h * dv;
+  const float* base = a.qkv + (int64_t)bf * T * ld;
+  const float* cb = a.dctx + (int64_t)bf * T * ldc;
+  const int64_t sbase = (int64_t)id * T * T;
+  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+    int i = e / dk, d = e % dk;
+    Qs[i * dkp + d] = base[(int64_t)i * ld + hd * dk + d];
+    Ks[i * dkp + d] = base[(int64_t)i * ld + a.h * dk + hd * dk + d];
+  }
+  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {
+    int i = e / dv, d = e % dv;
+    Vs[i * dvp + d] = base[(int64_t)i * ld + 2 * a.h * dk + hd * dv + d];
+    dCs[i * dvp + d] = cb[(int64_t)i * ldc + hd * dv + d];
+  }
+  for (int e = threadIdx.x; e < T * T; e += blockDim.x) As[e] = a.att[sbase + e];
+  __syncthreads();
+  float* dbase = a.dqkv + (int64_t)bf * T * ld;
+  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {  // dV[j][d] = sum_i A[i][j] dctx[i][d]
+    int j = e / dv, d = e % dv;
+    float s = 0.f;
+    for (int i = 0; i < T; ++i) s = fmaf(As[i * T + j], dCs[i * dvp + d], s);
+    dbase[(int64_t)j * ld + 2 * a.h * dk + hd * dv + d] = s;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < T; j += blockDim.x) {
+    float c = 0.f;
+    for (int i = 0; i < T; ++i) {
+      float da = 0.f;
+      for (int d = 0; d < dv; ++d) da = fmaf(dCs[i * dvp + d], Vs[j * dvp + d], da);
+      c = fmaf(As[i * T + j], da, c);
+    }
+    for (int i = 0; i < T; ++i) {
+      float da = 0.f;
+      for (int d = 0; d < dv; ++d) da = fmaf(dCs[i * dvp + d], Vs[j * dvp + d], da);
+      float v = As[i * T + j] * (da - c);
+      if (a.dre) v += a.dre[sbase + i * T + j];
+      As[i * T + j] = v;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * T; e += blockDim.x) a.dscore[sbase + e] = As[e];
+  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+    int i = e / dk, d = e % dk;
+    float sq = 0.f, sk = 0.f;
+    for (int j = 0; j < T; ++j) {
+      sq = fmaf(As[i * T + j], Ks[j * dkp + d], sq);
+      sk = fmaf(As[j * T + i], Qs[j * dkp + d], sk);
+    }
+    dbase[(int64_t)i * ld + hd * dk + d] = sq * a.scale;
+    dbase[(int64_t)i * ld + a.h * dk + hd * dk + d] = sk * a.scale;
+  }
+}
+
 // =====================================================================================
 // LayerNorm over rows of length L; one wave per row, values kept in registers.
 // =====================================================================================
@@ -562,11 +632,21 @@ int op_transpose(const float* in, float* out, int R, int Cc, int batch, int64_t 
   return 0;
 }
 
+// dynamic LDS above 64 KB must be opted into per kernel (gfx950 has 160 KB per workgroup)
+static int allow_lds(const void* kernel, size_t bytes) {
+  hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) { set_last_error(std::string("LDS attribute: ") + hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
 static size_t tat_fwd_lds(int T, int dk, int dv) {
   return sizeof(float) * (size_t)(2 * T * (dk + 1) + T * (dv + 1) + T * T);
 }
 static size_t tat_bwd_lds(int T, int dk, int dv) {
   return sizeof(float) * (size_t)(2 * T * (dk + 1) + 2 * T * (dv + 1) + 2 * T * T);
+}
+static size_t tat_bwd_lowmem_lds(int T, int dk, int dv) {
+  return sizeof(float) * (size_t)(2 * T * (dk + 1) + 2 * T * (dv + 1) + T * T);
 }
 
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
@@ -577,6 +657,7 @@ int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
   a.re_at = re_at; a.att = att; a.ctx = ctx;
   size_t lds = tat_fwd_lds(T, dk, dv);
   if (lds > 160 * 1024) { set_last_error("tat_fwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  if (lds > 64 * 1024) DS_TRY(allow_lds((const void*)tat_fwd_kernel, lds));
   hipLaunchKernelGGL(tat_fwd_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
@@ -589,7 +670,15 @@ int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
   a.qkv = qkv; a.att = const_cast<float*>(att); a.scale = 1.f / sqrtf((float)dk);
   a.dctx = dctx; a.dre = dre; a.dqkv = dqkv; a.dscore = dscore;
   size_t lds = tat_bwd_lds(T, dk, dv);
-  if (lds > 160 * 1024) { set_last_error("tat_bwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
+  if (lds > 160 * 1024) {  // long series: A-only LDS variant
+    lds = tat_bwd_lowmem_lds(T, dk, dv);
+    if (lds > 160 * 1024) { set_last_error("tat_bwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
+    DS_TRY(allow_lds((const void*)tat_bwd_lowmem_kernel, lds));
+    hipLaunchKernelGGL(tat_bwd_lowmem_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
+  if (lds > 64 * 1024) DS_TRY(allow_lds((const void*)tat_bwd_kernel, lds));
   hipLaunchKernelGGL(tat_bwd_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
