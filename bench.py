@@ -60,6 +60,66 @@ def build_block(device):
     return blk.to(device).train(), cheb, torch.FloatTensor(pa)
 
 
+def time_loop(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def extras(dev, steps, warmup):
+    """also the first block (F=1, res_att 0) and the full make_model train
+    step (nb_block=4 as configurations/PEMS08_dstagnn.conf, SmoothL1 + Adam lr 1e-4)."""
+    import dstagnn_drought_amd as D
+    c = CFG
+    B, N, T, K, h, Dm, dk, C = c["B"], c["N"], c["T"], c["K"], c["n_heads"], c["d_model"], c["d_k"], c["C"]
+    tmd, pa = synth_graph(N)
+    Lt = D.scaled_Laplacian(torch.FloatTensor(tmd))
+    cheb = [torch.from_numpy(p).float() for p in D.cheb_polynomial(Lt.numpy(), K)]
+    torch.manual_seed(1)
+    blk = D.DSTAGNN_block("cpu", 1, 1, K, C, C, 1, cheb, pa, tmd, N, T, Dm, dk, dk, h)
+    for p in blk.parameters():
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+        else:
+            torch.nn.init.uniform_(p)
+    blk = blk.to(dev).train()
+    gen = torch.Generator(device=dev).manual_seed(5)
+    x1 = torch.randn(B, N, 1, T, device=dev, generator=gen)
+    g1 = torch.randn(B, N, C, T, device=dev, generator=gen)
+    g1r = torch.randn(B, 1, h, T, T, device=dev, generator=gen)
+    prm = list(blk.parameters())
+
+    def first_step():
+        for p in prm:
+            p.grad = None
+        o, r = blk(x1, 0)
+        torch.autograd.backward([o, r], [g1, g1r])
+    t_first = time_loop(first_step, steps, warmup)
+
+    net = D.make_model(dev, 1, 4, 1, K, C, C, 1, tmd, pa, tmd, T, T, N, Dm, dk, dk, h)
+    net.train()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    crit = torch.nn.SmoothL1Loss().to(dev)
+    xm = torch.randn(B, N, 1, T, device=dev, generator=gen)
+    ym = torch.randn(B, N, T, device=dev, generator=gen)
+
+    def model_step():
+        opt.zero_grad(set_to_none=True)
+        loss = crit(net(xm), ym)
+        loss.backward()
+        opt.step()
+    t_model = time_loop(model_step, steps, warmup)
+    return {"first_block": {"samples_per_s": round(B / t_first, 1), "ms_per_step": round(t_first * 1e3, 4),
+                            "workload": "PEMS08 first DSTAGNN_block (F=1, res_att 0) fwd+bwd, B=32"},
+            "model_step": {"samples_per_s": round(B / t_model, 1), "ms_per_step": round(t_model * 1e3, 4),
+                           "workload": "make_model nb_block=4 PEMS08: fwd + SmoothL1 + bwd + Adam, B=32"}}
+
+
 def algorithmic_flops_per_sample(c=CFG):
     """SURVEY.md §8(d) formula (sparse-T_k count, fwd; fwd+bwd = 3x)."""
     B, N, F, T, h, dk, D, K, C = 1, c["N"], c["C"], c["T"], c["n_heads"], c["d_k"], c["d_model"], c["K"], c["C"]
@@ -127,6 +187,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hot-iters", type=int, default=50)
+    ap.add_argument("--no-extras", action="store_true", help="skip the first-block / full-model lines")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,6 +289,17 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(f"cpu baseline on {host_cores()} threads")
         cpu = cpu_baseline()
+    ext = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        log("extras: first block, full model step")
+        ext = extras(dev, max(5, args.steps // 2), 3)
+    # whole-block roofline: 758.8 MFLOP per sample fwd+bwd, compute-bound
+    # (arithmetic intensity ~460 flop/B vs the fp32 ridge ~20): peak samples/s = 157.3 TF / F_alg
+    f_alg = algorithmic_flops_per_sample()
+    peak_sps = PEAK_FP32_TFLOPS * 1e12 / f_alg
+    block_roof = {"bound": "mfma", "alg_flop_per_sample": round(f_alg / 1e6, 1), "unit_flop": "MFLOP",
+                  "peak_samples_per_s_per_gpu": round(peak_sps, 0),
+                  "frac": round(value / (world * peak_sps), 4)}
 
     if rank == 0:
         line = {
@@ -241,8 +313,11 @@ def main():
                        "parallelism": f"dp{world}"},
             "algorithmic_tflops": round(algorithmic_flops_per_sample() * value / 1e12, 3),
             "roofline": roof,
+            "block_roofline": block_roof,
             "cpu_baseline": cpu,
         }
+        if ext is not None:
+            line["extras"] = ext
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
