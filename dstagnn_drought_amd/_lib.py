@@ -99,6 +99,13 @@ def load():
                                      _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                      P(ctypes.c_float), _vp],
         "dstagnn_dropout_mask": [P(BlockDims), ctypes.c_int, _vp, _vp],
+        "dstagnn_stag_prep": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp],
+        "dstagnn_stag_emd_pairs": [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int64,
+                                   _vp, _vp, _vp, _vp],
+        "dstagnn_emd_dense": [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp],
+        "dstagnn_fast_stag_distances": [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_double, _vp, _vp],
+        "dstagnn_graph_topk": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp],
+        "dstagnn_stag_emd_lds_bytes": [ctypes.c_int, ctypes.c_int],
         "dstagnn_last_error": [],
         "dstagnn_version": [],
     }
@@ -107,6 +114,7 @@ def load():
         fn.argtypes = args
         fn.restype = ctypes.c_int
     lib.dstagnn_last_error.restype = ctypes.c_char_p
+    lib.dstagnn_stag_emd_lds_bytes.restype = ctypes.c_int64
     _lib = lib
     return lib
 

@@ -195,6 +195,48 @@ int dstagnn_block_time_stage(const dstagnn_block_dims* d, const dstagnn_block_pa
  * which = 0 (EmbedS output, (B,N,D)), 1 (fcmy output, (B,N,C,T) order of out). */
 int dstagnn_dropout_mask(const dstagnn_block_dims* d, int which, float* mask, dstagnn_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Graph builders (stag.hip).  fp64 throughout, like the reference's numpy/scipy code.
+ * ------------------------------------------------------------------------------------- */
+
+/* STAG_gen per-node preprocessing (data/STAG_gen.py:47-54 applied once per node instead of
+ * once per pair): data (T,N,F) -> xhat (N,T,F) unit rows (zero rows stay 0), p (N,T)
+ * marginals |x_t| / (sum_t |x_t| + 1e-12) with the 1e-12 zero-norm guard, psum (N) = sum p. */
+int dstagnn_stag_prep(const double* data, int T, int N, int F, double* xhat, double* p, double* psum,
+                      dstagnn_stream_t stream);
+
+/* STAG_gen exact EMD of node pairs (replaces process_node_pair + wasserstein_distance,
+ * data/STAG_gen.py:17-59, which solve the dense LP with scipy linprog/HiGHS).
+ * pairs (P,2) int32 node ids; out (P) the optimal transport cost under
+ * D = clip(1 - xhat_i xhat_j^T, 0, 1), or 1.0 where the reference's LP is infeasible
+ * (marginal totals differ by > 1e-7, e.g. an all-zero node; status 1).  status (P): 0 ok,
+ * 1 infeasible (1.0 returned, as the reference), 2 solver pivot cap (a bug: raise).
+ * pivots (P) optional (may be NULL).  Needs 2T+1 <= 32767 and
+ * dstagnn_stag_emd_lds_bytes(T,F) <= 160 KiB (T <= ~1100 at F = 4). */
+int64_t dstagnn_stag_emd_lds_bytes(int T, int F);
+int dstagnn_stag_emd_pairs(const double* xhat, const double* p, const double* psum, int T, int N, int F,
+                           const int32_t* pairs, int64_t P, double* out, int32_t* status, int64_t* pivots,
+                           dstagnn_stream_t stream);
+
+/* Batched wasserstein_distance(p, q, D) (data/STAG_gen.py:17-38): p, q (B,T), D (B,T,T) dense
+ * costs (nan -> 0, +-inf -> +-1e12 as the reference).  1.0 / status 1 when infeasible
+ * (negative mass or totals differing by > 1e-7). */
+int dstagnn_emd_dense(const double* p, const double* q, const double* D, int T, int64_t B, double* out,
+                      int32_t* status, dstagnn_stream_t stream);
+
+/* fast_STAG_gen.calculate_distances, symmetrised with a zero diagonal
+ * (data/fast_STAG_gen.py:16-35, 57-59): coords (N,Dc), feats (N,Fp) -> sta (N,N). */
+int dstagnn_fast_stag_distances(const double* coords, int N, int Dc, const double* feats, int Fp, double max_distance,
+                                double* sta, dstagnn_stream_t stream);
+
+/* Per-row top-k adjacency.  mode 0 = fast_STAG_gen (:66-74): the k smallest sta[i,:],
+ * A = 1, R = 1 - sta.  mode 1 = STAG_gen (:105-116): adj = 1 - sta + I, the k smallest
+ * adj[i,:], A = 1, R = adj.  Ties go to the lower column index (np.argsort kind='stable';
+ * the reference's default quicksort leaves tie order unspecified).  A, R (N,N) are fully
+ * written; nbr (N,k) optional, ascending by (key, index).  N <= 8192. */
+int dstagnn_graph_topk(const double* sta, int N, int k, int mode, double* A, double* R, int32_t* nbr,
+                       dstagnn_stream_t stream);
+
 const char* dstagnn_last_error(void);
 int dstagnn_version(void);
 

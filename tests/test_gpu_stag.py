@@ -1,0 +1,204 @@
+"""GPU parity of the graph builders (stag.hip through the C-ABI) against the reference's golden
+vectors and the CPU oracle (oracle/stag_ref.py: scipy linprog/HiGHS, numpy).
+
+Tolerances (fp64 throughout, as the reference):
+  EMD values      |gpu - ref| <= 1e-9   (HiGHS' own optimum is exact to ~1e-12 here; the
+                                         probes in tests/test_emd_solver_cpu.py agree to 1e-13)
+  sta distances   |gpu - ref| <= 1e-13  (a different fp64 summation order of 12 products)
+  top-k sets      exact, except that tied keys (|a - b| <= 1e-12) may be exchanged: the
+                  reference's quicksort leaves tie order unspecified; ours is lowest index.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import stag_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def load(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name), allow_pickle=False))
+
+
+# ---------------------------------------------------------------------------------------
+# STAG_gen
+# ---------------------------------------------------------------------------------------
+def test_emd_pairs_golden(dev, golden_dir):
+    from dstagnn_drought_amd import stag_gen as sg
+    g = load(golden_dir, "g7_stag_pairs.npz")
+    for T in (12, 48):
+        data, pairs, emd = g[f"data_T{T}"], g[f"pairs_T{T}"], g[f"emd_T{T}"]
+        nd = sg.NodeData(data, dev)
+        out, st = nd.emd_pairs(pairs)
+        out, st = out.cpu().numpy(), st.cpu().numpy()
+        assert set(np.unique(st)) <= {0, 1}
+        np.testing.assert_allclose(out, emd, rtol=0, atol=1e-9)
+        assert np.all((st == 1) == (emd == 1.0))   # the all-zero node's infeasible LPs
+
+
+def test_sta_matrix_golden(dev, golden_dir):
+    from dstagnn_drought_amd import stag_gen as sg
+    g = load(golden_dir, "g7b_stag_dataset.npz")
+    np.testing.assert_allclose(sg.sta_matrix(g["data"], dev), g["sta"], rtol=0, atol=1e-9)
+
+
+def test_process_node_pair_api(dev, golden_dir):
+    from dstagnn_drought_amd import stag_gen as sg
+    g = load(golden_dir, "g7_stag_pairs.npz")
+    i, j = (int(v) for v in g["pairs_T48"][3])
+    ri, rj, d = sg.process_node_pair((i, j, g["data_T48"]), dev)
+    assert (ri, rj) == (i, j) and abs(d - g["emd_T48"][3]) <= 1e-9
+
+
+@pytest.mark.parametrize("T", [7, 64, 287])
+def test_emd_pairs_vs_linprog(dev, T):
+    """Random, identical, non-negative and zero-row series; T = 287 is GAMBIA's length."""
+    from dstagnn_drought_amd import stag_gen as sg
+    rs = np.random.RandomState(T)
+    N = 6
+    data = rs.randn(T, N, 4)
+    data[:, 1] = data[:, 0]                  # identical nodes: degenerate optimum 0
+    data[:, 2] = np.abs(data[:, 2])
+    data[::4, 3] = 0.0                       # zero rows
+    data[:, 4] = np.round(data[:, 4])        # tied costs
+    pairs = np.array([(0, 1), (0, 2), (2, 3), (3, 4), (4, 5), (1, 5)] if T == 287 else
+                     [(i, j) for i in range(N) for j in range(i + 1, N)])
+    out, st = sg.NodeData(data, dev).emd_pairs(pairs)
+    out = out.cpu().numpy()
+    want = np.array([ref.process_node_pair(int(i), int(j), data) for i, j in pairs])
+    assert int(st.max()) == 0
+    np.testing.assert_allclose(out, want, rtol=0, atol=1e-9)
+
+
+def test_wasserstein_distance_dense(dev):
+    from dstagnn_drought_amd import stag_gen as sg
+    rs = np.random.RandomState(3)
+    T, B = 16, 8
+    p = rs.rand(B, T); p /= p.sum(1, keepdims=True)
+    q = rs.rand(B, T); q /= q.sum(1, keepdims=True)
+    D = rs.randn(B, T, T)
+    D[1, 3, 4] = np.nan                      # reference zeroes nan costs
+    D[2] = np.round(D[2])                    # ties
+    p[5] *= 1.001                            # infeasible -> 1.0
+    got = sg.wasserstein_distance(p, q, D, dev)
+    want = np.array([ref.emd_linprog(p[b], q[b], D[b]) for b in range(B)])
+    assert want[5] == 1.0
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-9)
+    assert abs(sg.wasserstein_distance(p[0], q[0], D[0], dev) - want[0]) <= 1e-9
+
+
+def test_stag_adjacency(dev):
+    from dstagnn_drought_amd import stag_gen as sg
+    rs = np.random.RandomState(11)
+    N = 50
+    s = np.triu(rs.rand(N, N), 1)
+    s = s + s.T
+    s[3, 7] = s[7, 3] = s[3, 9]               # a tie
+    A, R, nbr = sg.adjacency(s, 0.1, dev)
+    A0, R0 = ref.stag_adjacency(s, 0.1)
+    np.testing.assert_array_equal(A, A0)
+    np.testing.assert_array_equal(R, R0)
+    assert nbr.shape == (N, 5)
+
+
+def test_process_dataset_writes_graphs(dev, tmp_path):
+    """The reference crashes before writing its CSVs (quirk 18); ours writes all three."""
+    import pandas as pd
+    from dstagnn_drought_amd import stag_gen as sg
+    rs = np.random.RandomState(4)
+    data = rs.randn(12, 9, 4)
+    path = tmp_path / "TINY.npz"
+    np.savez(path, data=data)
+    sta, A = sg.process_dataset(str(path), "TINY", sparsity=0.34, device=dev)
+    np.testing.assert_allclose(np.load(tmp_path / "stag_034_TINY.npy"), ref.sta_matrix(data), rtol=0, atol=1e-9)
+    A0, R0 = ref.stag_adjacency(sta, 0.34)
+    np.testing.assert_array_equal(pd.read_csv(tmp_path / "stag_034_TINY.csv", header=None).to_numpy(), A0)
+    np.testing.assert_allclose(pd.read_csv(tmp_path / "strg_034_TINY.csv", header=None).to_numpy(), R0, atol=1e-15)
+
+
+# ---------------------------------------------------------------------------------------
+# fast_STAG_gen
+# ---------------------------------------------------------------------------------------
+def check_topk(A, R, sta, k, R_of_key, key):
+    """Row-wise: k ones; the selected keys are the k smallest up to ties (1e-12)."""
+    N = sta.shape[0]
+    assert np.all(A.sum(1) == k)
+    for i in range(N):
+        sel = A[i] == 1
+        ks = np.sort(key[i])
+        kth = ks[k - 1]
+        assert np.all(key[i][sel] <= kth + 1e-12)
+        assert np.all(key[i][~sel] >= kth - 1e-12)
+        np.testing.assert_array_equal(R[i][sel], R_of_key(i)[sel])
+        assert np.all(R[i][~sel] == 0)
+
+
+def test_fast_distances_golden(dev, golden_dir):
+    from dstagnn_drought_amd import fast_stag_gen as fg
+    g = load(golden_dir, "g8_fast_stag.npz")
+    got = fg.calculate_distances(g["coords"], g["feats"], device=dev)
+    np.testing.assert_allclose(got, g["sta_upper"], rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("N,sparsity", [(40, 0.1), (300, 0.01), (2139, 0.01)])
+def test_fast_graph_vs_oracle(dev, N, sparsity):
+    from dstagnn_drought_amd import fast_stag_gen as fg
+    rs = np.random.RandomState(N)
+    coords = np.arange(N)[:, None]
+    feats = rs.randn(N, 12)
+    feats[5] = feats[2]
+    sta_d = fg.distances_device(coords, feats, device=dev)
+    A, R, nbr = fg.adjacency(sta_d, sparsity, dev)
+    sta = sta_d.cpu().numpy()
+    if N <= 300:
+        s0, A0, R0 = ref.fast_stag_graph(coords, feats, sparsity)
+        np.testing.assert_allclose(sta, s0, rtol=0, atol=1e-13)
+    assert np.array_equal(sta, sta.T) and np.all(np.diag(sta) == 0)
+    k = max(1, int(N * sparsity))
+    check_topk(A, R, sta, k, lambda i: 1 - sta[i], sta)
+    # lowest-index tie order = np.argsort(kind="stable") on our own sta
+    np.testing.assert_array_equal(nbr, np.argsort(sta, axis=1, kind="stable")[:, :k])
+
+
+def test_topk_syn_size(dev):
+    """N = 4096 (BASELINE config 5): A row sums, selected keys <= the rest, both modes."""
+    from dstagnn_drought_amd import stag_gen as sg
+    from dstagnn_drought_amd import fast_stag_gen as fg
+    N = 4096
+    g = torch.Generator(device="cpu").manual_seed(0)
+    s = torch.rand(N, N, generator=g, dtype=torch.float64)
+    s = torch.triu(s, 1)
+    s = (s + s.t()).to(dev)
+    sn = s.cpu().numpy()
+    for mode, (A, R, nbr) in ((0, fg.adjacency(s, 0.01, dev)), (1, sg.adjacency(sn, 0.01, dev))):
+        key = sn if mode == 0 else 1 - sn + np.eye(N)
+        np.testing.assert_array_equal(nbr, np.argsort(key, axis=1, kind="stable")[:, :40])
+        assert np.all(A.sum(1) == 40)
+
+
+def test_fast_process_dataset(dev, tmp_path):
+    """End to end on a small (T, N, F) series: exact PCA(12) + distances + top-k, against the
+    oracle on sklearn's full-SVD PCA (cosine distances are sign-invariant per component)."""
+    from sklearn.decomposition import PCA
+    from dstagnn_drought_amd import fast_stag_gen as fg
+    rs = np.random.RandomState(9)
+    T, N, F = 20, 120, 4
+    data = rs.randn(T, N, F) + np.linspace(0, 3, N)[None, :, None]
+    path = tmp_path / "SMALL.npz"
+    np.savez(path, data=data)
+    sta, A, R = fg.process_dataset(str(path), "SMALL", sparsity=0.05, device=dev)
+    feats = PCA(n_components=12, svd_solver="full").fit_transform(data.transpose(1, 0, 2).reshape(N, -1))
+    s0, _, _ = ref.fast_stag_graph(np.arange(N)[:, None], feats, 0.05)
+    np.testing.assert_allclose(sta, s0, rtol=0, atol=1e-10)
+    check_topk(A, R, sta, 6, lambda i: 1 - sta[i], sta)
+    assert os.path.exists(tmp_path / "stag_001_SMALL.csv") and os.path.exists(tmp_path / "strg_001_SMALL.csv")
