@@ -106,6 +106,9 @@ def load():
         "dstagnn_fast_stag_distances": [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_double, _vp, _vp],
         "dstagnn_graph_topk": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp],
         "dstagnn_stag_emd_lds_bytes": [ctypes.c_int, ctypes.c_int],
+        "dstagnn_head_scratch_bytes": [],
+        "dstagnn_head_forward": [ctypes.c_int] * 7 + [_vp] * 8 + [ctypes.c_size_t, _vp],
+        "dstagnn_head_backward": [ctypes.c_int] * 7 + [_vp] * 12 + [ctypes.c_size_t, _vp],
         "dstagnn_last_error": [],
         "dstagnn_version": [],
     }
@@ -115,6 +118,7 @@ def load():
         fn.restype = ctypes.c_int
     lib.dstagnn_last_error.restype = ctypes.c_char_p
     lib.dstagnn_stag_emd_lds_bytes.restype = ctypes.c_int64
+    lib.dstagnn_head_scratch_bytes.restype = ctypes.c_int64
     _lib = lib
     return lib
 

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from .block_fn import DSTAGNNBlockFunction
+from .head_fn import DSTAGNNHeadFunction
 from .graph import cheb_polynomial, scaled_Laplacian
 
 HIP_ONLY = ("dstagnn_drought_amd: DSTAGNN_block runs only on the MI355X HIP path; "
@@ -243,9 +244,10 @@ class DSTAGNN_submodule(nn.Module):
         for block in self.BlockList:
             x, res_att = block(x, res_att)
             need_concat.append(x)
-        final_x = torch.cat(need_concat, dim=-1)
-        output1 = self.final_conv(final_x.permute(0, 3, 1, 2))[:, :, :, -1].permute(0, 2, 1)
-        return self.final_fc(output1)
+        # cat -> final_conv -> [..., -1] -> final_fc as one HIP head op (head.hip): the
+        # concatenation is never materialised (model/DSTAGNN_my.py:276-280)
+        return DSTAGNNHeadFunction.apply(self.final_conv.weight, self.final_conv.bias, self.final_fc.weight,
+                                         self.final_fc.bias, *need_concat)
 
 
 def make_model(DEVICE, num_of_d, nb_block, in_channels, K, nb_chev_filter, nb_time_filter, time_strides, adj_mx,

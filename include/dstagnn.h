@@ -32,6 +32,7 @@ extern "C" {
 typedef void* dstagnn_stream_t; /* a hipStream_t (0 = default stream) */
 
 #define DSTAGNN_MAX_K 8
+#define DSTAGNN_HEAD_MAX_BLOCKS 16
 
 enum {
   DSTAGNN_OK = 0,
@@ -194,6 +195,25 @@ int dstagnn_block_time_stage(const dstagnn_block_dims* d, const dstagnn_block_pa
 /* Dropout keep-mask the block draws (value 1/(1-p) or 0) for tests:
  * which = 0 (EmbedS output, (B,N,D)), 1 (fcmy output, (B,N,C,T) order of out). */
 int dstagnn_dropout_mask(const dstagnn_block_dims* d, int which, float* mask, dstagnn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Model head of DSTAGNN_submodule (model/DSTAGNN_my.py:265-280, head.hip): replaces
+ *   final_x = torch.cat(block outputs, -1); final_conv(final_x.permute(0,3,1,2))[..., -1]
+ *   .permute(0,2,1); final_fc(.)
+ * outs: nb device pointers (B,N,C,T) (host array); w1 final_conv.weight (O, nb*T, 1, C),
+ * b1 (O); w2 final_fc.weight (P, O), b2 (P).  h (B,N,O) is the final_conv output (saved for
+ * backward), y (B,N,P).  The cat is never materialised.  scratch >= dstagnn_head_scratch_bytes().
+ * ------------------------------------------------------------------------------------- */
+int64_t dstagnn_head_scratch_bytes(void);
+int dstagnn_head_forward(int B, int N, int C, int T, int nb, int O, int P, const float* const* outs,
+                         const float* w1, const float* b1, const float* w2, const float* b2, float* h, float* y,
+                         void* scratch, size_t scratch_bytes, dstagnn_stream_t stream);
+/* dy (B,N,P) -> dh (B,N,O) (scratch output), douts[j] (B,N,C,T) (NULL entries skipped),
+ * dw1, db1, dw2, db2 (each may be NULL). */
+int dstagnn_head_backward(int B, int N, int C, int T, int nb, int O, int P, const float* const* outs,
+                          const float* w1, const float* w2, const float* h, const float* dy, float* dh,
+                          float* const* douts, float* dw1, float* db1, float* dw2, float* db2, void* scratch,
+                          size_t scratch_bytes, dstagnn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Graph builders (stag.hip).  fp64 throughout, like the reference's numpy/scipy code.

@@ -172,6 +172,11 @@ def model_forward(blocks, final, x, cheb, adj_pa, dims, hoist=False):
     for p in blocks:
         x, res_att = block_forward(p, x, res_att, cheb, adj_pa, dims, hoist=hoist)
         need.append(x)
+    return model_head(final, need)
+
+
+def model_head(final, need):
+    """cat + final_conv + [..., -1] + final_fc (model/DSTAGNN_my.py:276-280)."""
     fx = torch.cat(need, dim=-1)
     o1 = F.conv2d(fx.permute(0, 3, 1, 2), final["final_conv.weight"], final["final_conv.bias"])[:, :, :, -1].permute(0, 2, 1)
     return o1 @ final["final_fc.weight"].t() + final["final_fc.bias"]

@@ -362,3 +362,37 @@ def test_block_vs_oracle_configs(name, first):
             assert prm.grad is None, n
         else:
             close_cal(prm.grad, grads_r[n], n)
+
+
+# ---------------------------------------------------------------------------------------
+# model head (final_conv + final_fc over the block outputs, head.hip) vs the oracle
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("B,N,C,T,nb,P", [(8, 170, 32, 12, 4, 12), (3, 37, 16, 12, 2, 5), (2, 883, 32, 12, 4, 12)])
+def test_head_vs_oracle(B, N, C, T, nb, P):
+    _need_gpu()
+    from oracle import dstagnn_ref as ref
+    from dstagnn_drought_amd.head_fn import DSTAGNNHeadFunction
+    gen = torch.Generator().manual_seed(B * 1000 + N)
+    O = 128
+    outs = [torch.randn(B, N, C, T, generator=gen) for _ in range(nb)]
+    final = {"final_conv.weight": torch.randn(O, nb * T, 1, C, generator=gen) * 0.05,
+             "final_conv.bias": torch.randn(O, generator=gen),
+             "final_fc.weight": torch.randn(P, O, generator=gen) * 0.1,
+             "final_fc.bias": torch.randn(P, generator=gen)}
+    dy = torch.randn(B, N, P, generator=gen)
+    # oracle forward + autograd
+    fr = {k: v.clone().requires_grad_(True) for k, v in final.items()}
+    orr = [o.clone().requires_grad_(True) for o in outs]
+    y_ref = ref.model_head(fr, orr)
+    y_ref.backward(dy)
+    # HIP
+    fg = {k: v.cuda().requires_grad_(True) for k, v in final.items()}
+    og = [o.cuda().requires_grad_(True) for o in outs]
+    y = DSTAGNNHeadFunction.apply(fg["final_conv.weight"], fg["final_conv.bias"], fg["final_fc.weight"],
+                                  fg["final_fc.bias"], *og)
+    y.backward(dy.cuda())
+    close(y, y_ref, what="y")
+    for k in final:
+        close(fg[k].grad, fr[k].grad, what=k)
+    for j in range(nb):
+        close(og[j].grad, orr[j].grad, what=f"d out_{j}")
