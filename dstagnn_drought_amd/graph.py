@@ -11,8 +11,6 @@ which make_model and the training script call:
 
 These run once when a model is built; they are not part of the hot path.
 """
-import csv
-
 import numpy as np
 import torch
 
@@ -42,42 +40,6 @@ def cheb_polynomial(L_tilde, K):
     return polys
 
 
-def _csv_matrix(path):
-    import pandas as pd
-    return pd.read_csv(path, header=None).to_numpy()
-
-
-def load_weighted_adjacency_matrix(file_path, num_v):
-    return np.float64(_csv_matrix(file_path) > 0)
-
-
-def load_PA(file_path):
-    return np.float64(_csv_matrix(file_path) > 0)
-
-
-def load_weighted_adjacency_matrix2(file_path, num_v):
-    return np.int64(_csv_matrix(file_path) > 0) - np.identity(num_v)
-
-
-def get_adjacency_matrix2(distance_df_filename, num_of_vertices, type_="connectivity", id_filename=None):
-    """Edge-list CSV (header line, then `from,to,cost`) -> float32 connectivity matrix."""
-    n = int(num_of_vertices)
-    A = np.zeros((n, n), dtype=np.float32)
-    ids = None
-    if id_filename:
-        with open(id_filename) as f:
-            ids = {int(v): i for i, v in enumerate(f.read().strip().split("\n"))}
-    with open(distance_df_filename) as f:
-        f.readline()
-        for row in csv.reader(f):
-            if len(row) != 3:
-                continue
-            i, j = int(row[0]), int(row[1])
-            if ids is not None:
-                A[ids[i], ids[j]] = 1
-                A[ids[j], ids[i]] = 1
-            elif type_ == "connectivity":
-                A[i, j] = 1
-            else:
-                raise ValueError("type_ error, must be connectivity or distance!")
-    return A
+# graph-file loaders live with the rest of the data I/O (data.py); re-exported here
+from .data import (get_adjacency_matrix2, load_PA, load_weighted_adjacency_matrix,  # noqa: E402,F401
+                   load_weighted_adjacency_matrix2)

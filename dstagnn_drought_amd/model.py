@@ -189,7 +189,10 @@ class DSTAGNN_block(nn.Module):
             raise RuntimeError(HIP_ONLY)
         meta = dict(self.meta)
         meta["train"] = bool(self.training)
-        meta["seed"] = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
+        # a fresh dropout seed per training forward, drawn from torch's global RNG (no draw
+        # when dropout is off: like F.dropout(p=0), which consumes no random numbers)
+        drop = self.training and meta.get("drop_p", 0.0) > 0.0
+        meta["seed"] = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop else 0
         names, params = self._param_list()
         graph = self._graph()
         return DSTAGNNBlockFunction.apply(meta, names, x.float(), res_att, graph, *params)
@@ -265,4 +268,16 @@ def make_model(DEVICE, num_of_d, nb_block, in_channels, K, nb_chev_filter, nb_ti
             nn.init.xavier_uniform_(p)
         else:
             nn.init.uniform_(p)
+    return model
+
+
+def set_dropout(model, p):
+    """Set the probability of both Dropout sites of every DSTAGNN_block in `model` (the
+    reference hard-codes 0.05 at model/DSTAGNN_my.py:218,221; 0 turns them off, e.g. for
+    trajectory parity runs)."""
+    for m in model.modules():
+        if isinstance(m, DSTAGNN_block):
+            m.meta["drop_p"] = float(p)
+            m.dropout.p = float(p)
+            m.fcmy[1].p = float(p)
     return model
