@@ -8,7 +8,8 @@ from .graph import (cheb_polynomial, get_adjacency_matrix2, load_PA, load_weight
                     load_weighted_adjacency_matrix2, scaled_Laplacian)
 from .data import load_graphdata_channel1, masked_mape_np, re_normalization, read_and_generate_dataset
 from .model import (DSTAGNN_block, DSTAGNN_submodule, Embedding, GTU, MultiHeadAttention, ScaledDotProductAttention,
-                    SMultiHeadAttention, SScaledDotProductAttention, cheb_conv, cheb_conv_withSAt, make_model)
+                    SMultiHeadAttention, SScaledDotProductAttention, cheb_conv, cheb_conv_withSAt, make_model,
+                    set_dropout)
 
 __all__ = ["make_model", "DSTAGNN_block", "DSTAGNN_submodule", "cheb_conv_withSAt", "cheb_conv", "Embedding", "GTU",
            "MultiHeadAttention", "SMultiHeadAttention", "ScaledDotProductAttention", "SScaledDotProductAttention",
