@@ -255,3 +255,23 @@ def load_graphdata_channel1(graph_signal_matrix_filename, num_of_hours, num_of_d
     print('test:', t['test_x'].size(), t['test_target'].size())
     return (t['train_x'], train_loader, t['train_target'], t['val_x'], val_loader, t['val_target'],
             t['test_x'], test_loader, t['test_target'], mean, std)
+
+
+def main(argv=None):
+    """``python -m dstagnn_drought_amd.data --config X.conf``: prepareData.py's CLI
+    (prepareData.py:164-192) — window the config's series and save the ``*_dstagnn.npz``."""
+    import argparse
+    import configparser
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default='configurations/GAMBIA_dstagnn.conf', type=str)
+    a = ap.parse_args(argv)
+    config = configparser.ConfigParser()
+    config.read(a.config)
+    dc, tc = config['Data'], config['Training']
+    return read_and_generate_dataset(dc['graph_signal_matrix_filename'], int(tc['num_of_weeks']),
+                                     int(tc['num_of_days']), int(tc['num_of_hours']), int(dc['num_for_predict']),
+                                     points_per_hour=int(dc['points_per_hour']), save=True)
+
+
+if __name__ == "__main__":
+    main()

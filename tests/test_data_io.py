@@ -102,3 +102,16 @@ def test_load_graphdata_channel1(golden_dir, tmp_path):
                                         sampler=lambda ds, r=rank: DistributedSampler(ds, 2, r, shuffle=False))
         seen.append(torch.cat([b[0] for b in out[1]]))
     assert seen[0].shape[0] + seen[1].shape[0] == tx.shape[0]
+
+
+def test_prepare_cli(golden_dir, tmp_path):
+    g = _g(golden_dir, "g10_prepare_b.npz")
+    T, N, F, h, d, w, pph, nfp = (int(v) for v in g["meta"])
+    np.savez(tmp_path / "SYN.npz", data=g["data"])
+    conf = tmp_path / "c.conf"
+    conf.write_text(f"[Data]\ngraph_signal_matrix_filename = {tmp_path}/SYN.npz\npoints_per_hour = {pph}\n"
+                    f"num_for_predict = {nfp}\n[Training]\nnum_of_weeks = {w}\nnum_of_days = {d}\n"
+                    f"num_of_hours = {h}\n")
+    D.main(["--config", str(conf)])
+    out = dict(np.load(tmp_path / f"SYN_r{h}_d{d}_w{w}_dstagnn.npz"))
+    np.testing.assert_array_equal(out["test_x"], g["out_test_x"])
