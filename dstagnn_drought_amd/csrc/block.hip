@@ -744,10 +744,18 @@ struct Bwd {
       g.M = F; g.N = (int)KC; g.K = B * N * m.T;
       g.A = x; g.am = idx1(T); g.ak = idx2(T, 1, FT);
       g.B = w.dxth; g.bk = idx1(KC); g.bn = idx1(1);
-      g.C = w.dthcat; g.cm = idx1(KC); g.cn = idx1(1);
+      // the K Theta grads adjacent in memory (one flat gradient buffer): write them as
+      // [k][f][c] directly, no unpack pass
+      bool adjacent = gd.theta[0] != nullptr;
+      for (int k = 1; k < K && adjacent; ++k) adjacent = gd.theta[k] == gd.theta[0] + (int64_t)k * F * C;
+      if (adjacent) {
+        g.C = gd.theta[0]; g.cm = idx1(C); g.cn = idx2(C, 1, (int64_t)F * C);
+      } else {
+        g.C = w.dthcat; g.cm = idx1(KC); g.cn = idx1(1);
+      }
       DS_TRY(sgemm(g));
+      if (!adjacent) DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sd));
     }
-    DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sd));
     {
       Gemm g;  // dx[b,i,f,t] += sum_{k,c} Theta_k[f,c] dxth[b,i,t,k,c]
       g.M = B * N * m.T; g.N = F; g.K = (int)KC;
@@ -806,13 +814,17 @@ struct Bwd {
       g.M = (int)ld; g.N = m.D; g.K = (int)m.BN;
       g.A = w.dqk; g.am = idx1(1); g.ak = idx1(ld);
       g.B = s.Zd; g.bk = idx1(m.D); g.bn = idx1(1);
-      g.C = w.dWqk; g.cm = idx1(m.D); g.cn = idx1(1);
+      // adjacent grads (one flat gradient buffer): the stacked GEMM writes them in place
+      const bool adjacent = gd.sat_wq && gd.sat_wk == gd.sat_wq + m.KD * m.D;
+      g.C = adjacent ? gd.sat_wq : w.dWqk; g.cm = idx1(m.D); g.cn = idx1(1);
       DS_TRY(sgemm(g));
-      PackRows pk;
-      pk.n = 2; pk.cols = m.D; pk.unpack = 1;
-      pk.src[0] = w.dWqk; pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
-      pk.dst[0] = gd.sat_wq; pk.dst[1] = gd.sat_wk;
-      DS_TRY(op_pack_rows(pk, sd));
+      if (!adjacent) {
+        PackRows pk;
+        pk.n = 2; pk.cols = m.D; pk.unpack = 1;
+        pk.src[0] = w.dWqk; pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
+        pk.dst[0] = gd.sat_wq; pk.dst[1] = gd.sat_wk;
+        DS_TRY(op_pack_rows(pk, sd));
+      }
     }
     DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}, {w.dY, gd.pre_conv_b}}, m.BN, m.D, 1));
     if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sd));
@@ -821,10 +833,9 @@ struct Bwd {
       g.M = m.D; g.N = (int)m.FT; g.K = (int)m.BN;
       g.A = w.dY; g.am = idx1(1); g.ak = idx1(m.D);
       g.B = s.O; g.bk = idx2(m.N, 1, m.FT * m.N); g.bn = idx1(m.N);
-      g.C = w.dWp; g.cm = idx1(m.FT); g.cn = idx1(1);
+      // written straight into pre_conv.weight's [d][t][0][f] layout: n = f*T + t
+      g.C = gd.pre_conv_w; g.cm = idx1(m.FT); g.cn = idx2(m.T, m.F, 1);
       DS_TRY(sgemm(g));
-      // pre_conv.weight[d][t][0][f] = dWp[d][f][t]
-      DS_TRY(op_transpose(w.dWp, gd.pre_conv_w, m.F, m.T, m.D, m.FT, m.FT, 0.f, sd));
     }
     return 0;
   }
@@ -848,12 +859,6 @@ struct Bwd {
       a.dx = w.dU; a.dxrow = idx1(N);
       a.gcontrib = w.gcon_a; a.bcontrib = nullptr;
       DS_TRY(op_ln_bwd(a, st));
-    }
-    // dE starts as a copy of dU: the side stream's fc weight grad keeps reading dU while the
-    // main chain accumulates the projection terms into dE (no mid-stage join)
-    {
-      hipError_t e = hipMemcpyAsync(w.dE, w.dU, sizeof(float) * (size_t)(m.BFT * N), hipMemcpyDeviceToDevice, st);
-      if (e != hipSuccess) { set_last_error(std::string("memcpy: ") + hipGetErrorString(e)); return (int)e; }
     }
     {  // dctx = dU Wfc
       Gemm g;
@@ -883,20 +888,25 @@ struct Bwd {
       g.M = (int)m.QW; g.N = m.N; g.K = (int)m.BFT;
       g.A = w.dqkv; g.am = idx1(1); g.ak = idx1(m.QW);
       g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
-      g.C = w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
+      const bool adjacent = gd.tat_wq && gd.tat_wk == gd.tat_wq + m.HQ * N && gd.tat_wv == gd.tat_wk + m.HQ * N;
+      g.C = adjacent ? gd.tat_wq : w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
       DS_TRY(sgemm(g));
-      PackRows pk;
-      pk.n = 3; pk.cols = m.N; pk.unpack = 1;
-      pk.src[0] = w.dWqkv; pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
-      pk.dst[0] = gd.tat_wq; pk.dst[1] = gd.tat_wk; pk.dst[2] = gd.tat_wv;
-      DS_TRY(op_pack_rows(pk, sd));
+      if (!adjacent) {
+        PackRows pk;
+        pk.n = 3; pk.cols = m.N; pk.unpack = 1;
+        pk.src[0] = w.dWqkv; pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
+        pk.dst[0] = gd.tat_wq; pk.dst[1] = gd.tat_wk; pk.dst[2] = gd.tat_wv;
+        DS_TRY(op_pack_rows(pk, sd));
+      }
     }
     {  // dE = dU + dqkv [Wq; Wk; Wv]
       Gemm g;
       g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.QW;
       g.A = w.dqkv; g.am = idx1(m.QW); g.ak = idx1(1);
       g.B = s.Wqkv; g.bk = idx1(N); g.bn = idx1(1);
-      g.C = w.dE; g.cm = idx1(N); g.cn = idx1(1);
+      // dU is only read (the side stream's fc weight grad also reads it): beta input C = dU,
+      // result to Cout = dE
+      g.C = w.dU; g.Cout = w.dE; g.cm = idx1(N); g.cn = idx1(1);
       g.beta = 1.f;
       DS_TRY(gemm(g));
     }

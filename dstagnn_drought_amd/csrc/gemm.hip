@@ -16,6 +16,7 @@
 // prefetched into registers while the MFMAs consume the current LDS buffer (2 LDS
 // buffers, one barrier per k-tile).  Long reductions are split over workgroups into
 // fp32 partial slabs summed by a deterministic second pass (no float atomics).
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -633,6 +634,10 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   const bool ktwo = g.ak.two || g.bk.two;
   // implementation: 1 = LDS-DMA 3-stage pipeline (default), 0 = register-staged
   static const int impl = getenv("DSTAGNN_GEMM_IMPL") ? atoi(getenv("DSTAGNN_GEMM_IMPL")) : 1;
+  static const bool glog = getenv("DSTAGNN_GEMM_LOG") != nullptr;
+  if (glog)
+    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld\n", g.M, g.N,
+            g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk);
   if (impl) {
     if (ktwo) { DS_CFG_SWITCH(true, true) } else { DS_CFG_SWITCH(false, true) }
   } else {
