@@ -9,6 +9,9 @@
 //   gate_fwd / gate_bwd   GTU gates tanh(p)*sigmoid(q) + concat (:192-197, :242)
 //   tail_fwd / tail_bwd   fcmy dropout + residual + ReLU + LN_C (:243-252)
 //   reductions            deterministic two-stage column sums (bias / gamma / beta grads)
+#include <map>
+#include <mutex>
+
 #include "common.hpp"
 #include "ops.hpp"
 
@@ -345,6 +348,37 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
 }
 
 // =====================================================================================
+// per-(device, stream) zero-armed ticket counters for single-launch reductions: kernels
+// that take tickets re-arm them (write 0) before they finish, so consecutive launches on
+// one stream can share them; different streams never do.
+// =====================================================================================
+}  // namespace
+
+int* stream_counters(hipStream_t st, int n) {
+  constexpr int kCounters = 1 << 16;
+  if (n > kCounters) return nullptr;
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, int*> table;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_pair(dev, st);
+  auto it = table.find(key);
+  if (it != table.end()) return it->second;
+  if (table.size() >= 256) return nullptr;
+  int* p = nullptr;
+  if (hipMalloc(&p, sizeof(int) * kCounters) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, sizeof(int) * kCounters, st) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  table[key] = p;
+  return p;
+}
+
+namespace {
+
+// =====================================================================================
 // reductions
 // =====================================================================================
 // Column sums of up to 4 same-shape sources in one launch pair (deterministic: fixed
@@ -419,6 +453,126 @@ __global__ __launch_bounds__(1024) void colsum_stage2(ColsumArgs a) {
     float* d = a.out[src] + (int64_t)oo * a.ostride;
     *d = (a.beta != 0.f ? a.beta * *d : 0.f) + red[l];
   }
+}
+
+// -------------------------------------------------------------------------------------
+// Single-launch column sums (deterministic).  Each source is an (A, E) row-major matrix.
+// Columns: E <= 256 -> one group, RP = 256/E rows per block pass (thread t: column t % E,
+// row lane t / E, so a pass reads RP*E consecutive floats); E > 256 -> groups of
+// W = I*floor(256/I) columns, one row per pass.  Rows: R chunks (grid.x), ~1K blocks in
+// total, 8 independent loads in flight per thread.  The cross-block sum is a two-level
+// ticket tree: the last block of each run of 32 row chunks adds their partials (fixed
+// order) into a level-2 partial; the last of those adds the <= 32 level-2 partials, folds
+// each output's I columns and stores.  Tickets are re-armed (0) by the blocks that drew the
+// last one, so the next launch on this stream finds them zero.  One launch, no float atomics.
+// -------------------------------------------------------------------------------------
+constexpr int kCsW = 256;   // partial width (columns)
+constexpr int kCsL1 = 32;   // row chunks per level-1 ticket
+
+struct Colsum2dArgs {
+  const float* in[4] = {};
+  float* out[4] = {};
+  int nsrc = 1;
+  int64_t A = 0; int O = 0, I = 1, E = 0;
+  int W = 256, G = 1, RP = 1, R = 1, R2 = 1;  // group width, groups/source, rows per pass, chunks, level-2 count
+  int64_t achunk = 1;
+  int64_t ostride = 1; float beta = 0.f;
+  float* part = nullptr;   // level 1: [nsrc*G][R][256], then level 2: [nsrc*G][R2][256]
+  int* cnt = nullptr;      // [nsrc*G][R2] level-1 tickets, then [nsrc*G] level-2 tickets
+};
+
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum of n <= 32 partial rows p[q*256 + t] in fixed order; all loads issued before the
+// first add (one memory round trip: the sc1 loads are served beyond the XCD's L2)
+__device__ __forceinline__ float sum_partials(const float* p, int n, int t) {
+  float u[kCsL1];
+#pragma unroll
+  for (int k = 0; k < kCsL1; ++k) u[k] = k < n ? ld_agent(p + (int64_t)k * kCsW + t) : 0.f;
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < kCsL1; ++k) v += u[k];
+  return v;
+}
+
+__global__ __launch_bounds__(256) void colsum2d_kernel(Colsum2dArgs a) {
+  __shared__ float red[kCsW];
+  __shared__ int last;
+  const int t = threadIdx.x;
+  const int r = blockIdx.x, gidx = blockIdx.y;  // gidx = src * G + group
+  const int src = gidx / a.G, grp = gidx - src * a.G;
+  const float* __restrict__ in = a.in[src];
+  const int64_t a0 = (int64_t)r * a.achunk, a1 = min(a.A, a0 + a.achunk);
+  // thread -> (column, row lane)
+  int col, lane;
+  bool act;
+  if (a.G == 1 && a.E <= kCsW) { col = t % a.E; lane = t / a.E; act = lane < a.RP; }
+  else { col = grp * a.W + t; lane = 0; act = t < a.W && col < a.E; }
+  float s0 = 0.f, s1 = 0.f;
+  if (act) {
+    const int RP = a.RP;
+    int64_t aa = a0 + lane;
+    for (; aa + 15 * RP < a1; aa += 16 * RP) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = in[(aa + (int64_t)u * RP) * a.E + col];
+#pragma unroll
+      for (int u = 0; u < 16; u += 2) { s0 += v[u]; s1 += v[u + 1]; }
+    }
+    for (; aa < a1; aa += RP) s0 += in[aa * a.E + col];
+  }
+  // fold the row lanes in fixed order: thread t holds column t % E of lane t / E (E <= 256)
+  red[t] = act ? s0 + s1 : 0.f;
+  __syncthreads();
+  float colv = red[t];
+  if (a.G == 1 && a.E <= kCsW) {
+    colv = 0.f;
+    if (t < a.E)
+      for (int l = 0; l < a.RP; ++l) colv += red[l * a.E + t];
+  }
+  // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): sc1 stores,
+  // every storing wave drains them (vmcnt(0)), a barrier, then ONE lane's agent-scope ticket;
+  // the block whose ticket came last reads with sc1 loads.  No fences (a release fence
+  // writes back the XCD's whole L2).
+  float* p1 = a.part + ((int64_t)gidx * a.R + r) * kCsW;
+  if (t < a.W) st_agent(p1 + t, colv);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int c1 = r / kCsL1;
+  const int n1 = min(kCsL1, a.R - c1 * kCsL1);
+  if (t == 0) last = atomicAdd(a.cnt + (int64_t)gidx * a.R2 + c1, 1) == n1 - 1;
+  __syncthreads();
+  if (!last) return;
+  float* p2 = a.part + ((int64_t)a.nsrc * a.G * a.R + (int64_t)gidx * a.R2 + c1) * kCsW;
+  if (t < a.W) st_agent(p2 + t, sum_partials(a.part + ((int64_t)gidx * a.R + (int64_t)c1 * kCsL1) * kCsW, n1, t));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* cnt2 = a.cnt + (int64_t)a.nsrc * a.G * a.R2 + gidx;
+  if (t == 0) {
+    __hip_atomic_store(a.cnt + (int64_t)gidx * a.R2 + c1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = atomicAdd(cnt2, 1) == a.R2 - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  red[t] = t < a.W ? sum_partials(a.part + ((int64_t)a.nsrc * a.G * a.R + (int64_t)gidx * a.R2) * kCsW, a.R2, t)
+                   : 0.f;
+  __syncthreads();
+  const int opg = a.W / a.I;
+  if (t < opg) {
+    const int o = grp * opg + t;
+    if (o < a.O) {
+      float v = 0.f;
+      for (int i = 0; i < a.I; ++i) v += red[t * a.I + i];
+      float* d = a.out[src] + (int64_t)o * a.ostride;
+      *d = (a.beta != 0.f ? a.beta * *d : 0.f) + v;
+    }
+  }
+  if (t == 0) __hip_atomic_store(cnt2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // out[a][i] = beta*out + sum_m in[a][m][i]; grid (i blocks, a)
@@ -719,6 +873,30 @@ int op_colsum_multi(const float* const* ins, float* const* outs, int nsrc, int64
   if (nsrc < 1 || nsrc > 4) { set_last_error("colsum: 1..4 sources"); return DSTAGNN_E_ARG; }
   if (E > 16384) { set_last_error("colsum: O*I > 16384"); return DSTAGNN_E_SHAPE; }
   if (A <= 0 || O <= 0) return 0;
+  static const int kCsBlocks = getenv("DSTAGNN_COLSUM_BLOCKS") ? atoi(getenv("DSTAGNN_COLSUM_BLOCKS")) : 256;
+  static const bool two_stage = getenv("DSTAGNN_COLSUM_2STAGE") && atoi(getenv("DSTAGNN_COLSUM_2STAGE")) != 0;
+  if (I <= kCsW && !two_stage) {
+    Colsum2dArgs c;
+    for (int q = 0; q < nsrc; ++q) { c.in[q] = ins[q]; c.out[q] = outs[q]; }
+    c.nsrc = nsrc; c.A = A; c.O = O; c.I = I; c.E = E;
+    if (E <= kCsW) { c.W = E; c.G = 1; c.RP = kCsW / E; }
+    else { c.W = I * (kCsW / I); c.G = (int)cdiv64(E, c.W); c.RP = 1; }
+    const int64_t groups = (int64_t)nsrc * c.G;
+    // ~512 blocks in total, >= 16 row passes per block, <= 1024 chunks (two ticket levels of 32)
+    int64_t R = std::max<int64_t>(1, std::min<int64_t>(1024, cdiv64(kCsBlocks, groups)));
+    R = std::min<int64_t>(R, std::max<int64_t>(1, A / (16 * c.RP)));
+    c.achunk = cdiv64(A, R);
+    c.R = (int)cdiv64(A, c.achunk);
+    c.R2 = (int)cdiv64(c.R, kCsL1);
+    c.ostride = ostride; c.beta = beta; c.part = part;
+    int* cnt = stream_counters(st, (int)(groups * (c.R2 + 1)));
+    if (cnt && (size_t)groups * (c.R + c.R2) * kCsW <= part_floats) {
+      c.cnt = cnt;
+      hipLaunchKernelGGL(colsum2d_kernel, dim3((unsigned)c.R, (unsigned)groups), dim3(256), 0, st, c);
+      DS_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   ColsumArgs a;
   for (int q = 0; q < nsrc; ++q) { a.in[q] = ins[q]; a.out[q] = outs[q]; }
   a.nsrc = nsrc; a.A = A; a.O = O; a.I = I; a.ostride = ostride; a.beta = beta; a.part = part;

@@ -144,6 +144,8 @@ int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
                const float* dre, float* dqkv, float* dscore, hipStream_t st);
 int op_ln_fwd(const LnFwd& a, hipStream_t st);
 int op_ln_bwd(const LnBwd& a, hipStream_t st);
+// zero-armed int tickets private to (current device, stream); nullptr if unavailable
+int* stream_counters(hipStream_t st, int n);
 int op_colsum(const float* in, int64_t A, int O, int I, float* out, int64_t ostride, float beta, float* part,
               size_t part_floats, hipStream_t st);
 int op_colsum_multi(const float* const* ins, float* const* outs, int nsrc, int64_t A, int O, int I,
