@@ -213,39 +213,46 @@ ChebSp make_sp(int B, int N, int K, int C, int T, const dstagnn_graph* g) {
   return a;
 }
 
-int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
-  const int64_t NN = (int64_t)c.N * c.N, KC = (int64_t)c.K * c.C, T = c.T, CT = (int64_t)c.C * T,
-                KCT = KC * T, FT = (int64_t)c.F * T;
+int cheb_softmax(const ChebIO& c, hipStream_t st) {
   ChebSm sm;
   sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.S = c.S; sm.apa = c.g->adj_pa; sm.cheb = c.g->cheb; sm.P = c.P;
   sm.W = c.sparse ? nullptr : c.W;
   for (int k = 0; k < c.K; ++k) sm.mask[k] = c.mask[k];
-  DS_TRY(op_cheb_softmax_fwd(sm, st));
-  // xth[(b,i,t),(k,c)] = sum_f x[b,i,f,t] Theta_k[f,c]   (plain row-major (B*N*T, K*C))
-  {
-    Gemm g;
-    g.M = c.B * c.N * c.T; g.N = (int)KC; g.K = c.F;
-    g.A = c.x; g.am = idx2(T, 1, FT); g.ak = idx1(T);
-    g.B = c.thcat; g.bk = idx1(KC); g.bn = idx1(1);
-    g.C = c.xth; g.cm = idx1(KC); g.cn = idx1(1);
-    DS_TRY(run_gemm(g, ws, kGemmWs, st));
-  }
-  // X[b,j,(t,c)] = relu( sum_{k,i} W[b,k,i,j] xth[b,i,t,k,c] )
+  return op_cheb_softmax_fwd(sm, st);
+}
+
+// xth[(b,i,t),(k,c)] = sum_f x[b,i,f,t] Theta_k[f,c]   (plain row-major (B*N*T, K*C))
+int cheb_xtheta(const ChebIO& c, float* ws, hipStream_t st) {
+  const int64_t KC = (int64_t)c.K * c.C, T = c.T, FT = (int64_t)c.F * T;
+  Gemm g;
+  g.M = c.B * c.N * c.T; g.N = (int)KC; g.K = c.F;
+  g.A = c.x; g.am = idx2(T, 1, FT); g.ak = idx1(T);
+  g.B = c.thcat; g.bk = idx1(KC); g.bn = idx1(1);
+  g.C = c.xth; g.cm = idx1(KC); g.cn = idx1(1);
+  return run_gemm(g, ws, kGemmWs, st);
+}
+
+// X[b,j,(t,c)] = relu( sum_{k,i} W[b,k,i,j] xth[b,i,t,k,c] )
+int cheb_aggregate(const ChebIO& c, float* ws, hipStream_t st) {
+  const int64_t NN = (int64_t)c.N * c.N, KC = (int64_t)c.K * c.C, T = c.T, CT = (int64_t)c.C * T, KCT = KC * T;
   if (c.sparse) {
     ChebSp sp = make_sp(c.B, c.N, c.K, c.C, c.T, c.g);
     sp.P = c.P; sp.xth = c.xth; sp.out = c.X;
     return op_cheb_spmm_fwd(sp, st);
   }
-  {
-    Gemm g;
-    g.M = c.N; g.N = (int)CT; g.K = c.K * c.N; g.batch = c.B;
-    g.A = c.W; g.am = idx1(1); g.ak = idx2(c.N, c.N, NN); g.az = idx1(c.K * NN);
-    g.B = c.xth; g.bk = idx2(c.N, KCT, c.C); g.bn = idx2(c.C, 1, KC); g.bz = idx1(c.N * KCT);
-    g.C = c.X; g.cm = idx1(CT); g.cn = idx1(1); g.cz = idx1(c.N * CT);
-    g.relu = 1;
-    DS_TRY(run_gemm(g, ws, kGemmWs, st));
-  }
-  return 0;
+  Gemm g;
+  g.M = c.N; g.N = (int)CT; g.K = c.K * c.N; g.batch = c.B;
+  g.A = c.W; g.am = idx1(1); g.ak = idx2(c.N, c.N, NN); g.az = idx1(c.K * NN);
+  g.B = c.xth; g.bk = idx2(c.N, KCT, c.C); g.bn = idx2(c.C, 1, KC); g.bz = idx1(c.N * KCT);
+  g.C = c.X; g.cm = idx1(CT); g.cn = idx1(1); g.cz = idx1(c.N * CT);
+  g.relu = 1;
+  return run_gemm(g, ws, kGemmWs, st);
+}
+
+int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
+  DS_TRY(cheb_softmax(c, st));
+  DS_TRY(cheb_xtheta(c, ws, st));
+  return cheb_aggregate(c, ws, st);
 }
 
 struct ChebGradIO {
@@ -559,26 +566,37 @@ struct Fwd {
     return 0;
   }
 
-  int stage_cheb() {
+  ChebIO cheb_io() {
     ChebIO c;
     c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
     c.x = x; c.S = s.P; c.mask = p.mask; c.g = &gr; c.sparse = m.sparse; c.thcat = s.thcat;
     c.P = s.P; c.W = s.W; c.xth = s.xth; c.X = s.X;
-    return cheb_forward(c, w.gemm_ws, st);
+    return c;
+  }
+  int stage_cheb() { return cheb_forward(cheb_io(), w.gemm_ws, st); }
+
+  int gtu_conv(int q, hipStream_t qs, float* ws) {
+    // conv[(bn,t), o] = b[o] + sum_{(j,c)} X[bn, t+j, c] W[o,c,j]; with X rows (t,c) the
+    // window (j, c) is one contiguous run of ks*C floats (GTU :190 as an implicit-im2col GEMM)
+    const int ks = m.ks[q], Tg = m.Tg[q];
+    Gemm g;
+    g.M = (int)(m.BN * Tg); g.N = 2 * m.C; g.K = m.C * ks;
+    g.A = s.X; g.am = idx2(Tg, m.C, m.CT); g.ak = idx1(1);
+    g.B = s.Wgf[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);  // re-laid (o, j, c)
+    g.C = s.conv[q]; g.cm = idx1(2 * m.C); g.cn = idx1(1);
+    g.bias = p.gtu_b[q];
+    return run_gemm(g, ws, kGemmWs, qs);
   }
 
-  int stage_tail() {
-    for (int q = 0; q < 3; ++q) {  // GTU convs (:190) as implicit-im2col GEMMs
-      // conv[(bn,t), o] = b[o] + sum_{(j,c)} X[bn, t+j, c] W[o,c,j]; with X rows (t,c) the
-      // window (j, c) is one contiguous run of ks*C floats
-      const int ks = m.ks[q], Tg = m.Tg[q];
-      Gemm g;
-      g.M = (int)(m.BN * Tg); g.N = 2 * m.C; g.K = m.C * ks;
-      g.A = s.X; g.am = idx2(Tg, m.C, m.CT); g.ak = idx1(1);
-      g.B = s.Wgf[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);  // re-laid (o, j, c)
-      g.C = s.conv[q]; g.cm = idx1(2 * m.C); g.cn = idx1(1);
-      g.bias = p.gtu_b[q];
-      DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
+  int stage_tail(bool split) {
+    if (split) {  // the three convolutions are independent: two of them on the side stream
+      DS_TRY(ks.fork());
+      DS_TRY(gtu_conv(1, ks.sd, w.gemm_ws_side));
+      DS_TRY(gtu_conv(0, st, w.gemm_ws));
+      DS_TRY(gtu_conv(2, st, w.gemm_ws));
+      DS_TRY(ks.join());
+    } else {
+      for (int q = 0; q < 3; ++q) DS_TRY(gtu_conv(q, st, w.gemm_ws));
     }
     GtuTailArgs t;  // gates + fcmy + dropout + residual + LN, one workgroup per node
     t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
@@ -592,19 +610,32 @@ struct Fwd {
 
   int run() {
     static const bool prof = getenv("DSTAGNN_HOST_PROFILE") != nullptr;
+    static const bool conc = !getenv("DSTAGNN_FWD_CONCURRENT") || atoi(getenv("DSTAGNN_FWD_CONCURRENT")) != 0;
     HostTimer ht(prof, "fwd");
     ks.init(st);
+    const bool split = conc && ks.sd != st && !params_forked;
     DS_TRY(stage_params());
     ht.lap("params");
+    ChebIO c = cheb_io();
+    if (split) {  // x Theta needs only x and Theta: it runs beside the whole attention chain
+      DS_TRY(ks.fork());
+      DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
+    }
     DS_TRY(stage_tat());
     ht.lap("tat");
     DS_TRY(stage_preconv());
     ht.lap("preconv");
     DS_TRY(stage_sat());
     ht.lap("sat");
-    DS_TRY(stage_cheb());
+    if (split) {
+      DS_TRY(cheb_softmax(c, st));
+      DS_TRY(ks.join());
+      DS_TRY(cheb_aggregate(c, w.gemm_ws, st));
+    } else {
+      DS_TRY(stage_cheb());
+    }
     ht.lap("cheb");
-    DS_TRY(stage_tail());
+    DS_TRY(stage_tail(split));
     ht.lap("tail");
     return 0;
   }

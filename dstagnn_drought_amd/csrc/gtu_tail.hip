@@ -42,31 +42,78 @@ constexpr int kU = 8;
 // KC / KT: compile-time C and T (0 = runtime) so the index divisions fold.  WL: the fcmy
 // weight (T x 3T-12) staged in LDS; false for long series (GAMBIA T=144: 242 KB), where
 // it is read through L1/L2 instead.
+//
+// Access patterns: the conv outputs are read with c fastest (rows (t', o) are contiguous
+// in o), the X tile (t, c) is staged in LDS coalesced, G goes to HBM from LDS in its
+// [c][s] order; LDS rows of G / W / X are padded to an odd stride (S+1, C+1) so the
+// column walks are bank-conflict free; the LayerNorm statistics over C use P = 64/T lane
+// groups per t (a fixed-order two-level sum) instead of T lanes walking all of C.
+
+// LDS layout (floats), shared by the kernel and the host size computation
+struct TailFwdLds {
+  int SP, CP, P, gs, rl, xs, red, mus, rss, wl, total;
+  __host__ __device__ TailFwdLds(int C, int T, bool stage_w) {
+    const int S = 3 * T - 12;
+    SP = S + 1; CP = C + 1; P = T < kNT ? kNT / T : 1;
+    gs = 0; rl = gs + C * SP; xs = rl + C * T; red = xs + T * CP;
+    mus = red + (P * T > kNT ? P * T : kNT); rss = mus + T; wl = rss + T;
+    total = wl + (stage_w ? T * SP : 0);
+  }
+};
+
+// sum over c of v[c*T + t] for every t, into out[t] (lanes: t = l % T, part = l / T)
+__device__ __forceinline__ void col_sums_over_c(const float* v, int C, int T, int P, float* red, float* out,
+                                                int tid) {
+  for (int l = tid; l < P * T; l += kNT) {
+    const int t = l % T, part = l / T;
+    float acc = 0.f;
+    for (int c = part; c < C; c += P) acc += v[c * T + t];
+    red[l] = acc;
+  }
+  __syncthreads();
+  for (int t = tid; t < T; t += kNT) {
+    float acc = 0.f;
+    for (int q = 0; q < P; ++q) acc += red[q * T + t];
+    out[t] = acc;
+  }
+  __syncthreads();
+}
+
 template <int KC, int KT, bool WL>
-__global__ __launch_bounds__(64) void gtu_tail_fwd_kernel(GtuTailArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C, CS = C * S;
-  float* Gs = lds;                       // C*S
-  float* rl = Gs + CS;                   // CT
-  float* mus = rl + CT;                  // T
-  float* rss = mus + T;                  // T
-  float* Wl = rss + T;                   // T*S (WL only)
+  const TailFwdLds L(C, T, WL);
+  const int SP = L.SP, CP = L.CP;
+  float* Gs = lds + L.gs;    // [c][SP]
+  float* rl = lds + L.rl;    // [c][t]
+  float* Xs = lds + L.xs;    // [t][CP]
+  float* red = lds + L.red;
+  float* mus = lds + L.mus;
+  float* rss = lds + L.rss;
+  float* Wl = lds + L.wl;    // [t][SP] (WL only)
   const float* Ws = WL ? Wl : a.fcmy_w;
+  const int WS = WL ? SP : S;
   const int tid = threadIdx.x;
   if (WL)
-    for (int e = tid; e < T * S; e += kNT) Wl[e] = a.fcmy_w[e];
+    for (int e = tid; e < T * S; e += kNT) Wl[(e / S) * SP + e % S] = a.fcmy_w[e];
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
-    // gates (G also goes to HBM for the backward's fcmy weight gradient)
+    const int64_t base = bn * CT;
+    // gates, element (s, c) with c fastest: coalesced conv-row reads
+    #pragma unroll 1
     for (int e0 = 0; e0 < CS; e0 += kNT * kU) {
       float pv[kU], qv[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = min(e0 + tid + kNT * u, CS - 1);
-        const int c = e / S, s = e - c * S;
+        const int sidx = e / C, c = e - sidx * C;
         int gi, t;
-        gate_index(s, T, &gi, &t);
+        gate_index(sidx, T, &gi, &t);
         const int Tg = T - 2 - 2 * gi;
-        const float* cv = a.conv[gi] + (bn * Tg + t) * C2;
+        // select, not index: a per-lane index into the kernel-argument array would copy it
+        // to scratch memory
+        const float* cg = gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2]);
+        const float* cv = cg + (bn * Tg + t) * C2;
         pv[u] = cv[c];
         qv[u] = cv[C + c];
       }
@@ -74,45 +121,40 @@ __global__ __launch_bounds__(64) void gtu_tail_fwd_kernel(GtuTailArgs a) {
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + tid + kNT * u;
         if (e < CS) {
-          const float g = fast_tanh(pv[u]) * fast_sigmoid(qv[u]);
-          Gs[e] = g;
-          a.G[bn * CS + e] = g;
+          const int sidx = e / C, c = e - sidx * C;
+          Gs[c * SP + sidx] = fast_tanh(pv[u]) * fast_sigmoid(qv[u]);
         }
       }
     }
+    if (!a.first)
+      for (int e = tid; e < CT; e += kNT) Xs[(e / C) * CP + e % C] = a.X[base + e];  // X rows (t, c)
     __syncthreads();
+    for (int e = tid; e < CS; e += kNT) a.G[bn * CS + e] = Gs[(e / S) * SP + e % S];  // [c][s], coalesced
     // fcmy + dropout + residual + ReLUs; element e = (c, t) of the (C, T) output
-    const int64_t base = bn * CT;
+    #pragma unroll 1
     for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
-      float xv[kU], Xv[kU];
+      float xv[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = min(e0 + tid + kNT * u, CT - 1);
-        const int c = e / T, t = e - c * T;
-        if (a.first) {
-          xv[u] = a.x[bn * T + t];
-          Xv[u] = 0.f;
-        } else {
-          xv[u] = a.x[base + e];
-          Xv[u] = a.X[base + t * C + c];  // X rows are (t, c)
-        }
+        xv[u] = a.first ? a.x[bn * T + e % T] : a.x[base + e];
       }
-#pragma unroll
+#pragma unroll 1
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + tid + kNT * u;
         if (e >= CT) continue;
         const int c = e / T, t = e - c * T;
         float tc = a.fcmy_b[t];
-        const float* gr = Gs + c * S;
-        const float* wr = Ws + t * S;
-        for (int s = 0; s < S; ++s) tc = fmaf(gr[s], wr[s], tc);
+        const float* gr = Gs + c * SP;
+        const float* wr = Ws + t * WS;
+        for (int sidx = 0; sidx < S; ++sidx) tc = fmaf(gr[sidx], wr[sidx], tc);
         if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
         float tco, xres;
         if (a.first) {
           tco = fmaxf(tc, 0.f);
           xres = a.res_w[c] * xv[u] + a.res_b[c];
         } else {
-          tco = fmaxf(Xv[u] + tc, 0.f);
+          tco = fmaxf(Xs[t * CP + c] + tc, 0.f);
           xres = xv[u];
         }
         const float r = fmaxf(xres + tco, 0.f);
@@ -122,15 +164,25 @@ __global__ __launch_bounds__(64) void gtu_tail_fwd_kernel(GtuTailArgs a) {
       }
     }
     __syncthreads();
+    // LayerNorm over C: mean, then the centred second moment (two fixed-order passes)
+    col_sums_over_c(rl, C, T, L.P, red, mus, tid);
+    for (int t = tid; t < T; t += kNT) mus[t] *= 1.f / C;
+    __syncthreads();
+    for (int l = tid; l < L.P * T; l += kNT) {
+      const int t = l % T, part = l / T;
+      const float mean = mus[t];
+      float acc = 0.f;
+      for (int c = part; c < C; c += L.P) { const float d = rl[c * T + t] - mean; acc += d * d; }
+      red[l] = acc;
+    }
+    __syncthreads();
     for (int t = tid; t < T; t += kNT) {
-      float sum = 0.f;
-      for (int c = 0; c < C; ++c) sum += rl[c * T + t];
-      const float mean = sum * (1.f / C);
       float var = 0.f;
-      for (int c = 0; c < C; ++c) { const float d = rl[c * T + t] - mean; var += d * d; }
+      for (int q = 0; q < L.P; ++q) var += red[q * T + t];
       const float rs = rsqrtf(var * (1.f / C) + 1e-5f);
-      mus[t] = mean; rss[t] = rs;
-      a.mu[bn * T + t] = mean; a.rs[bn * T + t] = rs;
+      rss[t] = rs;
+      a.mu[bn * T + t] = mus[t];
+      a.rs[bn * T + t] = rs;
     }
     __syncthreads();
     for (int e = tid; e < CT; e += kNT) {
@@ -141,17 +193,32 @@ __global__ __launch_bounds__(64) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   }
 }
 
+struct TailBwdLds {
+  int SP, CP, P, dxh, xhl, rr, dg, s1, s2, dxs, red, wl, total;
+  __host__ __device__ TailBwdLds(int C, int T, bool stage_w) {
+    const int S = 3 * T - 12, CT = C * T;
+    SP = S + 1; CP = C + 1; P = T < kNT ? kNT / T : 1;
+    dxh = 0; xhl = dxh + CT; rr = xhl + CT; dg = rr + CT; s1 = dg + C * SP; s2 = s1 + T; dxs = s2 + T;
+    red = dxs + T * CP; wl = red + 2 * (P * T > kNT ? P * T : kNT);
+    total = wl + (stage_w ? T * S : 0);
+  }
+};
+
 template <int KC, int KT, bool WL>
-__global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
-  float* dxh = lds;           // CT  (LN dxhat, then dtc)
-  float* xhl = dxh + CT;      // CT
-  float* rr = xhl + CT;       // CT  (r, kept for the ReLU masks)
-  float* dGs = rr + CT;       // C*S
-  float* s1s = dGs + C * S;   // T
-  float* s2s = s1s + T;       // T
-  float* Wl = s2s + T;        // T*S (WL only)
+  const TailBwdLds L(C, T, WL);
+  const int SP = L.SP, CP = L.CP;
+  float* dxh = lds + L.dxh;   // CT  (LN dxhat, then dtc)
+  float* xhl = lds + L.xhl;   // CT
+  float* rr = lds + L.rr;     // CT  (r, kept for the ReLU masks)
+  float* dGs = lds + L.dg;    // [c][SP]
+  float* s1s = lds + L.s1;    // T
+  float* s2s = lds + L.s2;    // T
+  float* dXs = lds + L.dxs;   // [t][CP] (dX tile, written to HBM coalesced)
+  float* red = lds + L.red;
+  float* Wl = lds + L.wl;     // T*S (WL only)
   const float* Ws = WL ? Wl : a.fcmy_w;
   const int tid = threadIdx.x;
   if (WL)
@@ -161,6 +228,7 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
     const float* mu = a.mu + bn * T;
     const float* rsv = a.rs + bn * T;
     // LayerNorm over C backward
+    #pragma unroll 1
     for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
       float dyv[kU], rv[kU], muv[kU], rsw[kU];
 #pragma unroll
@@ -185,13 +253,22 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
       }
     }
     __syncthreads();
+    for (int l = tid; l < L.P * T; l += kNT) {  // sum_c dxhat and dxhat*xhat per t, P lane groups
+      const int t = l % T, part = l / T;
+      float s1 = 0.f, s2 = 0.f;
+      for (int c = part; c < C; c += L.P) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
+      red[l] = s1;
+      red[L.P * T + l] = s2;
+    }
+    __syncthreads();
     for (int t = tid; t < T; t += kNT) {
       float s1 = 0.f, s2 = 0.f;
-      for (int c = 0; c < C; ++c) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
+      for (int q = 0; q < L.P; ++q) { s1 += red[q * T + t]; s2 += red[L.P * T + q * T + t]; }
       s1s[t] = s1 * (1.f / C); s2s[t] = s2 * (1.f / C);
     }
     __syncthreads();
     // ReLUs, residual, dropout: dtc (kept in LDS, dxh reused) and the direct grads
+    #pragma unroll 1
     for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
       float tcov[kU], xv[kU], rsw[kU];
 #pragma unroll
@@ -214,18 +291,19 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
         if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
         a.dtc[base + e] = dtc;
         if (a.first) {
-          a.dX[base + t * C + c] = 0.f;
+          dXs[t * CP + c] = 0.f;
           a.rcontrib[base + e] = dr * xv[u];
           a.dres[base + e] = dr;
           xhl[e] = dr;  // for the residual_conv channel reduction below
         } else {
-          a.dX[base + t * C + c] = dtco;  // dX rows are (t, c), like X
+          dXs[t * CP + c] = dtco;  // dX rows are (t, c), like X
           a.dx[base + e] = dr;
         }
         dxh[e] = dtc;
       }
     }
     __syncthreads();
+    for (int e = tid; e < CT; e += kNT) a.dX[base + e] = dXs[(e / C) * CP + e % C];  // coalesced
     if (a.first) {
       for (int t = tid; t < T; t += kNT) {
         float sum = 0.f;
@@ -238,7 +316,7 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
       const int c = e / S, s = e - c * S;
       float g = 0.f;
       for (int t = 0; t < T; ++t) g = fmaf(dxh[c * T + t], Ws[t * S + s], g);
-      dGs[e] = g;
+      dGs[c * SP + s] = g;
     }
     __syncthreads();
     // gates backward into the zero-padded (t', o) rows of each GTU
@@ -251,6 +329,7 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
       const int E = C2 * Lp;
       float* orow = a.dconv_pad[gi] + bn * E;
       const float* cv = a.conv[gi] + bn * C2 * Tg;
+      #pragma unroll 1
       for (int e0 = 0; e0 < E; e0 += kNT * kU) {
         float pv[kU], qv[kU];
 #pragma unroll
@@ -271,7 +350,7 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
           float v = 0.f;
           if (t >= 0 && t < Tg) {
             const int c = o < C ? o : o - C;
-            const float dg = dGs[c * S + off + t];
+            const float dg = dGs[c * SP + off + t];
             const float th = fast_tanh(pv[u]), sg = fast_sigmoid(qv[u]);
             v = o < C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
           }
@@ -283,14 +362,8 @@ __global__ __launch_bounds__(64) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   }
 }
 
-size_t fwd_lds(const GtuTailArgs& a, bool wl) {
-  const size_t S = 3 * (size_t)a.T - 12;
-  return sizeof(float) * ((size_t)a.C * S + (size_t)a.C * a.T + 2 * (size_t)a.T + (wl ? (size_t)a.T * S : 0));
-}
-size_t bwd_lds(const GtuTailArgs& a, bool wl) {
-  const size_t S = 3 * (size_t)a.T - 12;
-  return sizeof(float) * (3 * (size_t)a.C * a.T + (size_t)a.C * S + 2 * (size_t)a.T + (wl ? (size_t)a.T * S : 0));
-}
+size_t fwd_lds(const GtuTailArgs& a, bool wl) { return sizeof(float) * (size_t)TailFwdLds(a.C, a.T, wl).total; }
+size_t bwd_lds(const GtuTailArgs& a, bool wl) { return sizeof(float) * (size_t)TailBwdLds(a.C, a.T, wl).total; }
 
 unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 65536); }
 
