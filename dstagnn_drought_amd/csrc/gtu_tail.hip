@@ -193,13 +193,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
   }
 }
 
+// dG, the dX tile and the LN reduction scratch share one region (disjoint phases)
 struct TailBwdLds {
-  int SP, CP, P, dxh, xhl, rr, dg, s1, s2, dxs, red, wl, total;
+  int SP, CP, P, dxh, xhl, rr, dg, dxs, red, s1, s2, wl, total;
   __host__ __device__ TailBwdLds(int C, int T, bool stage_w) {
     const int S = 3 * T - 12, CT = C * T;
     SP = S + 1; CP = C + 1; P = T < kNT ? kNT / T : 1;
-    dxh = 0; xhl = dxh + CT; rr = xhl + CT; dg = rr + CT; s1 = dg + C * SP; s2 = s1 + T; dxs = s2 + T;
-    red = dxs + T * CP; wl = red + 2 * (P * T > kNT ? P * T : kNT);
+    const int nred = 2 * (P * T > kNT ? P * T : kNT);
+    int shared = C * SP;
+    if (T * CP > shared) shared = T * CP;
+    if (nred > shared) shared = nred;
+    dxh = 0; xhl = dxh + CT; rr = xhl + CT; dg = rr + CT; dxs = dg; red = dg; s1 = dg + shared; s2 = s1 + T; wl = s2 + T;
     total = wl + (stage_w ? T * S : 0);
   }
 };
@@ -276,6 +280,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         const int e = min(e0 + tid + kNT * u, CT - 1);
         const int t = e % T;
         tcov[u] = a.tco[base + e];
+
         xv[u] = a.first ? a.x[bn * T + t] : 0.f;
         rsw[u] = rsv[t];
       }
@@ -304,6 +309,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
     __syncthreads();
     for (int e = tid; e < CT; e += kNT) a.dX[base + e] = dXs[(e / C) * CP + e % C];  // coalesced
+    __syncthreads();  // dXs shares its LDS with dGs
     if (a.first) {
       for (int t = tid; t < T; t += kNT) {
         float sum = 0.f;
@@ -312,6 +318,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       }
     }
     // fcmy backward: dG[c, s] = sum_t dtc[c, t] W[t, s]
+    #pragma unroll 1
     for (int e = tid; e < C * S; e += kNT) {
       const int c = e / S, s = e - c * S;
       float g = 0.f;
@@ -320,15 +327,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
     __syncthreads();
     // gates backward into the zero-padded (t', o) rows of each GTU
-#pragma unroll
+#pragma unroll 1
     for (int gi = 0; gi < 3; ++gi) {
       const int ks = 3 + 2 * gi;
       const int Tg = T - ks + 1;
       const int Lp = T + ks - 1;
       const int off = gi == 0 ? 0 : (gi == 1 ? T - 2 : 2 * T - 6);
       const int E = C2 * Lp;
-      float* orow = a.dconv_pad[gi] + bn * E;
-      const float* cv = a.conv[gi] + bn * C2 * Tg;
+      float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * E;
+      const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
       #pragma unroll 1
       for (int e0 = 0; e0 < E; e0 += kNT * kU) {
         float pv[kU], qv[kU];
@@ -395,7 +402,8 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
   const bool wl = bwd_lds(a, true) <= 32 * 1024;
   const size_t lds = bwd_lds(a, wl);
   if (lds > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-  if (a.C == 32 && a.T == 12 && wl) return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
+  static const bool generic = getenv("DSTAGNN_TAIL_GENERIC") && atoi(getenv("DSTAGNN_TAIL_GENERIC")) != 0;
+  if (a.C == 32 && a.T == 12 && wl && !generic) return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
   if (wl) return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, true>, lds, a, st);
   return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false>, lds, a, st);
 }
