@@ -611,16 +611,43 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
   const float* S = a.S + (int64_t)bk * N * N;
   const float* Mk = a.mask[k];
   const float* Tk = a.cheb + (int64_t)k * N * N;
+  // pass 1: column max (4 independent chains, loads batched), pass 2: sum of exp
   float m = -INFINITY, l = 0.f;
   if (j < N) {
-#pragma unroll 2
-    for (int i = g; i < N; i += kSmG) {
-      const int64_t o = (int64_t)i * N + j;
-      const float z = S[o] + a.apa[o] * Mk[o];
-      const float mn = fmaxf(m, z);
-      l = l * __expf(m - mn) + __expf(z - mn);
-      m = mn;
+    float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int i = g;
+    for (; i + 3 * kSmG < N; i += 4 * kSmG) {
+      float z[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = (int64_t)(i + u * kSmG) * N + j;
+        z[u] = S[o] + a.apa[o] * Mk[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) m4[u] = fmaxf(m4[u], z[u]);
     }
+    for (; i < N; i += kSmG) {
+      const int64_t o = (int64_t)i * N + j;
+      m4[0] = fmaxf(m4[0], S[o] + a.apa[o] * Mk[o]);
+    }
+    m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+    float l4[4] = {0.f, 0.f, 0.f, 0.f};
+    i = g;
+    for (; i + 3 * kSmG < N; i += 4 * kSmG) {
+      float z[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = (int64_t)(i + u * kSmG) * N + j;
+        z[u] = S[o] + a.apa[o] * Mk[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) l4[u] += __expf(z[u] - m);
+    }
+    for (; i < N; i += kSmG) {
+      const int64_t o = (int64_t)i * N + j;
+      l4[0] += __expf(S[o] + a.apa[o] * Mk[o] - m);
+    }
+    l = (l4[0] + l4[1]) + (l4[2] + l4[3]);
   }
   sm_m[g][cj] = m; sm_l[g][cj] = l;
   __syncthreads();
@@ -657,15 +684,28 @@ __global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
   const float* dW = a.dW + (int64_t)bk * N * N;
   const float* Tk = a.cheb + (int64_t)k * N * N;
   float c = 0.f;
-  if (j < N)
-#pragma unroll 2
-    for (int i = g; i < N; i += kSmG) {
-      const int64_t o = (int64_t)i * N + j;
-      // dW is only defined where some T_k is non-zero (the sparse path writes the
-      // support only, no memset): select, so off-support garbage never propagates
-      const float t = Tk[o];
-      c += P[o] * (t != 0.f ? t * dW[o] : 0.f);
+  if (j < N) {
+    // dW is only defined where some T_k is non-zero (the sparse path writes the
+    // support only, no memset): select, so off-support garbage never propagates
+    float c4[4] = {0.f, 0.f, 0.f, 0.f};
+    int i = g;
+    for (; i + 3 * kSmG < N; i += 4 * kSmG) {
+      float pv[4], tv[4], dv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = (int64_t)(i + u * kSmG) * N + j;
+        pv[u] = P[o]; tv[u] = Tk[o]; dv[u] = dW[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) c4[u] += pv[u] * (tv[u] != 0.f ? tv[u] * dv[u] : 0.f);
     }
+    for (; i < N; i += kSmG) {
+      const int64_t o = (int64_t)i * N + j;
+      const float t = Tk[o];
+      c4[0] += P[o] * (t != 0.f ? t * dW[o] : 0.f);
+    }
+    c = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+  }
   sm_c[g][cj] = c;
   __syncthreads();
   c = 0.f;
