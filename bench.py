@@ -57,6 +57,7 @@ def build_block(device):
             torch.nn.init.xavier_uniform_(p)
         else:
             torch.nn.init.uniform_(p)
+    D.set_direct_grads(blk)  # .grad written by the block's backward (no AccumulateGrad nodes)
     return blk.to(device).train(), cheb, torch.FloatTensor(pa)
 
 
@@ -87,7 +88,7 @@ def extras(dev, steps, warmup):
             torch.nn.init.xavier_uniform_(p)
         else:
             torch.nn.init.uniform_(p)
-    blk = blk.to(dev).train()
+    blk = D.set_direct_grads(blk.to(dev).train())
     gen = torch.Generator(device=dev).manual_seed(5)
     x1 = torch.randn(B, N, 1, T, device=dev, generator=gen)
     g1 = torch.randn(B, N, C, T, device=dev, generator=gen)
@@ -102,7 +103,7 @@ def extras(dev, steps, warmup):
     t_first = time_loop(first_step, steps, warmup)
 
     net = D.make_model(dev, 1, 4, 1, K, C, C, 1, tmd, pa, tmd, T, T, N, Dm, dk, dk, h)
-    net.train()
+    D.set_direct_grads(net).train()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
     crit = torch.nn.SmoothL1Loss().to(dev)
     xm = torch.randn(B, N, 1, T, device=dev, generator=gen)

@@ -179,6 +179,9 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         ctx.meta, ctx.names, ctx.mode, ctx.dims, ctx.graph = meta, names, mode, dims, graph
         ctx.save_buf, ctx.sizes = save, (sv, sc)
         ctx.save_for_backward(x, ra if ra is not None else torch.empty(0, device=dev), *params)
+        # direct-grad mode (set_direct_grads): the backward stores the parameter gradients in
+        # .grad itself instead of returning them through 36 AccumulateGrad nodes
+        ctx.direct_params = params if meta.get("direct_grads") else None
         return out, re_at
 
     @staticmethod
@@ -211,6 +214,15 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
                                         _lib.stream_handle(dev))
         _lib.check(rc, "dstagnn_block_backward")
         ctx.save_buf = None
+        if ctx.direct_params is not None:
+            for prm, g in zip(ctx.direct_params, grads):
+                if g is None or not prm.requires_grad:
+                    continue
+                if prm.grad is None:
+                    prm.grad = g
+                else:
+                    prm.grad.add_(g)
+            grads = [None] * len(grads)
         return (None, None, d_x, d_ra, None, *grads)
 
 

@@ -178,6 +178,7 @@ class DSTAGNN_block(nn.Module):
         self.num_of_d = num_of_d
         self.nb_time_filter = nb_time_filter
         self.sparse_cheb = True  # use the CSC/CSR support path when the support is sparse
+        self.direct_grads = False  # see set_direct_grads
 
     def forward(self, x, res_att):
         B, N, Fd, T = x.shape
@@ -189,6 +190,7 @@ class DSTAGNN_block(nn.Module):
             raise RuntimeError(HIP_ONLY)
         meta = dict(self.meta)
         meta["train"] = bool(self.training)
+        meta["direct_grads"] = self.direct_grads
         # a fresh dropout seed per training forward, drawn from torch's global RNG (no draw
         # when dropout is off: like F.dropout(p=0), which consumes no random numbers)
         drop = self.training and meta.get("drop_p", 0.0) > 0.0
@@ -202,11 +204,18 @@ class DSTAGNN_block(nn.Module):
     # is replaced, e.g. by .to())
     def _param_list(self):
         c = self.__dict__.get("_plist")
-        if c is None or len(c[1]) != sum(1 for _ in self.parameters()):
+        # valid while every (submodule, attribute) still holds the same Parameter object
+        # (in-place updates such as load_state_dict keep them; re-assignment does not)
+        if c is None or any(mod._parameters.get(attr) is not prm for mod, attr, prm in c[2]):
             names, params = zip(*self.named_parameters())
-            c = (tuple(names), tuple(params))
+            slots = []
+            for n in names:
+                mod_name, _, attr = n.rpartition(".")
+                mod = self.get_submodule(mod_name) if mod_name else self
+                slots.append((mod, attr, mod._parameters[attr]))
+            c = (tuple(names), tuple(params), tuple(slots))
             self.__dict__["_plist"] = c
-        return c
+        return c[0], c[1]
 
     def _graph(self):
         cc = self.cheb_conv_SAt
@@ -280,4 +289,18 @@ def set_dropout(model, p):
             m.meta["drop_p"] = float(p)
             m.dropout.p = float(p)
             m.fcmy[1].p = float(p)
+    return model
+
+
+def set_direct_grads(model, enabled=True):
+    """Direct-gradient mode for every DSTAGNN_block in `model`: the block's backward writes
+    its parameter gradients into ``param.grad`` (set, or added when a gradient is already
+    there) instead of handing them to autograd's per-parameter AccumulateGrad nodes — about
+    4 us of host time per parameter per step (36 per block).  ``loss.backward()`` /
+    optimiser semantics are unchanged; what it gives up: ``torch.autograd.grad(..., inputs=
+    <block parameters>)`` no longer returns those gradients, and post-accumulate-grad hooks on
+    them do not fire.  Off by default; the training driver and the benchmark turn it on."""
+    for m in model.modules():
+        if isinstance(m, DSTAGNN_block):
+            m.direct_grads = bool(enabled)
     return model

@@ -40,7 +40,7 @@ import torch.utils.data
 
 from . import data as data_io
 from .dp import GradAllReducer, mask_support_of
-from .model import make_model, set_dropout
+from .model import make_model, set_direct_grads, set_dropout
 
 
 def seed_torch(seed):
@@ -242,6 +242,7 @@ def run(config_path, *, epochs=None, double_step=True, dropout=None, max_batches
                                         int(tc['batch_size']))
     next(iter(train_loader))  # the reference probes one batch (:59-61): same RNG draw before the init
     net = build(config, device)
+    set_direct_grads(net)  # the loop only uses loss.backward() + .grad
     if dropout is not None:
         set_dropout(net, dropout)
     train_x, train_y, val_x, val_y, test_x, test_y = (t.to(device) for t in

@@ -396,3 +396,42 @@ def test_head_vs_oracle(B, N, C, T, nb, P):
         close(fg[k].grad, fr[k].grad, what=k)
     for j in range(nb):
         close(og[j].grad, orr[j].grad, what=f"d out_{j}")
+
+
+def test_direct_grads_equal_autograd_grads():
+    """set_direct_grads: the block's backward writes .grad itself; values identical to the
+    AccumulateGrad path, accumulation across two backward passes included."""
+    _need_gpu()
+    import dstagnn_drought_amd as D
+    B, N, T, K, h, Dm, dk, C = 2, 24, 12, 3, 2, 32, 8, 8
+    rs = np.random.RandomState(3)
+    tmd = np.eye(N)
+    pa = np.zeros((N, N))
+    for i in range(N):
+        tmd[i, rs.choice(N, 2, replace=False)] = 1.0
+        pa[i, rs.choice(N, 3, replace=False)] = 1.0
+    cheb = [torch.from_numpy(c_).float() for c_ in D.cheb_polynomial(D.scaled_Laplacian(tmd), K)]
+    torch.manual_seed(0)
+    blk = D.DSTAGNN_block("cpu", C, C, K, C, C, 1, cheb, pa, tmd, N, T, Dm, dk, dk, h).cuda().eval()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(B, N, C, T, device="cuda", generator=g)
+    res = torch.randn(B, 1, h, T, T, device="cuda", generator=g)
+    go = torch.randn(B, N, C, T, device="cuda", generator=g)
+    gr = torch.randn(B, C, h, T, T, device="cuda", generator=g)
+
+    def grads(direct, passes):
+        D.set_direct_grads(blk, direct)
+        for p in blk.parameters():
+            p.grad = None
+        for _ in range(passes):
+            o, r = blk(x, res)
+            torch.autograd.backward([o, r], [go, gr])
+        return {n: (None if p.grad is None else p.grad.clone()) for n, p in blk.named_parameters()}
+
+    for passes in (1, 2):
+        a, b = grads(False, passes), grads(True, passes)
+        for n in a:
+            assert (a[n] is None) == (b[n] is None), n
+            if a[n] is not None:
+                assert torch.equal(a[n], b[n]), n
+    D.set_direct_grads(blk, False)
