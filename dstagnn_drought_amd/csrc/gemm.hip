@@ -96,12 +96,40 @@ template <int WM, int WN>
 __device__ __forceinline__ void gemm_epilogue(const GemmK& g, const TileCoord& c, int wrow0, int wcol0, int lane,
                                               floatx16 (&acc)[WM][WN]) {
   const int lr = lane & 31, lk = lane >> 5;
+  const bool reads = g.splitk == 1 && (g.beta != 0.f || g.emask);
 #pragma unroll
   for (int i = 0; i < WM; ++i)
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
       const int n = c.n0 + wcol0 + j * 32 + lr;
       if (n >= g.N) continue;
+      if (reads) {
+        // beta * C and the ReLU mask: all 16 loads issued before the first store (the
+        // stores may alias C, so element-wise load/store pairs would serialise 16 memory
+        // round trips per lane)
+        const int64_t zo = zoff(g.cz, c.zb);
+        const int32_t no = koff(g.cn, n);
+        float cin[16], em[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = min(c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk, g.M - 1);
+          const int64_t o = zo + koff(g.cm, m) + no;
+          cin[r] = g.beta != 0.f ? g.C[o] : 0.f;
+          em[r] = g.emask ? g.emask[o] : 1.f;
+        }
+        float* dst = g.Cout ? g.Cout : g.C;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (m >= g.M) continue;
+          float v = acc[i][j][r] * g.alpha + g.beta * cin[r];
+          if (g.bias) v += g.bias[n * g.bias_stride];
+          if (g.relu) v = fmaxf(v, 0.f);
+          if (em[r] <= 0.f) v = 0.f;
+          dst[zo + koff(g.cm, m) + no] = v;
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
@@ -605,8 +633,9 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
 
   // split-K when the grid leaves CUs idle and the reduction is long
   int splitk = 1;
+  static const int split_target = getenv("DSTAGNN_SPLITK_TARGET") ? atoi(getenv("DSTAGNN_SPLITK_TARGET")) : 512;
   if (g.K > 0 && blocks < 128 && g.K >= 512 && ws) {
-    int want = (int)std::min<int64_t>(512, cdiv64(512, blocks));
+    int want = (int)std::min<int64_t>(512, cdiv64(split_target, blocks));
     int maxk = g.K / 128;  // keep >= 128 k per split
     splitk = std::max(1, std::min(want, maxk));
     if (env_split > 0) splitk = std::min(env_split, std::max(1, g.K / 64));

@@ -412,7 +412,13 @@ def test_direct_grads_equal_autograd_grads():
         pa[i, rs.choice(N, 3, replace=False)] = 1.0
     cheb = [torch.from_numpy(c_).float() for c_ in D.cheb_polynomial(D.scaled_Laplacian(tmd), K)]
     torch.manual_seed(0)
-    blk = D.DSTAGNN_block("cpu", C, C, K, C, C, 1, cheb, pa, tmd, N, T, Dm, dk, dk, h).cuda().eval()
+    blk = D.DSTAGNN_block("cpu", C, C, K, C, C, 1, cheb, pa, tmd, N, T, Dm, dk, dk, h)
+    for p in blk.parameters():  # make_model's init (Theta / mask are allocated uninitialised)
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+        else:
+            torch.nn.init.uniform_(p)
+    blk = blk.cuda().eval()
     g = torch.Generator(device="cuda").manual_seed(1)
     x = torch.randn(B, N, C, T, device="cuda", generator=g)
     res = torch.randn(B, 1, h, T, T, device="cuda", generator=g)
