@@ -24,6 +24,9 @@
 namespace {
 
 constexpr int BKMAX = 32;  // k-tile depth (16 or 32, template parameter)
+#ifndef DSTAGNN_GEMM_NS4
+#define DSTAGNN_GEMM_NS4 0  // 1: 4-stage LDS-DMA pipeline where the vmcnt budget allows (measured slower: occupancy)
+#endif
 
 #ifdef DSTAGNN_ABLATE_STAMP
 // timeline probe build: thread 0 of each of the first 4096 workgroups records s_memtime
@@ -367,9 +370,12 @@ __device__ __forceinline__ void wait_vm_barrier() {
 
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO>
 __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
-  constexpr int BK = 32, NS = 3;
+  constexpr int BK = 32;
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // DMA instructions per thread per tile
+  // pipeline depth: NS-1 tiles in flight; the counted wait holds (NS-2) tiles' DMAs, which
+  // must fit the 6-bit vmcnt (63)
+  constexpr int NS = (DSTAGNN_GEMM_NS4 && 2 * (LA + LB) <= 63) ? 4 : 3;
   __shared__ __attribute__((aligned(16))) float As[NS][BM * BK];
   __shared__ __attribute__((aligned(16))) float Bs[NS][BN * BK];
 
@@ -459,18 +465,23 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if (ntiles > 0) issue(kbeg, 0);
-  if (ntiles > 1) issue(kbeg + BK, 1);
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < ntiles) issue(kbeg + s0 * BK, s0);
   DS_STAMP(1);
   // lane half h (lane >> 5) supplies k = 16 h + s at MFMA step s (A and B agree)
   const int lr = lane & 31, lk = lane >> 5;
   const int arow0 = wr * 32 * WM, bcol0 = wc * 32 * WN;
   int st = 0;
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) wait_vm_barrier<LA + LB>();
-    else wait_vm_barrier<0>();
+    {  // retire tile t; the tiles issued after it stay in flight
+      const int ahead = min(ntiles - 1 - t, NS - 2);
+      if (NS == 4 && ahead >= 2) wait_vm_barrier<(NS == 4 ? 2 : 0) * (LA + LB)>();
+      else if (ahead >= 1) wait_vm_barrier<LA + LB>();
+      else wait_vm_barrier<0>();
+    }
     if (t == 0) DS_STAMP(2);
-    if (t + 2 < ntiles) issue(kbeg + (t + 2) * BK, st == 0 ? 2 : st - 1);
+    if (t + NS - 1 < ntiles) issue(kbeg + (t + NS - 1) * BK, st == 0 ? NS - 1 : st - 1);
     const float* as = As[st];
     const float* bs = Bs[st];
 #pragma unroll
@@ -509,7 +520,7 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][c], bv[j][c], acc[i][j], 0, 0, 0);
     }
     if (t < 8) DS_STAMP(3 + t);
-    st = st == 2 ? 0 : st + 1;
+    st = st == NS - 1 ? 0 : st + 1;
   }
   gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
 #ifdef DSTAGNN_ABLATE_STAMP
