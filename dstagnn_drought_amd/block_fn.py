@@ -136,18 +136,15 @@ _GLAYOUT = {}
 
 
 def _grad_layout(names, params, first):
-    """Offsets of every used parameter's gradient in one flat buffer (256-B aligned slots)."""
+    """(used mask, total elements) of the flat gradient buffer: the used parameters' gradients
+    packed back to back in parameter order (adjacent Q|K|V, Q'|K', Theta_k slots let the
+    library write the stacked weight gradients in place)."""
     key = (names, tuple(tuple(t.shape) for t in params), first)
     lay = _GLAYOUT.get(key)
     if lay is None:
-        offs, total = [], 0
-        for n, t in zip(names, params):
-            if first or not n.startswith(UNUSED_INNER):
-                offs.append(total)
-                total += (t.numel() + 63) // 64 * 64
-            else:
-                offs.append(None)
-        lay = _GLAYOUT[key] = (offs, total)
+        used = tuple(first or not n.startswith(UNUSED_INNER) for n in names)
+        total = sum(t.numel() for t, u in zip(params, used) if u)
+        lay = _GLAYOUT[key] = (used, total)
     return lay
 
 
@@ -197,9 +194,10 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         first = dims.F == 1
         # every parameter gradient is a view of ONE flat buffer: one allocation per
         # backward instead of one per parameter (autograd adopts the views as .grad)
-        offs, total = _grad_layout(names, params, first)
+        used, total = _grad_layout(names, params, first)
         flat = torch.empty(total, dtype=torch.float32, device=dev)
-        grads = [None if o is None else flat[o:o + t.numel()].view(t.shape) for o, t in zip(offs, params)]
+        views = iter(torch._utils._unflatten_dense_tensors(flat, [t for t, u in zip(params, used) if u]))
+        grads = [next(views) if u else None for u in used]
         gs = _fill(_lib.BlockGrads(), names, grads)
         p = _params_struct(names, params)
         g = _graph_struct_cached(ctx.graph)
