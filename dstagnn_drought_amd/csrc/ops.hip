@@ -63,6 +63,176 @@ struct TatArgs {
   float* dscore;         // (B,F,h,T,T) dS (== d res_att before f-reduction)
 };
 
+// -------------------------------------------------------------------------------------
+// Wave-per-problem variants for short series (T <= 16): one 64-lane wave owns one
+// (b, f, head) problem, four per workgroup, so no lane idles through the T-wide softmax
+// phases: the column softmax over the query axis runs on lanes (j = lane % 16, part =
+// lane / 16) with the part sums combined by xor-shuffles over lane bits 4 and 5.  All
+// global accesses are row-contiguous (coalesced).
+// -------------------------------------------------------------------------------------
+constexpr int kTatW = 4;  // problems (waves) per workgroup
+
+__device__ __forceinline__ float xor_max_1632(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float xor_sum_1632(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+__host__ __device__ inline int tat_wave_fwd_floats(int T, int dk, int dv) {
+  return 2 * T * (dk + 1) + T * (dv + 1) + T * T;
+}
+__host__ __device__ inline int tat_wave_bwd_floats(int T, int dk, int dv) {
+  return 2 * T * (dk + 1) + 2 * T * (dv + 1) + 2 * T * T;
+}
+
+__global__ __launch_bounds__(256) void tat_fwd_wave_kernel(TatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int T = a.T, dk = a.dk, dv = a.dv, dkp = dk + 1, dvp = dv + 1;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int id = blockIdx.x * kTatW + w;  // ((b*F + f)*h + hd)
+  const bool live = id < a.B * a.F * a.h;
+  float* Qs = sm + w * tat_wave_fwd_floats(T, dk, dv);
+  float* Ks = Qs + T * dkp;
+  float* Vs = Ks + T * dkp;
+  float* Ss = Vs + T * dvp;
+  const int hd = id % a.h, bf = id / a.h, b = bf / a.F;
+  const int ld = 2 * a.h * dk + a.h * dv;
+  const float* base = a.qkv + (int64_t)bf * T * ld;
+  if (live) {
+    for (int e = lane; e < T * dk; e += 64) {
+      const int i = e / dk, d = e - i * dk;
+      Qs[i * dkp + d] = base[(int64_t)i * ld + hd * dk + d];
+      Ks[i * dkp + d] = base[(int64_t)i * ld + a.h * dk + hd * dk + d];
+    }
+    for (int e = lane; e < T * dv; e += 64) {
+      const int i = e / dv, d = e - i * dv;
+      Vs[i * dvp + d] = base[(int64_t)i * ld + 2 * a.h * dk + hd * dv + d];
+    }
+  }
+  __syncthreads();
+  const int64_t sbase = (int64_t)id * T * T;
+  if (live) {
+    const float* rp = nullptr;
+    if (a.res_mode == DSTAGNN_RES_BCAST) rp = a.res + ((int64_t)b * a.h + hd) * T * T;
+    else if (a.res_mode == DSTAGNN_RES_FULL) rp = a.res + sbase;
+    for (int e = lane; e < T * T; e += 64) {
+      const int i = e / T, j = e - i * T;
+      float sc = 0.f;
+      for (int d = 0; d < dk; ++d) sc = fmaf(Qs[i * dkp + d], Ks[j * dkp + d], sc);
+      sc *= a.scale;
+      if (rp) sc += rp[e];
+      Ss[e] = sc;
+      a.re_at[sbase + e] = sc;
+    }
+  }
+  __syncthreads();
+  if (live) {  // softmax over i for column j
+    const int j = lane & 15, part = lane >> 4;
+    float m = -INFINITY;
+    if (j < T)
+      for (int i = part; i < T; i += 4) m = fmaxf(m, Ss[i * T + j]);
+    m = xor_max_1632(m);
+    float l = 0.f;
+    if (j < T)
+      for (int i = part; i < T; i += 4) l += __expf(Ss[i * T + j] - m);
+    l = xor_sum_1632(l);
+    const float inv = 1.f / l;
+    if (j < T)
+      for (int i = part; i < T; i += 4) Ss[i * T + j] = __expf(Ss[i * T + j] - m) * inv;
+  }
+  __syncthreads();
+  if (live) {
+    for (int e = lane; e < T * T; e += 64) a.att[sbase + e] = Ss[e];
+    const int ldc = a.h * dv;
+    float* cbase = a.ctx + (int64_t)bf * T * ldc;
+    for (int e = lane; e < T * dv; e += 64) {
+      const int i = e / dv, d = e - i * dv;
+      float acc = 0.f;
+      for (int j = 0; j < T; ++j) acc = fmaf(Ss[i * T + j], Vs[j * dvp + d], acc);
+      cbase[(int64_t)i * ldc + hd * dv + d] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void tat_bwd_wave_kernel(TatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int T = a.T, dk = a.dk, dv = a.dv, dkp = dk + 1, dvp = dv + 1;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int id = blockIdx.x * kTatW + w;
+  const bool live = id < a.B * a.F * a.h;
+  float* Qs = sm + w * tat_wave_bwd_floats(T, dk, dv);
+  float* Ks = Qs + T * dkp;
+  float* Vs = Ks + T * dkp;
+  float* dCs = Vs + T * dvp;
+  float* As = dCs + T * dvp;
+  float* dAs = As + T * T;
+  const int hd = id % a.h, bf = id / a.h;
+  const int ld = 2 * a.h * dk + a.h * dv, ldc = a.h * dv;
+  const float* base = a.qkv + (int64_t)bf * T * ld;
+  const float* cb = a.dctx + (int64_t)bf * T * ldc;
+  const int64_t sbase = (int64_t)id * T * T;
+  if (live) {
+    for (int e = lane; e < T * dk; e += 64) {
+      const int i = e / dk, d = e - i * dk;
+      Qs[i * dkp + d] = base[(int64_t)i * ld + hd * dk + d];
+      Ks[i * dkp + d] = base[(int64_t)i * ld + a.h * dk + hd * dk + d];
+    }
+    for (int e = lane; e < T * dv; e += 64) {
+      const int i = e / dv, d = e - i * dv;
+      Vs[i * dvp + d] = base[(int64_t)i * ld + 2 * a.h * dk + hd * dv + d];
+      dCs[i * dvp + d] = cb[(int64_t)i * ldc + hd * dv + d];
+    }
+    for (int e = lane; e < T * T; e += 64) As[e] = a.att[sbase + e];
+  }
+  __syncthreads();
+  float* dbase = a.dqkv + (int64_t)bf * T * ld;
+  if (live) {
+    for (int e = lane; e < T * T; e += 64) {  // dA[i][j] = sum_d dctx[i][d] V[j][d]
+      const int i = e / T, j = e - i * T;
+      float acc = 0.f;
+      for (int d = 0; d < dv; ++d) acc = fmaf(dCs[i * dvp + d], Vs[j * dvp + d], acc);
+      dAs[e] = acc;
+    }
+    for (int e = lane; e < T * dv; e += 64) {  // dV[j][d] = sum_i A[i][j] dctx[i][d]
+      const int j = e / dv, d = e - j * dv;
+      float acc = 0.f;
+      for (int i = 0; i < T; ++i) acc = fmaf(As[i * T + j], dCs[i * dvp + d], acc);
+      dbase[(int64_t)j * ld + 2 * a.h * dk + hd * dv + d] = acc;
+    }
+  }
+  __syncthreads();
+  if (live) {  // column softmax backward: dS = A (dA - sum_i A dA) + d re_At
+    const int j = lane & 15, part = lane >> 4;
+    float c = 0.f;
+    if (j < T)
+      for (int i = part; i < T; i += 4) c = fmaf(As[i * T + j], dAs[i * T + j], c);
+    c = xor_sum_1632(c);
+    if (j < T)
+      for (int i = part; i < T; i += 4) {
+        float v = As[i * T + j] * (dAs[i * T + j] - c);
+        if (a.dre) v += a.dre[sbase + i * T + j];
+        dAs[i * T + j] = v;
+      }
+  }
+  __syncthreads();
+  if (live) {
+    for (int e = lane; e < T * T; e += 64) a.dscore[sbase + e] = dAs[e];
+    for (int e = lane; e < T * dk; e += 64) {
+      const int i = e / dk, d = e - i * dk;
+      float sq = 0.f, sk = 0.f;
+      for (int j = 0; j < T; ++j) {
+        sq = fmaf(dAs[i * T + j], Ks[j * dkp + d], sq);
+        sk = fmaf(dAs[j * T + i], Qs[j * dkp + d], sk);
+      }
+      dbase[(int64_t)i * ld + hd * dk + d] = sq * a.scale;
+      dbase[(int64_t)i * ld + a.h * dk + hd * dk + d] = sk * a.scale;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void tat_fwd_kernel(TatArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int T = a.T, dk = a.dk, dv = a.dv;
@@ -849,6 +1019,13 @@ int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
   a.B = B; a.F = F; a.T = T; a.h = h; a.dk = dk; a.dv = dv;
   a.qkv = qkv; a.res = res; a.res_mode = res ? res_mode : 0; a.scale = 1.f / sqrtf((float)dk);
   a.re_at = re_at; a.att = att; a.ctx = ctx;
+  const int P = B * F * h;
+  if (T <= 16 && (size_t)kTatW * tat_wave_fwd_floats(T, dk, dv) * sizeof(float) <= 64 * 1024) {
+    hipLaunchKernelGGL(tat_fwd_wave_kernel, dim3((unsigned)cdiv64(P, kTatW)), dim3(64 * kTatW),
+                       (size_t)kTatW * tat_wave_fwd_floats(T, dk, dv) * sizeof(float), st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   size_t lds = tat_fwd_lds(T, dk, dv);
   if (lds > 160 * 1024) { set_last_error("tat_fwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
   if (lds > 64 * 1024) DS_TRY(allow_lds((const void*)tat_fwd_kernel, lds));
@@ -863,6 +1040,13 @@ int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
   a.B = B; a.F = F; a.T = T; a.h = h; a.dk = dk; a.dv = dv;
   a.qkv = qkv; a.att = const_cast<float*>(att); a.scale = 1.f / sqrtf((float)dk);
   a.dctx = dctx; a.dre = dre; a.dqkv = dqkv; a.dscore = dscore;
+  const int P = B * F * h;
+  if (T <= 16 && (size_t)kTatW * tat_wave_bwd_floats(T, dk, dv) * sizeof(float) <= 64 * 1024) {
+    hipLaunchKernelGGL(tat_bwd_wave_kernel, dim3((unsigned)cdiv64(P, kTatW)), dim3(64 * kTatW),
+                       (size_t)kTatW * tat_wave_bwd_floats(T, dk, dv) * sizeof(float), st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   size_t lds = tat_bwd_lds(T, dk, dv);
   if (lds > 160 * 1024) {  // long series: A-only LDS variant
     lds = tat_bwd_lowmem_lds(T, dk, dv);
