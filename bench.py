@@ -194,10 +194,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DSTAGNN_DIST_BACKEND=gloo + DSTAGNN_DEVICE_MOD=1 rehearse the multi-rank path on a single
+    # GPU (ranks share cuda:0; RCCL refuses two ranks on one device) — test use only
+    backend = os.environ.get("DSTAGNN_DIST_BACKEND", "nccl")
+    local = local % int(os.environ.get("DSTAGNN_DEVICE_MOD", "1000000"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     from dstagnn_drought_amd import _lib

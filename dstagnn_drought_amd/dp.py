@@ -28,10 +28,15 @@ def shard_batch(t, rank, world):
 class GradAllReducer:
     """Bucketed mean all-reduce of parameter gradients with sparse mask payloads."""
 
-    def __init__(self, named_params, mask_support=None, bucket_bytes=32 << 20, group=None):
+    def __init__(self, named_params, mask_support=None, bucket_bytes=32 << 20, group=None,
+                 dense_limit=256 << 20):
         """named_params: iterable of (name, Parameter).  mask_support: dict name -> bool (N,N)
-        tensor (adj_pa > 0) for cheb mask params whose grads are supported there only."""
+        tensor (adj_pa > 0) for cheb mask params whose grads are supported there only.
+        dense_limit: a block's flat gradient buffer up to this size is all-reduced whole
+        (mask grads included, dense); larger ones (N = 4096: the masks are 1.3 GB) go through
+        the bucketed path that sends the masks as their support only."""
         self.group = group
+        self.dense_limit = dense_limit
         self.items = []  # (param, index or None)
         sup = mask_support or {}
         for n, p in named_params:
@@ -45,9 +50,33 @@ class GradAllReducer:
         g = p.grad.reshape(-1)
         return g if idx is None else g.index_select(0, idx)
 
+    def _flat_groups(self, live):
+        """Gradients that exactly tile one flat base tensor (the HIP block's backward packs a
+        block's parameter gradients back to back into one buffer): reduce the base itself —
+        one collective and one scale, no pack / unpack kernels."""
+        by_base = {}
+        for it in live:
+            g = it[1].grad
+            b = g._base
+            if b is None or not b.is_contiguous() or not g.is_contiguous():
+                continue
+            by_base.setdefault(id(b), (b, []))[1].append(it)
+        groups, taken = [], set()
+        for b, its in by_base.values():
+            if sum(it[1].grad.numel() for it in its) != b.numel() or b.numel() * 4 > self.dense_limit:
+                continue
+            groups.append(b)
+            taken.update(id(it[1]) for it in its)
+        return groups, taken
+
     def all_reduce(self):
         world = dist.get_world_size(self.group)
         live = [(n, p, idx) for n, p, idx in self.items if p.grad is not None]
+        bases, taken = self._flat_groups(live)
+        for b in bases:
+            dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group)
+            b.div_(world)
+        live = [it for it in live if id(it[1]) not in taken]
         buckets, cur, size = [], [], 0
         for it in live:
             k = it[1].numel() if it[2] is None else it[2].numel()
@@ -73,7 +102,7 @@ class GradAllReducer:
                     g.zero_()
                     g.index_copy_(0, idx, flat[off:off + k])
                 off += k
-        return len(buckets)
+        return len(buckets) + len(bases)
 
     def payload_bytes(self):
         return 4 * sum((p.numel() if idx is None else idx.numel()) for _, p, idx in self.items)

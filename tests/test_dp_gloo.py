@@ -103,3 +103,44 @@ def test_shard_batch_partitions():
     t = torch.arange(10)
     parts = [shard_batch(t, r, 3) for r in range(3)]
     assert torch.equal(torch.cat(parts), t)
+
+
+def _flat_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dstagnn_drought_amd.dp import GradAllReducer
+        shapes = [(4, 3), (5,), (2, 2, 2)]
+        params = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+        extra = torch.nn.Parameter(torch.zeros(7))  # a separate gradient: bucketed path
+        flat = torch.arange(25, dtype=torch.float32) * (rank + 1)
+        for p, g in zip(params, torch._utils._unflatten_dense_tensors(flat, params)):
+            p.grad = g
+        extra.grad = torch.full((7,), float(rank + 1))
+        named = [(f"p{i}", p) for i, p in enumerate(params)] + [("extra", extra)]
+        red = GradAllReducer(named)
+        n = red.all_reduce()
+        mean = sum(r + 1 for r in range(world)) / world
+        ok = torch.allclose(flat, torch.arange(25, dtype=torch.float32) * mean) and \
+            torch.allclose(extra.grad, torch.full((7,), mean)) and params[0].grad.data_ptr() == flat.data_ptr()
+        q.put((rank, n, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flat_gradient_buffer_reduced_in_place():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flat_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for rank, n, ok in res:
+        assert ok, rank
+        assert n == 2  # one flat collective + one bucket
