@@ -6,6 +6,7 @@ launched on torch's current HIP stream.  PyTorch only provides the device
 memory (caching allocator) and the stream.
 """
 import ctypes
+import os
 
 import torch
 
@@ -84,14 +85,18 @@ def graph_struct(graph):
 
 
 def use_sparse(graph, meta, T):
-    """Sparse Chebyshev aggregation when the union support is <= 1/4 dense and C*T <= 1024."""
+    """Sparse Chebyshev aggregation when the union support is <= 1/4 dense (rows of any length:
+    the kernels walk C*T in 1024-element chunks)."""
     if graph.get("csc_row") is None:
         return False
     N = graph["adj_pa"].shape[0]
-    return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= 1024
+    return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= (1 << 20)
 
 
 _SIZES = {}
+# DSTAGNN_POISON=1: every buffer the library writes starts as NaN (a read of memory the
+# kernels never wrote shows up as NaN instead of as whatever the allocator handed back)
+_POISON = os.environ.get("DSTAGNN_POISON", "0") == "1"
 
 
 def workspace_sizes(dims):
@@ -166,6 +171,9 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
         out = torch.empty(B, N, meta["C"], T, dtype=torch.float32, device=dev)
         re_at = torch.empty(B, F, meta["n_heads"], T, T, dtype=torch.float32, device=dev)
+        if _POISON:
+            for t in (save, scratch, out, re_at):
+                t.fill_(0xFF)  # all-ones bytes = NaN floats
         p = _params_struct(names, params)
         g = _graph_struct_cached(graph)
         rc = lib.dstagnn_block_forward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
@@ -205,6 +213,9 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         d_ra = torch.empty_like(ra) if mode != _lib.RES_NONE else None
         sv, sc = ctx.sizes
         scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
+        if _POISON:
+            for t in (scratch, flat, d_x) + ((d_ra,) if d_ra is not None else ()):
+                t.fill_(float("nan") if t.is_floating_point() else 0xFF)
         rc = lib.dstagnn_block_backward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
                                         _lib.ptr(ra if mode != _lib.RES_NONE else None), _lib.ptr(d_out),
                                         _lib.ptr(d_re_at), _lib.ptr(d_x), _lib.ptr(d_ra), ctypes.byref(gs),

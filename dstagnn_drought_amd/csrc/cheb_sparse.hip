@@ -21,18 +21,22 @@
 
 namespace {
 
-constexpr int kMaxNQ = 16;  // C*T <= 64*16 = 1024 (host checks; larger C*T uses the dense path)
+constexpr int kMaxNQ = 16;  // a wave covers 64*16 = 1024 elements of a row per pass
+constexpr int kChunk = 64 * kMaxNQ;
+// Rows longer than 1024 (C*T: GAMBIA 32 x 144 = 4608) are cut into 1024-element chunks:
+// grid.y = chunk for the two SpMMs (independent outputs), a loop over chunks inside the
+// SDDMM (its dot product spans the whole row).
 
 // Lanes past C*T read a clamped (valid) address and are never stored / are zeroed in
 // the one operand loaded outside the hot loop: no predicated loads in the inner loops.
 
 // per-lane offsets of elements e = lane + 64 q (clamped to the last one) in a node's xth block
 template <int kNQ>
-__device__ __forceinline__ void xth_offsets(const ChebSp& a, int lane, int (&xo)[kNQ]) {
+__device__ __forceinline__ void xth_offsets(const ChebSp& a, int e0, int lane, int (&xo)[kNQ]) {
   const int skip = (a.K - 1) * a.C;
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) {
-    const int e = min(lane + 64 * q, a.CT - 1);
+    const int e = min(e0 + lane + 64 * q, a.CT - 1);
     xo[q] = e + (e / a.C) * skip;
   }
 }
@@ -43,12 +47,13 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), j = (int)(wv % a.N);
+  const int e0 = blockIdx.y * kChunk;
   const int64_t NN = (int64_t)a.N * a.N;
   float acc[kNQ];
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) acc[q] = 0.f;
   int xo[kNQ];
-  xth_offsets<kNQ>(a, lane, xo);
+  xth_offsets<kNQ>(a, e0, lane, xo);
   const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csc_ptr[j], p1 = a.csc_ptr[j + 1];
   for (int k = 0; k < a.K; ++k) {
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   float* orow = a.out + ((int64_t)b * a.N + j) * a.CT;
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) {
-    const int e = lane + 64 * q;
+    const int e = e0 + lane + 64 * q;
     if (e < a.CT) orow[e] = fmaxf(acc[q], 0.f);
   }
 }
@@ -78,25 +83,47 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), j = (int)(wv % a.N);
   const int64_t NN = (int64_t)a.N * a.N;
-  float g[kNQ];
   const float* grow = a.g + ((int64_t)b * a.N + j) * a.CT;
-#pragma unroll
-  for (int q = 0; q < kNQ; ++q) {
-    const int e = lane + 64 * q;
-    g[q] = e < a.CT ? grow[e] : 0.f;
-  }
-  int xo[kNQ];
-  xth_offsets<kNQ>(a, lane, xo);
   const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csc_ptr[j], p1 = a.csc_ptr[j + 1];
-  for (int k = 0; k < a.K; ++k) {
+  if (a.CT <= kChunk) {  // one pass: the row of g stays in registers
+    float g[kNQ];
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q) {
+      const int e = lane + 64 * q;
+      g[q] = e < a.CT ? grow[e] : 0.f;
+    }
+    int xo[kNQ];
+    xth_offsets<kNQ>(a, 0, lane, xo);
+    for (int k = 0; k < a.K; ++k) {
+      float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
+      for (int p = p0; p < p1; ++p) {
+        const int i = a.csc_row[p];
+        const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], xr[xo[q]], s);
+        s = wave_sum(s);
+        if (lane == 0) dWk[(int64_t)i * a.N + j] = s;
+      }
+    }
+    return;
+  }
+  for (int k = 0; k < a.K; ++k) {  // long rows: the dot product walks the chunks
     float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
     for (int p = p0; p < p1; ++p) {
       const int i = a.csc_row[p];
       const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
       float s = 0.f;
+      for (int e0 = 0; e0 < a.CT; e0 += kChunk) {
+        int xo[kNQ];
+        xth_offsets<kNQ>(a, e0, lane, xo);
 #pragma unroll
-      for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], xr[xo[q]], s);
+        for (int q = 0; q < kNQ; ++q) {
+          const int e = e0 + lane + 64 * q;
+          s = fmaf(e < a.CT ? grow[e] : 0.f, xr[xo[q]], s);
+        }
+      }
       s = wave_sum(s);
       if (lane == 0) dWk[(int64_t)i * a.N + j] = s;
     }
@@ -109,9 +136,10 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
   const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), i = (int)(wv % a.N);
+  const int e0 = blockIdx.y * kChunk;
   const int64_t NN = (int64_t)a.N * a.N;
   int xo[kNQ];
-  xth_offsets<kNQ>(a, lane, xo);
+  xth_offsets<kNQ>(a, e0, lane, xo);
   const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csr_ptr[i], p1 = a.csr_ptr[i + 1];
   for (int k = 0; k < a.K; ++k) {
@@ -126,12 +154,12 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
       const float w = Tk[o] * Pk[o];
       const float* gr = a.g + ((int64_t)b * a.N + j) * a.CT;
 #pragma unroll
-      for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, gr[min(lane + 64 * q, a.CT - 1)], acc[q]);
+      for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, gr[min(e0 + lane + 64 * q, a.CT - 1)], acc[q]);
     }
     float* dr = a.dxth + ((int64_t)b * a.N + i) * KCT + k * a.C;
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
-      const int e = lane + 64 * q;
+      const int e = e0 + lane + 64 * q;
       if (e < a.CT) dr[xo[q]] = acc[q];
     }
   }
@@ -139,13 +167,14 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
 
 }  // namespace
 
-bool cheb_sparse_ok(int CT) { return CT > 0 && CT <= 64 * kMaxNQ; }
+bool cheb_sparse_ok(int CT) { return CT > 0 && CT <= (1 << 20); }
 
 namespace {
-#define DS_NQ_DISPATCH(KER, a, st)                                                                 \
+#define DS_NQ_DISPATCH(KER, a, st, CHUNKED)                                                        \
   do {                                                                                             \
-    const int nq = (int)cdiv64((a).CT, 64);                                                        \
-    const dim3 grid((unsigned)cdiv64((int64_t)(a).B * (a).N, 4));                                 \
+    const int nq = (int)cdiv64(std::min((a).CT, kChunk), 64);                                      \
+    const dim3 grid((unsigned)cdiv64((int64_t)(a).B * (a).N, 4),                                   \
+                    (CHUNKED) ? (unsigned)cdiv64((a).CT, kChunk) : 1u);                            \
     if (nq <= 1) hipLaunchKernelGGL(KER<1>, grid, dim3(256), 0, st, a);                            \
     else if (nq <= 2) hipLaunchKernelGGL(KER<2>, grid, dim3(256), 0, st, a);                       \
     else if (nq <= 3) hipLaunchKernelGGL(KER<3>, grid, dim3(256), 0, st, a);                       \
@@ -154,22 +183,22 @@ namespace {
     else if (nq <= 8) hipLaunchKernelGGL(KER<8>, grid, dim3(256), 0, st, a);                       \
     else if (nq <= 12) hipLaunchKernelGGL(KER<12>, grid, dim3(256), 0, st, a);                     \
     else if (nq <= 16) hipLaunchKernelGGL(KER<16>, grid, dim3(256), 0, st, a);                     \
-    else { set_last_error("cheb sparse: C*T > 1024"); return DSTAGNN_E_SHAPE; }                    \
+    else { set_last_error("cheb sparse: bad row length"); return DSTAGNN_E_SHAPE; }               \
   } while (0)
 }  // namespace
 
 int op_cheb_spmm_fwd(const ChebSp& a, hipStream_t st) {
-  DS_NQ_DISPATCH(cheb_spmm_fwd_kernel, a, st);
+  DS_NQ_DISPATCH(cheb_spmm_fwd_kernel, a, st, true);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_cheb_sddmm_bwd(const ChebSp& a, hipStream_t st) {
-  DS_NQ_DISPATCH(cheb_sddmm_bwd_kernel, a, st);
+  DS_NQ_DISPATCH(cheb_sddmm_bwd_kernel, a, st, false);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_cheb_spmm_t_bwd(const ChebSp& a, hipStream_t st) {
-  DS_NQ_DISPATCH(cheb_spmm_t_bwd_kernel, a, st);
+  DS_NQ_DISPATCH(cheb_spmm_t_bwd_kernel, a, st, true);
   DS_CHECK_LAUNCH();
   return 0;
 }

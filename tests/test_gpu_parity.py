@@ -217,6 +217,24 @@ def test_model_golden(golden_dir):
 # ---------------------------------------------------------------------------------------
 # larger shapes vs the CPU oracle (PEMS08 geometry, small batch)
 # ---------------------------------------------------------------------------------------
+def _scaled_laplacian_fixed_start(W):
+    """scaled_Laplacian (lib/utils.py:149-177) with a run-independent lambda_max.  ARPACK's
+    default start vector comes from its own RNG, whose state persists across calls, and on
+    these non-symmetric L its "LR" answer depends on the start (GAMBIA: 3.392-0.212j vs the
+    true 3.4115), so lambda_max (hence T_k) would depend on which tests ran before; at GAMBIA size a
+    1e-3 change in T_k moves a pre-ReLU Chebyshev output across 0 and flips one grad_x entry
+    by O(1) between an fp32 and an fp64 evaluation.  A fixed start makes each case the same
+    case in every run."""
+    from scipy.sparse.linalg import eigs
+    Lap = np.diag(W.sum(axis=1)) - W
+    if W.shape[0] <= 2500:  # exact: ARPACK's "LR" pick on these non-symmetric L is start-dependent
+        ev = np.linalg.eigvals(Lap)
+        lam = ev[np.argmax(ev.real)].real
+    else:
+        lam = eigs(Lap, k=1, which="LR", v0=np.random.RandomState(0).rand(W.shape[0]))[0].real
+    return (2.0 * Lap) / lam - np.eye(W.shape[0])
+
+
 def _oracle_case(B, N, T, K, h, D, dk, C, first, res_kind, seed, train=False):
     from oracle import dstagnn_ref as ref
     import dstagnn_drought_amd as D_
@@ -227,7 +245,7 @@ def _oracle_case(B, N, T, K, h, D, dk, C, first, res_kind, seed, train=False):
     for i in range(N):
         tmd[i, rs.choice(N, 2, replace=False)] = 1.0
         pa[i, rs.choice(N, 4, replace=False)] = 1.0
-    Lt = D_.scaled_Laplacian(tmd)
+    Lt = _scaled_laplacian_fixed_start(tmd)
     cheb = [torch.from_numpy(c).float() for c in D_.cheb_polynomial(Lt, K)][:K]
     F = 1 if first else C
     p = ref.random_block_params(gen, F, F, K, C, N, T, D, dk, dk, h)
@@ -309,7 +327,7 @@ CONFIGS = {
     # name: (N, T, K, h, D, dk, C)
     "pems04": (307, 12, 3, 3, 512, 32, 32),
     "pems07": (883, 12, 3, 4, 512, 32, 32),
-    "gambia": (2139, 144, 2, 2, 64, 32, 32),   # long series: dense Chebyshev path (C*T > 1024)
+    "gambia": (2139, 144, 2, 2, 64, 32, 32),   # long series: sparse Chebyshev rows in 1024-element chunks
     "syn": (4096, 24, 5, 8, 512, 32, 32),
 }
 
