@@ -121,7 +121,7 @@ struct Scratch {
   // per-stage so the side stream's reductions never race a later main-chain write)
   float *gemm_ws_side, *part_side, *dWqkv, *dWqk;
   float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dconv[3], *dW, *dxth,
-      *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dE, *dctx, *dqkv, *dscore, *du_et;
+      *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dE, *dctx, *dqkv, *dscore, *du_et, *dGt;
 };
 
 Scratch plan_scratch(const Dims& m, Arena& a) {
@@ -157,6 +157,7 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.dqkv = a.take(m.BFT * m.QW);
   s.dscore = a.take(m.BFT * m.h * m.T);
   s.du_et = m.first ? a.take((int64_t)m.B * m.T * m.N) : nullptr;
+  s.dGt = gtu_tail_bwd_split(m.C, m.T) ? a.take(m.BN * m.C * m.S) : nullptr;  // long series only
   return s;
 }
 
@@ -690,7 +691,7 @@ struct Bwd {
     if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
     t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c;
     t.dout = dout; t.gcontrib = w.gcon_t; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
-    t.rcontrib = w.bcon_t; t.dres = w.dres_t;
+    t.rcontrib = w.bcon_t; t.dres = w.dres_t; t.dG = w.dGt;
     DS_TRY(op_gtu_tail_bwd(t, st));
     // --- side: LN / residual / fcmy / GTU parameter gradients (one fork)
     DS_TRY(fork());

@@ -11,6 +11,14 @@
 // the gates' backward into the zero-padded (t', o) rows the transposed-convolution GEMMs
 // read.  Replaces gate_fwd + fcmy GEMM + tail_fwd (3 launches, 2 HBM round trips of G and
 // tc) and tail_bwd + dG GEMM + gate_bwd.
+//
+// Long series (GAMBIA T=144: S = 420, the fcmy weight is 242 KB and a node's G tile 54 KB)
+// do not fit that mould: one wave per node would run the 2*C*T*S = 3.9 MFLOP fcmy product
+// per node as scalar FMAs out of cache (measured 0.37 TFLOP/s, 93 % of the step).  There
+// the tail splits around the product (PH template argument): gates -> G (PH 1), the fcmy
+// product as one MFMA GEMM over all B*N*C rows (bias in its epilogue, written into tco),
+// residual / ReLUs / LayerNorm reading it back (PH 2); backward: LN / residual -> dtc
+// (PH 1), dG = dtc W as one GEMM, gates backward reading dG (PH 2).
 #include "common.hpp"
 #include "ops.hpp"
 
@@ -52,10 +60,10 @@ constexpr int kU = 8;
 // LDS layout (floats), shared by the kernel and the host size computation
 struct TailFwdLds {
   int SP, CP, P, gs, rl, xs, red, mus, rss, wl, total;
-  __host__ __device__ TailFwdLds(int C, int T, bool stage_w) {
+  __host__ __device__ TailFwdLds(int C, int T, bool stage_w, bool has_g = true) {
     const int S = 3 * T - 12;
     SP = S + 1; CP = C + 1; P = T < kNT ? kNT / T : 1;
-    gs = 0; rl = gs + C * SP; xs = rl + C * T; red = xs + T * CP;
+    gs = 0; rl = gs + (has_g ? C * SP : 0); xs = rl + C * T; red = xs + T * CP;
     mus = red + (P * T > kNT ? P * T : kNT); rss = mus + T; wl = rss + T;
     total = wl + (stage_w ? T * SP : 0);
   }
@@ -79,11 +87,12 @@ __device__ __forceinline__ void col_sums_over_c(const float* v, int C, int T, in
   __syncthreads();
 }
 
-template <int KC, int KT, bool WL>
+// PH: 0 = fused, 1 = gates -> G only, 2 = from the GEMM's tc (in tco) to the output
+template <int KC, int KT, bool WL, int PH = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C, CS = C * S;
-  const TailFwdLds L(C, T, WL);
+  const TailFwdLds L(C, T, WL, PH != 2);
   const int SP = L.SP, CP = L.CP;
   float* Gs = lds + L.gs;    // [c][SP]
   float* rl = lds + L.rl;    // [c][t]
@@ -101,7 +110,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
     const int64_t base = bn * CT;
     // gates, element (s, c) with c fastest: coalesced conv-row reads
     #pragma unroll 1
-    for (int e0 = 0; e0 < CS; e0 += kNT * kU) {
+    for (int e0 = 0; e0 < (PH == 2 ? 0 : CS); e0 += kNT * kU) {
       float pv[kU], qv[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
@@ -126,28 +135,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
         }
       }
     }
-    if (!a.first)
+    if (!a.first && PH != 1)
       for (int e = tid; e < CT; e += kNT) Xs[(e / C) * CP + e % C] = a.X[base + e];  // X rows (t, c)
     __syncthreads();
-    for (int e = tid; e < CS; e += kNT) a.G[bn * CS + e] = Gs[(e / S) * SP + e % S];  // [c][s], coalesced
+    if (PH != 2)
+      for (int e = tid; e < CS; e += kNT) a.G[bn * CS + e] = Gs[(e / S) * SP + e % S];  // [c][s], coalesced
+    if (PH == 1) {
+      __syncthreads();  // LDS reuse by the next node
+      continue;
+    }
     // fcmy + dropout + residual + ReLUs; element e = (c, t) of the (C, T) output
     #pragma unroll 1
     for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
-      float xv[kU];
+      float xv[kU], tcv[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = min(e0 + tid + kNT * u, CT - 1);
         xv[u] = a.first ? a.x[bn * T + e % T] : a.x[base + e];
+        if (PH == 2) tcv[u] = a.tco[base + e];  // fcmy output (bias included) from the GEMM
       }
 #pragma unroll 1
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + tid + kNT * u;
         if (e >= CT) continue;
         const int c = e / T, t = e - c * T;
-        float tc = a.fcmy_b[t];
-        const float* gr = Gs + c * SP;
-        const float* wr = Ws + t * WS;
-        for (int sidx = 0; sidx < S; ++sidx) tc = fmaf(gr[sidx], wr[sidx], tc);
+        float tc;
+        if (PH == 2) {
+          tc = tcv[u];
+        } else {
+          tc = a.fcmy_b[t];
+          const float* gr = Gs + c * SP;
+          const float* wr = Ws + t * WS;
+          for (int sidx = 0; sidx < S; ++sidx) tc = fmaf(gr[sidx], wr[sidx], tc);
+        }
         if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
         float tco, xres;
         if (a.first) {
@@ -196,11 +216,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
 // dG, the dX tile and the LN reduction scratch share one region (disjoint phases)
 struct TailBwdLds {
   int SP, CP, P, dxh, xhl, rr, dg, dxs, red, s1, s2, wl, total;
-  __host__ __device__ TailBwdLds(int C, int T, bool stage_w) {
+  __host__ __device__ TailBwdLds(int C, int T, bool stage_w, bool has_g = true) {
     const int S = 3 * T - 12, CT = C * T;
     SP = S + 1; CP = C + 1; P = T < kNT ? kNT / T : 1;
     const int nred = 2 * (P * T > kNT ? P * T : kNT);
-    int shared = C * SP;
+    int shared = has_g ? C * SP : 0;
     if (T * CP > shared) shared = T * CP;
     if (nred > shared) shared = nred;
     dxh = 0; xhl = dxh + CT; rr = xhl + CT; dg = rr + CT; dxs = dg; red = dg; s1 = dg + shared; s2 = s1 + T; wl = s2 + T;
@@ -208,11 +228,12 @@ struct TailBwdLds {
   }
 };
 
-template <int KC, int KT, bool WL>
+// PH: 0 = fused, 1 = LN / residual backward to dtc only, 2 = gates backward from a.dG
+template <int KC, int KT, bool WL, int PH = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
-  const TailBwdLds L(C, T, WL);
+  const TailBwdLds L(C, T, WL, PH == 0);
   const int SP = L.SP, CP = L.CP;
   float* dxh = lds + L.dxh;   // CT  (LN dxhat, then dtc)
   float* xhl = lds + L.xhl;   // CT
@@ -231,6 +252,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const int64_t base = bn * CT;
     const float* mu = a.mu + bn * T;
     const float* rsv = a.rs + bn * T;
+    if (PH != 2) {
     // LayerNorm over C backward
     #pragma unroll 1
     for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
@@ -317,15 +339,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         a.dx[bn * T + t] = sum;
       }
     }
+    if (PH == 1) {
+      __syncthreads();  // LDS reuse by the next node
+      continue;
+    }
     // fcmy backward: dG[c, s] = sum_t dtc[c, t] W[t, s]
     #pragma unroll 1
-    for (int e = tid; e < C * S; e += kNT) {
+    for (int e = tid; e < (PH == 0 ? C * S : 0); e += kNT) {
       const int c = e / S, s = e - c * S;
       float g = 0.f;
       for (int t = 0; t < T; ++t) g = fmaf(dxh[c * T + t], Ws[t * S + s], g);
       dGs[c * SP + s] = g;
     }
     __syncthreads();
+    }  // PH != 2
+    const float* dGg = a.dG + bn * (int64_t)C * S;  // PH 2: dG rows [c][s] from the GEMM
     // gates backward into the zero-padded (t', o) rows of each GTU
 #pragma unroll 1
     for (int gi = 0; gi < 3; ++gi) {
@@ -338,7 +366,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
       #pragma unroll 1
       for (int e0 = 0; e0 < E; e0 += kNT * kU) {
-        float pv[kU], qv[kU];
+        float pv[kU], qv[kU], dgv[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           const int e = min(e0 + tid + kNT * u, E - 1);
@@ -347,6 +375,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
           const int c = o < C ? o : o - C;
           pv[u] = cv[t * C2 + c];
           qv[u] = cv[t * C2 + C + c];
+          if (PH == 2) dgv[u] = dGg[c * S + off + t];
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -357,7 +386,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
           float v = 0.f;
           if (t >= 0 && t < Tg) {
             const int c = o < C ? o : o - C;
-            const float dg = dGs[c * SP + off + t];
+            const float dg = PH == 2 ? dgv[u] : dGs[c * SP + off + t];
             const float th = fast_tanh(pv[u]), sg = fast_sigmoid(qv[u]);
             v = o < C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
           }
@@ -369,8 +398,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   }
 }
 
-size_t fwd_lds(const GtuTailArgs& a, bool wl) { return sizeof(float) * (size_t)TailFwdLds(a.C, a.T, wl).total; }
-size_t bwd_lds(const GtuTailArgs& a, bool wl) { return sizeof(float) * (size_t)TailBwdLds(a.C, a.T, wl).total; }
+size_t fwd_lds(const GtuTailArgs& a, bool wl, bool has_g = true) {
+  return sizeof(float) * (size_t)TailFwdLds(a.C, a.T, wl, has_g).total;
+}
+size_t bwd_lds(const GtuTailArgs& a, bool wl, bool has_g = true) {
+  return sizeof(float) * (size_t)TailBwdLds(a.C, a.T, wl, has_g).total;
+}
 
 unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 65536); }
 
@@ -387,23 +420,57 @@ int launch_node_kernel(K kernel, size_t lds, const GtuTailArgs& a, hipStream_t s
   return 0;
 }
 
+// rows [r0, r0+M) of C[r, n] = sum_k A[r, k] B[k, n] (+ bias[n]); row chunks keep every
+// operand offset inside the GEMM's int32 index range
+int rows_gemm(const float* A, int lda, const float* B, Idx2 bk, Idx2 bn, float* Cm, int ldc, int64_t M, int N,
+              int K, const float* bias, hipStream_t st) {
+  const int64_t chunk = std::max<int64_t>(64, ((int64_t)1 << 28) / std::max(lda, ldc)) / 64 * 64;
+  for (int64_t r0 = 0; r0 < M; r0 += chunk) {
+    Gemm g;
+    g.M = (int)std::min(chunk, M - r0); g.N = N; g.K = K;
+    g.A = A + r0 * lda; g.am = idx1(lda); g.ak = idx1(1);
+    g.B = B; g.bk = bk; g.bn = bn;
+    g.C = Cm + r0 * ldc; g.cm = idx1(ldc); g.cn = idx1(1);
+    g.bias = bias;
+    DS_TRY(run_gemm(g, nullptr, 0, st));
+  }
+  return 0;
+}
+
 }  // namespace
+
+bool gtu_tail_bwd_split(int C, int T) {
+  GtuTailArgs a;
+  a.C = C; a.T = T;
+  return bwd_lds(a, true) > 32 * 1024;
+}
 
 int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
   const bool wl = fwd_lds(a, true) <= 32 * 1024;
-  const size_t lds = fwd_lds(a, wl);
-  if (lds > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-  if (a.C == 32 && a.T == 12 && wl) return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true>, lds, a, st);
-  if (wl) return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, true>, lds, a, st);
-  return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false>, lds, a, st);
+  if (!wl) {  // long series: gates | fcmy GEMM | tail
+    const int S = 3 * a.T - 12;
+    if (fwd_lds(a, false, true) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
+    DS_TRY(launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 1>, fwd_lds(a, false, true), a, st));
+    DS_TRY(rows_gemm(a.G, S, a.fcmy_w, idx1(1), idx1(S), a.tco, a.T, a.BN * a.C, a.T, S, a.fcmy_b, st));
+    return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2>, fwd_lds(a, false, false), a, st);
+  }
+  const size_t lds = fwd_lds(a, true);
+  if (a.C == 32 && a.T == 12) return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true>, lds, a, st);
+  return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, true>, lds, a, st);
 }
 
 int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
   const bool wl = bwd_lds(a, true) <= 32 * 1024;
-  const size_t lds = bwd_lds(a, wl);
-  if (lds > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
   static const bool generic = getenv("DSTAGNN_TAIL_GENERIC") && atoi(getenv("DSTAGNN_TAIL_GENERIC")) != 0;
-  if (a.C == 32 && a.T == 12 && wl && !generic) return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
-  if (wl) return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, true>, lds, a, st);
-  return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false>, lds, a, st);
+  if (!wl) {  // long series: LN / residual | dG GEMM | gates
+    if (!a.dG) { set_last_error("gtu_tail: split backward needs the dG scratch"); return DSTAGNN_E_ARG; }
+    const int S = 3 * a.T - 12;
+    if (bwd_lds(a, false, false) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
+    DS_TRY(launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false, 1>, bwd_lds(a, false, false), a, st));
+    DS_TRY(rows_gemm(a.dtc, a.T, a.fcmy_w, idx1(S), idx1(1), a.dG, S, a.BN * a.C, S, a.T, nullptr, st));
+    return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false, 2>, 0, a, st);
+  }
+  const size_t lds = bwd_lds(a, true);
+  if (a.C == 32 && a.T == 12 && !generic) return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
+  return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, true>, lds, a, st);
 }

@@ -105,6 +105,7 @@ struct GtuTailArgs {
   float* dx = nullptr;            // d block input
   float* rcontrib = nullptr; float* dres = nullptr;  // first block residual_conv grads
   float* dconv_pad[3] = {};       // [bn][T+ks-1][2C]
+  float* dG = nullptr;            // [bn][C][3T-12] scratch of the split (long-series) backward
 };
 
 
@@ -158,5 +159,7 @@ int op_cheb_mask_grad(const ChebSm& a, hipStream_t st);
 int op_pack_rows(const PackRows& a, hipStream_t st);
 int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st);
 int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st);
+// true when the backward runs split (LN | dG GEMM | gates) and needs GtuTailArgs::dG
+bool gtu_tail_bwd_split(int C, int T);
 int op_param_prep(const ParamPrep& a, hipStream_t st);
 int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st);
