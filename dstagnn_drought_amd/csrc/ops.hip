@@ -767,24 +767,36 @@ __global__ __launch_bounds__(256) void relu_mask_kernel(const float* __restrict_
 
 // =====================================================================================
 // Chebyshev spatial-attention softmax (column softmax over source node i)
-// grid (ceil(N/64), B*K), block 256 = 64 columns x 4 row groups
+// grid ceil(N/64)*B*K (see sm_tile), block 512 = 64 columns x 8 row groups
 // =====================================================================================
 constexpr int kSmG = 8;  // row groups per workgroup (64 columns x 8 groups = 512 threads)
+
+// workgroup -> (column group, b, k) with b fastest: the B workgroups that share one
+// (k, column group) tile of A_pa, M_k and T_k are dispatched together (round-robin over the
+// XCDs, B/8 per XCD), so those tiles come from L2 instead of HBM once per batch element
+__device__ __forceinline__ void sm_tile(const ChebSm& a, int* b, int* k, int* cg) {
+  const int ncg = (a.N + 63) / 64;
+  int id = blockIdx.x;
+  *b = id % a.B; id /= a.B;
+  *cg = id % ncg;
+  *k = id / ncg;
+}
 
 __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
   __shared__ float sm_m[kSmG][64], sm_l[kSmG][64];
   const int N = a.N;
-  const int bk = blockIdx.y;
-  const int k = bk % a.K;
+  int b, k, cg;
+  sm_tile(a, &b, &k, &cg);
+  const int bk = b * a.K + k;
   const int cj = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + cj;
+  const int j = cg * 64 + cj;
   const float* S = a.S + (int64_t)bk * N * N;
   const float* Mk = a.mask[k];
   const float* Tk = a.cheb + (int64_t)k * N * N;
-  // pass 1: column max (4 independent chains, loads batched), pass 2: sum of exp
+  // one pass: online column max and sum of exp (4 independent chains, loads batched)
   float m = -INFINITY, l = 0.f;
   if (j < N) {
-    float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, l4[4] = {0.f, 0.f, 0.f, 0.f};
     int i = g;
     for (; i + 3 * kSmG < N; i += 4 * kSmG) {
       float z[4];
@@ -794,30 +806,22 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
         z[u] = S[o] + a.apa[o] * Mk[o];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) m4[u] = fmaxf(m4[u], z[u]);
+      for (int u = 0; u < 4; ++u) {
+        const float mn = fmaxf(m4[u], z[u]);
+        l4[u] = l4[u] * __expf(m4[u] - mn) + __expf(z[u] - mn);
+        m4[u] = mn;
+      }
     }
     for (; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
-      m4[0] = fmaxf(m4[0], S[o] + a.apa[o] * Mk[o]);
+      const float z = S[o] + a.apa[o] * Mk[o];
+      const float mn = fmaxf(m4[0], z);
+      l4[0] = l4[0] * __expf(m4[0] - mn) + __expf(z - mn);
+      m4[0] = mn;
     }
     m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-    float l4[4] = {0.f, 0.f, 0.f, 0.f};
-    i = g;
-    for (; i + 3 * kSmG < N; i += 4 * kSmG) {
-      float z[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t o = (int64_t)(i + u * kSmG) * N + j;
-        z[u] = S[o] + a.apa[o] * Mk[o];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) l4[u] += __expf(z[u] - m);
-    }
-    for (; i < N; i += kSmG) {
-      const int64_t o = (int64_t)i * N + j;
-      l4[0] += __expf(S[o] + a.apa[o] * Mk[o] - m);
-    }
-    l = (l4[0] + l4[1]) + (l4[2] + l4[3]);
+    for (int u = 0; u < 4; ++u) l += m4[u] == -INFINITY ? 0.f : l4[u] * __expf(m4[u] - m);
   }
   sm_m[g][cj] = m; sm_l[g][cj] = l;
   __syncthreads();
@@ -826,7 +830,7 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
   for (int q = 1; q < kSmG; ++q) M = fmaxf(M, sm_m[q][cj]);
   float L = 0.f;
 #pragma unroll
-  for (int q = 0; q < kSmG; ++q) L += sm_l[q][cj] * __expf(sm_m[q][cj] - M);
+  for (int q = 0; q < kSmG; ++q) L += sm_m[q][cj] == -INFINITY ? 0.f : sm_l[q][cj] * __expf(sm_m[q][cj] - M);
   const float inv = 1.f / L;
   if (j < N) {
     float* P = a.P + (int64_t)bk * N * N;
@@ -846,10 +850,11 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
 __global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
   __shared__ float sm_c[kSmG][64];
   const int N = a.N;
-  const int bk = blockIdx.y;
-  const int k = bk % a.K;
+  int b, k, cg;
+  sm_tile(a, &b, &k, &cg);
+  const int bk = b * a.K + k;
   const int cj = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + cj;
+  const int j = cg * 64 + cj;
   const float* P = a.P + (int64_t)bk * N * N;
   const float* dW = a.dW + (int64_t)bk * N * N;
   const float* Tk = a.cheb + (int64_t)k * N * N;
@@ -898,9 +903,13 @@ __global__ __launch_bounds__(256) void cheb_mask_grad_kernel(ChebSm a) {
   const int k = blockIdx.y;
   float* out = a.dmask[k];
   for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < NN; o += (int64_t)gridDim.x * blockDim.x) {
+    const float w = a.apa[o];
     float s = 0.f;
-    for (int b = 0; b < a.B; ++b) s += a.dz[((int64_t)b * a.K + k) * NN + o];
-    out[o] = a.apa[o] * s;
+    if (w != 0.f) {  // dz is read only under the A_pa support (dM_k is 0 elsewhere)
+#pragma unroll 8
+      for (int b = 0; b < a.B; ++b) s += a.dz[((int64_t)b * a.K + k) * NN + o];
+    }
+    out[o] = w * s;
   }
 }
 
@@ -1162,13 +1171,13 @@ int op_relu_mask(const float* g, const float* y, float* out, int64_t n, hipStrea
 }
 
 int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st) {
-  dim3 grid((unsigned)cdiv64(a.N, 64), (unsigned)(a.B * a.K));
+  dim3 grid((unsigned)(cdiv64(a.N, 64) * a.B * a.K));
   hipLaunchKernelGGL(cheb_softmax_fwd_kernel, grid, dim3(64 * kSmG), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st) {
-  dim3 grid((unsigned)cdiv64(a.N, 64), (unsigned)(a.B * a.K));
+  dim3 grid((unsigned)(cdiv64(a.N, 64) * a.B * a.K));
   hipLaunchKernelGGL(cheb_softmax_bwd_kernel, grid, dim3(64 * kSmG), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
