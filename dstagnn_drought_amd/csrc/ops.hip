@@ -770,6 +770,7 @@ __global__ __launch_bounds__(256) void relu_mask_kernel(const float* __restrict_
 // grid ceil(N/64)*B*K (see sm_tile), block 512 = 64 columns x 8 row groups
 // =====================================================================================
 constexpr int kSmG = 8;  // row groups per workgroup (64 columns x 8 groups = 512 threads)
+constexpr int kSmCondN = 1024;  // N from which the softmax kernels load under the support only
 
 // workgroup -> (column group, b, k) with b fastest: the B workgroups that share one
 // (k, column group) tile of A_pa, M_k and T_k are dispatched together (round-robin over the
@@ -782,6 +783,10 @@ __device__ __forceinline__ void sm_tile(const ChebSm& a, int* b, int* k, int* cg
   *k = id / ncg;
 }
 
+// CL ("conditional loads"): read M_k (fwd) and P / dW (bwd) only under the A_pa / T_k
+// support.  Pays at large N (HBM-bound passes over N^2 tiles); at small N (PEMS08, 170) the
+// passes are latency chains and the dependent load costs more than the bytes it saves.
+template <bool CL>
 __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
   __shared__ float sm_m[kSmG][64], sm_l[kSmG][64];
   const int N = a.N;
@@ -799,11 +804,23 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
     float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, l4[4] = {0.f, 0.f, 0.f, 0.f};
     int i = g;
     for (; i + 3 * kSmG < N; i += 4 * kSmG) {
-      float z[4];
+      float z[4], w[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t o = (int64_t)(i + u * kSmG) * N + j;
-        z[u] = S[o] + a.apa[o] * Mk[o];
+        z[u] = S[o];
+        w[u] = a.apa[o];
+      }
+      float mv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) mv[u] = CL ? 0.f : Mk[(int64_t)(i + u * kSmG) * N + j];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // CL: M_k read only under the A_pa support
+        if (CL) {
+          if (w[u] != 0.f) z[u] += w[u] * Mk[(int64_t)(i + u * kSmG) * N + j];
+        } else {
+          z[u] += w[u] * mv[u];
+        }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -814,7 +831,8 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
     }
     for (; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
-      const float z = S[o] + a.apa[o] * Mk[o];
+      const float w = a.apa[o];
+      const float z = S[o] + (CL ? (w != 0.f ? w * Mk[o] : 0.f) : w * Mk[o]);
       const float mn = fmaxf(m4[0], z);
       l4[0] = l4[0] * __expf(m4[0] - mn) + __expf(z - mn);
       m4[0] = mn;
@@ -838,7 +856,8 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
 #pragma unroll 2
     for (int i = g; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
-      const float z = S[o] + a.apa[o] * Mk[o];
+      const float w = a.apa[o];
+      const float z = S[o] + (CL ? (w != 0.f ? w * Mk[o] : 0.f) : w * Mk[o]);
       const float p = __expf(z - M) * inv;
       P[o] = p;
       if (W) W[o] = Tk[o] * p;
@@ -847,6 +866,7 @@ __global__ __launch_bounds__(512) void cheb_softmax_fwd_kernel(ChebSm a) {
 }
 
 // dz = P * (T*dW - sum_i P*T*dW)   written to dz (may alias dW)
+template <bool CL>
 __global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
   __shared__ float sm_c[kSmG][64];
   const int N = a.N;
@@ -860,24 +880,34 @@ __global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
   const float* Tk = a.cheb + (int64_t)k * N * N;
   float c = 0.f;
   if (j < N) {
-    // dW is only defined where some T_k is non-zero (the sparse path writes the
-    // support only, no memset): select, so off-support garbage never propagates
+    // dW is only defined where T_k is non-zero (the sparse path writes the support only,
+    // no memset) and only needed there: T_k (shared by the batch, from L2) is read first and
+    // P / dW only under its support, so a sparse graph costs one dense pass over P, not
+    // three over P, T_k and dW.  Off-support garbage in dW never propagates.
     float c4[4] = {0.f, 0.f, 0.f, 0.f};
     int i = g;
     for (; i + 3 * kSmG < N; i += 4 * kSmG) {
-      float pv[4], tv[4], dv[4];
+      float tv[4], pv[4], dv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t o = (int64_t)(i + u * kSmG) * N + j;
-        pv[u] = P[o]; tv[u] = Tk[o]; dv[u] = dW[o];
+        tv[u] = Tk[o];
+        if (!CL) { pv[u] = P[o]; dv[u] = dW[o]; }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) c4[u] += pv[u] * (tv[u] != 0.f ? tv[u] * dv[u] : 0.f);
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = (int64_t)(i + u * kSmG) * N + j;
+        if (CL) {
+          if (tv[u] != 0.f) c4[u] += P[o] * (tv[u] * dW[o]);
+        } else {
+          c4[u] += pv[u] * (tv[u] != 0.f ? tv[u] * dv[u] : 0.f);
+        }
+      }
     }
     for (; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
       const float t = Tk[o];
-      c4[0] += P[o] * (t != 0.f ? t * dW[o] : 0.f);
+      if (t != 0.f) c4[0] += P[o] * (t * dW[o]);
     }
     c = (c4[0] + c4[1]) + (c4[2] + c4[3]);
   }
@@ -888,8 +918,23 @@ __global__ __launch_bounds__(512) void cheb_softmax_bwd_kernel(ChebSm a) {
   for (int q = 0; q < kSmG; ++q) c += sm_c[q][cj];
   if (j < N) {
     float* dz = a.dz + (int64_t)bk * N * N;
-#pragma unroll 2
-    for (int i = g; i < N; i += kSmG) {
+    int i = g;
+    for (; i + kSmG < N; i += 2 * kSmG) {
+      const int64_t o0 = (int64_t)i * N + j, o1 = o0 + (int64_t)kSmG * N;
+      const float t0 = Tk[o0], t1 = Tk[o1], p0 = P[o0], p1 = P[o1];
+      float w0, w1;
+      if (CL) {
+        w0 = t0 != 0.f ? t0 * dW[o0] : 0.f;
+        w1 = t1 != 0.f ? t1 * dW[o1] : 0.f;
+      } else {
+        const float d0 = dW[o0], d1 = dW[o1];
+        w0 = t0 != 0.f ? t0 * d0 : 0.f;
+        w1 = t1 != 0.f ? t1 * d1 : 0.f;
+      }
+      dz[o0] = p0 * (w0 - c);
+      dz[o1] = p1 * (w1 - c);
+    }
+    for (; i < N; i += kSmG) {
       const int64_t o = (int64_t)i * N + j;
       const float t = Tk[o];
       dz[o] = P[o] * ((t != 0.f ? t * dW[o] : 0.f) - c);
@@ -1172,13 +1217,15 @@ int op_relu_mask(const float* g, const float* y, float* out, int64_t n, hipStrea
 
 int op_cheb_softmax_fwd(const ChebSm& a, hipStream_t st) {
   dim3 grid((unsigned)(cdiv64(a.N, 64) * a.B * a.K));
-  hipLaunchKernelGGL(cheb_softmax_fwd_kernel, grid, dim3(64 * kSmG), 0, st, a);
+  if (a.N >= kSmCondN) hipLaunchKernelGGL(cheb_softmax_fwd_kernel<true>, grid, dim3(64 * kSmG), 0, st, a);
+  else hipLaunchKernelGGL(cheb_softmax_fwd_kernel<false>, grid, dim3(64 * kSmG), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_cheb_softmax_bwd(const ChebSm& a, hipStream_t st) {
   dim3 grid((unsigned)(cdiv64(a.N, 64) * a.B * a.K));
-  hipLaunchKernelGGL(cheb_softmax_bwd_kernel, grid, dim3(64 * kSmG), 0, st, a);
+  if (a.N >= kSmCondN) hipLaunchKernelGGL(cheb_softmax_bwd_kernel<true>, grid, dim3(64 * kSmG), 0, st, a);
+  else hipLaunchKernelGGL(cheb_softmax_bwd_kernel<false>, grid, dim3(64 * kSmG), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
