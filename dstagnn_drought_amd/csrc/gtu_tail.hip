@@ -439,15 +439,27 @@ int rows_gemm(const float* A, int lda, const float* B, Idx2 bk, Idx2 bn, float* 
 
 }  // namespace
 
+// split (gates | GEMM | tail) when the weight does not fit LDS, or from T >= 20 on
+// (measured: SYN T=24 step 60.9 -> 57.7 ms split; PEMS08 T=12 0.91 fused vs 0.99 split);
+// DSTAGNN_TAIL_SPLIT_T overrides the threshold (0 = always split, used by the parity runs)
+constexpr int kTailSplitT = 20;
+bool tail_split_fwd(const GtuTailArgs& a) {
+  static const int split_t = getenv("DSTAGNN_TAIL_SPLIT_T") ? atoi(getenv("DSTAGNN_TAIL_SPLIT_T")) : kTailSplitT;
+  return fwd_lds(a, true) > 32 * 1024 || a.T >= split_t;
+}
+bool tail_split_bwd(const GtuTailArgs& a) {
+  static const int split_t = getenv("DSTAGNN_TAIL_SPLIT_T") ? atoi(getenv("DSTAGNN_TAIL_SPLIT_T")) : kTailSplitT;
+  return bwd_lds(a, true) > 32 * 1024 || a.T >= split_t;
+}
+
 bool gtu_tail_bwd_split(int C, int T) {
   GtuTailArgs a;
   a.C = C; a.T = T;
-  return bwd_lds(a, true) > 32 * 1024;
+  return tail_split_bwd(a);
 }
 
 int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
-  const bool wl = fwd_lds(a, true) <= 32 * 1024;
-  if (!wl) {  // long series: gates | fcmy GEMM | tail
+  if (tail_split_fwd(a)) {  // long series: gates | fcmy GEMM | tail
     const int S = 3 * a.T - 12;
     if (fwd_lds(a, false, true) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
     DS_TRY(launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 1>, fwd_lds(a, false, true), a, st));
@@ -460,9 +472,8 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
 }
 
 int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
-  const bool wl = bwd_lds(a, true) <= 32 * 1024;
   static const bool generic = getenv("DSTAGNN_TAIL_GENERIC") && atoi(getenv("DSTAGNN_TAIL_GENERIC")) != 0;
-  if (!wl) {  // long series: LN / residual | dG GEMM | gates
+  if (tail_split_bwd(a)) {  // long series: LN / residual | dG GEMM | gates
     if (!a.dG) { set_last_error("gtu_tail: split backward needs the dG scratch"); return DSTAGNN_E_ARG; }
     const int S = 3 * a.T - 12;
     if (bwd_lds(a, false, false) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }

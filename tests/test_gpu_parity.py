@@ -329,11 +329,12 @@ CONFIGS = {
     "pems07": (883, 12, 3, 4, 512, 32, 32),
     "gambia": (2139, 144, 2, 2, 64, 32, 32),   # long series: sparse Chebyshev rows in 1024-element chunks
     "syn": (4096, 24, 5, 8, 512, 32, 32),
+    "t24": (64, 24, 3, 2, 64, 32, 32),         # small graph, T >= 20: the split GTU tail
 }
 
 
 @pytest.mark.parametrize("name,first", [("pems04", False), ("pems07", False), ("gambia", True),
-                                        ("gambia", False), ("syn", False)])
+                                        ("gambia", False), ("syn", False), ("t24", True), ("t24", False)])
 def test_block_vs_oracle_configs(name, first):
     """Held against the oracle evaluated in float64.  Bound per tensor: the stated 1e-4
     (scaled by max(1, max|ref|)), or twice the error of the reference's own fp32 arithmetic
