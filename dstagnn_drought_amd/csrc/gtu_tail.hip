@@ -15,10 +15,11 @@
 // Long series (GAMBIA T=144: S = 420, the fcmy weight is 242 KB and a node's G tile 54 KB)
 // do not fit that mould: one wave per node would run the 2*C*T*S = 3.9 MFLOP fcmy product
 // per node as scalar FMAs out of cache (measured 0.37 TFLOP/s, 93 % of the step).  There
-// the tail splits around the product (PH template argument): gates -> G (PH 1), the fcmy
-// product as one MFMA GEMM over all B*N*C rows (bias in its epilogue, written into tco),
-// residual / ReLUs / LayerNorm reading it back (PH 2); backward: LN / residual -> dtc
-// (PH 1), dG = dtc W as one GEMM, gates backward reading dG (PH 2).
+// the tail splits around the product (also from T >= 20, measured faster): gates -> G
+// (gtu_gates_kernel, LDS transpose), the fcmy product as one MFMA GEMM over all B*N*C rows
+// (bias in its epilogue, written into tco), residual / ReLUs / LayerNorm reading it back
+// (node kernel, PH 2); backward: LN / residual -> dtc (node kernel, PH 1), dG = dtc W as
+// one GEMM, the gates backward from dG (gtu_gates_bwd_kernel).
 #include "common.hpp"
 #include "ops.hpp"
 
@@ -87,7 +88,8 @@ __device__ __forceinline__ void col_sums_over_c(const float* v, int C, int T, in
   __syncthreads();
 }
 
-// PH: 0 = fused, 1 = gates -> G only, 2 = from the GEMM's tc (in tco) to the output
+// PH: 0 = fused, 2 = split path: from the GEMM's tc (in tco) to the output (the gates run
+// in gtu_gates_kernel)
 template <int KC, int KT, bool WL, int PH = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
@@ -135,15 +137,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
         }
       }
     }
-    if (!a.first && PH != 1)
+    if (!a.first)
       for (int e = tid; e < CT; e += kNT) Xs[(e / C) * CP + e % C] = a.X[base + e];  // X rows (t, c)
     __syncthreads();
     if (PH != 2)
       for (int e = tid; e < CS; e += kNT) a.G[bn * CS + e] = Gs[(e / S) * SP + e % S];  // [c][s], coalesced
-    if (PH == 1) {
-      __syncthreads();  // LDS reuse by the next node
-      continue;
-    }
     // fcmy + dropout + residual + ReLUs; element e = (c, t) of the (C, T) output
     #pragma unroll 1
     for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
@@ -213,6 +211,75 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
   }
 }
 
+// Split path, gates only: G[bn][c][s] = tanh(P) * sigmoid(Q) for one (node, 64-wide s
+// chunk) per 256-thread workgroup.  Conv rows are read with c fastest (coalesced), the tile
+// is transposed through LDS ([c][s], odd stride) and written as 64-float G row segments.
+// Small LDS (C*65 floats), so many workgroups per CU: this is an HBM stream, not a chain.
+constexpr int kGsW = 64;
+__global__ __launch_bounds__(256) void gtu_gates_kernel(GtuTailArgs a, int nchunk) {
+  extern __shared__ float lds[];
+  const int C = a.C, T = a.T, S = 3 * T - 12, C2 = 2 * C;
+  const int64_t bn = blockIdx.x / nchunk;
+  const int s0 = (int)(blockIdx.x % nchunk) * kGsW;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < kGsW * C; e += 256) {
+    const int sl = e / C, c = e - sl * C, sidx = s0 + sl;
+    if (sidx < S) {
+      int gi, t;
+      gate_index(sidx, T, &gi, &t);
+      const int Tg = T - 2 - 2 * gi;
+      const float* cg = gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2]);
+      const float* cv = cg + (bn * Tg + t) * C2;
+      lds[c * (kGsW + 1) + sl] = fast_tanh(cv[c]) * fast_sigmoid(cv[C + c]);
+    }
+  }
+  __syncthreads();
+  float* G = a.G + bn * (int64_t)C * S;
+  for (int e = tid; e < C * kGsW; e += 256) {
+    const int c = e / kGsW, sl = e - c * kGsW;
+    if (s0 + sl < S) G[(int64_t)c * S + s0 + sl] = lds[c * (kGsW + 1) + sl];
+  }
+}
+
+// Split path, gates backward: one (node, gate, 64-row chunk of the zero-padded (t', o)
+// output) per 256-thread workgroup.  The dG slice is read along s (coalesced), transposed
+// through LDS to [t][c]; conv rows and the output rows are walked with o fastest.
+__global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int nchunk) {
+  extern __shared__ float lds[];
+  const int C = a.C, T = a.T, S = 3 * T - 12, C2 = 2 * C, CP = C + 1;
+  int id = blockIdx.x;
+  const int chunk = id % nchunk; id /= nchunk;
+  const int gi = id % 3;
+  const int64_t bn = id / 3;
+  const int ks = 3 + 2 * gi, Tg = T - ks + 1, Lp = T + ks - 1;
+  const int off = gi == 0 ? 0 : (gi == 1 ? T - 2 : 2 * T - 6);
+  const int tp0 = chunk * kGsW;
+  if (tp0 >= Lp) return;
+  const int tid = threadIdx.x;
+  const float* dG = a.dG + bn * (int64_t)C * S + off;
+  for (int e = tid; e < kGsW * C; e += 256) {
+    const int c = e / kGsW, tl = e - c * kGsW, t = tp0 + tl - (ks - 1);
+    lds[tl * CP + c] = (t >= 0 && t < Tg) ? dG[(int64_t)c * S + t] : 0.f;
+  }
+  __syncthreads();
+  const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
+  float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * (int64_t)C2 * Lp;
+  for (int e = tid; e < kGsW * C2; e += 256) {
+    const int tl = e / C2, o = e - tl * C2, tp = tp0 + tl;
+    if (tp >= Lp) continue;
+    const int t = tp - (ks - 1);
+    float v = 0.f;
+    if (t >= 0 && t < Tg) {
+      const int c = o < C ? o : o - C;
+      const float pv = cv[t * C2 + c], qv = cv[t * C2 + C + c];
+      const float dg = lds[tl * CP + c];
+      const float th = fast_tanh(pv), sg = fast_sigmoid(qv);
+      v = o < C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
+    }
+    orow[(int64_t)tp * C2 + o] = v;
+  }
+}
+
 // dG, the dX tile and the LN reduction scratch share one region (disjoint phases)
 struct TailBwdLds {
   int SP, CP, P, dxh, xhl, rr, dg, dxs, red, s1, s2, wl, total;
@@ -228,7 +295,8 @@ struct TailBwdLds {
   }
 };
 
-// PH: 0 = fused, 1 = LN / residual backward to dtc only, 2 = gates backward from a.dG
+// PH: 0 = fused, 1 = split path: LN / residual backward to dtc only (dG by a GEMM, the
+// gates backward in gtu_gates_bwd_kernel)
 template <int KC, int KT, bool WL, int PH = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
@@ -252,7 +320,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const int64_t base = bn * CT;
     const float* mu = a.mu + bn * T;
     const float* rsv = a.rs + bn * T;
-    if (PH != 2) {
     // LayerNorm over C backward
     #pragma unroll 1
     for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
@@ -352,8 +419,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       dGs[c * SP + s] = g;
     }
     __syncthreads();
-    }  // PH != 2
-    const float* dGg = a.dG + bn * (int64_t)C * S;  // PH 2: dG rows [c][s] from the GEMM
     // gates backward into the zero-padded (t', o) rows of each GTU
 #pragma unroll 1
     for (int gi = 0; gi < 3; ++gi) {
@@ -366,7 +431,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
       #pragma unroll 1
       for (int e0 = 0; e0 < E; e0 += kNT * kU) {
-        float pv[kU], qv[kU], dgv[kU];
+        float pv[kU], qv[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           const int e = min(e0 + tid + kNT * u, E - 1);
@@ -375,7 +440,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
           const int c = o < C ? o : o - C;
           pv[u] = cv[t * C2 + c];
           qv[u] = cv[t * C2 + C + c];
-          if (PH == 2) dgv[u] = dGg[c * S + off + t];
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -386,7 +450,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
           float v = 0.f;
           if (t >= 0 && t < Tg) {
             const int c = o < C ? o : o - C;
-            const float dg = PH == 2 ? dgv[u] : dGs[c * SP + off + t];
+            const float dg = dGs[c * SP + off + t];
             const float th = fast_tanh(pv[u]), sg = fast_sigmoid(qv[u]);
             v = o < C ? dg * (1.f - th * th) * sg : dg * th * sg * (1.f - sg);
           }
@@ -461,8 +525,15 @@ bool gtu_tail_bwd_split(int C, int T) {
 int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
   if (tail_split_fwd(a)) {  // long series: gates | fcmy GEMM | tail
     const int S = 3 * a.T - 12;
-    if (fwd_lds(a, false, true) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-    DS_TRY(launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 1>, fwd_lds(a, false, true), a, st));
+    if (fwd_lds(a, false, false) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
+    {
+      const int nchunk = (S + kGsW - 1) / kGsW;
+      const int64_t nwg = a.BN * nchunk;
+      if (nwg >= (1ll << 31)) { set_last_error("gtu_gates: grid too large"); return DSTAGNN_E_SHAPE; }
+      hipLaunchKernelGGL(gtu_gates_kernel, dim3((unsigned)nwg), dim3(256), sizeof(float) * a.C * (kGsW + 1), st, a,
+                         nchunk);
+      DS_CHECK_LAUNCH();
+    }
     DS_TRY(rows_gemm(a.G, S, a.fcmy_w, idx1(1), idx1(S), a.tco, a.T, a.BN * a.C, a.T, S, a.fcmy_b, st));
     return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2>, fwd_lds(a, false, false), a, st);
   }
@@ -479,7 +550,13 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
     if (bwd_lds(a, false, false) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
     DS_TRY(launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false, 1>, bwd_lds(a, false, false), a, st));
     DS_TRY(rows_gemm(a.dtc, a.T, a.fcmy_w, idx1(S), idx1(1), a.dG, S, a.BN * a.C, S, a.T, nullptr, st));
-    return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false, 2>, 0, a, st);
+    const int nchunk = (a.T + 6 + kGsW - 1) / kGsW;  // rows of the longest padded output (ks = 7)
+    const int64_t nwg = a.BN * 3 * nchunk;
+    if (nwg >= (1ll << 31)) { set_last_error("gtu_gates_bwd: grid too large"); return DSTAGNN_E_SHAPE; }
+    hipLaunchKernelGGL(gtu_gates_bwd_kernel, dim3((unsigned)nwg), dim3(256), sizeof(float) * kGsW * (a.C + 1), st, a,
+                       nchunk);
+    DS_CHECK_LAUNCH();
+    return 0;
   }
   const size_t lds = bwd_lds(a, true);
   if (a.C == 32 && a.T == 12 && !generic) return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
