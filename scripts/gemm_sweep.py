@@ -47,8 +47,17 @@ BIG = [
 ]
 # occupancy probes: 64x64 tiles, N=512 (8 n-tiles), K=384 -> M/64*8 blocks
 BIG += [(f"occ{m // 64 * 8}", m, 512, 384, 1, False, False) for m in (2048, 4096, 6144, 8192, 16384, 32768)]
+# long-series / large-graph configs (GAMBIA B=4: N=2139, T=144; SYN B=32: N=4096, T=24)
+LARGE = [
+    ("gam_dX7", 1232064, 32, 448, 1, False, False),
+    ("gam_fcmy", 273792, 144, 420, 1, True, False),
+    ("gam_dG", 273792, 420, 144, 1, True, True),
+    ("syn_dX7", 1048576, 32, 448, 1, False, False),  # M cut to keep a dense A under 2^30 floats
+]
 if os.environ.get("DSTAGNN_SWEEP_BIG"):
     SHAPES = SHAPES + BIG
+if os.environ.get("DSTAGNN_SWEEP_LARGE"):
+    SHAPES = SHAPES + LARGE
 
 
 def child(iters, only=None):
@@ -100,11 +109,15 @@ def main():
     ap.add_argument("--configs", default="auto:1,auto:0,0:1,0:0,1:1,1:0,2:1,3:1,3:0,4:1")
     ap.add_argument("--only", default=None)
     ap.add_argument("--big", action="store_true", help="add large square steady-state probes")
+    ap.add_argument("--large", action="store_true", help="add the GAMBIA / SYN large-M shapes")
     args = ap.parse_args()
+    global SHAPES
     if args.big:
         os.environ["DSTAGNN_SWEEP_BIG"] = "1"
-        global SHAPES
         SHAPES = SHAPES + BIG
+    if args.large:
+        os.environ["DSTAGNN_SWEEP_LARGE"] = "1"
+        SHAPES = SHAPES + LARGE
     if args.child:
         child(args.iters, args.only)
         return

@@ -460,3 +460,61 @@ def test_direct_grads_equal_autograd_grads():
             if a[n] is not None:
                 assert torch.equal(a[n], b[n]), n
     D.set_direct_grads(blk, False)
+
+
+@pytest.mark.parametrize("N,T,first,sparse", [(170, 12, False, True), (170, 12, True, True), (170, 12, False, False),
+                                              (64, 24, False, True), (64, 24, True, True)])
+def test_block_never_reads_unwritten_memory(N, T, first, sparse):
+    """Every buffer the library writes (save / scratch workspaces, outputs, the flat gradient
+    buffer) starts as NaN (block_fn._POISON): the results must be bit-identical to a run on
+    whatever the allocator hands back.  Guards the no-memset paths (sparse dW written on the
+    support only, split-K slabs, the split GTU tail's dG scratch at T=24)."""
+    _need_gpu()
+    import dstagnn_drought_amd as D
+    from dstagnn_drought_amd import block_fn
+    K, h, Dm, dk, C, B = 3, 3, 64, 16, 32, 4
+    rs = np.random.RandomState(5)
+    tmd = np.eye(N)
+    pa = np.zeros((N, N))
+    for i in range(N):
+        tmd[i, rs.choice(N, 2, replace=False)] = 1.0
+        pa[i, rs.choice(N, 4, replace=False)] = 1.0
+    cheb = [torch.from_numpy(c_).float() for c_ in D.cheb_polynomial(_scaled_laplacian_fixed_start(tmd), K)][:K]
+    F = 1 if first else C
+    torch.manual_seed(0)
+    blk = D.DSTAGNN_block("cpu", F, F, K, C, C, 1, cheb, pa, tmd, N, T, Dm, dk, dk, h)
+    for p in blk.parameters():
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+        else:
+            torch.nn.init.uniform_(p)
+    blk = blk.cuda().eval()
+    blk.sparse_cheb = sparse
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(B, N, F, T, device="cuda", generator=g)
+    res = 0 if first else torch.randn(B, 1, h, T, T, device="cuda", generator=g)
+    go = torch.randn(B, N, C, T, device="cuda", generator=g)
+    gr = torch.randn(B, F, h, T, T, device="cuda", generator=g)
+
+    def run():
+        for p in blk.parameters():
+            p.grad = None
+        xg = x.clone().requires_grad_(True)
+        o, r = blk(xg, res)
+        torch.autograd.backward([o, r], [go, gr])
+        out = {"out": o.detach().clone(), "re_at": r.detach().clone(), "grad_x": xg.grad.clone()}
+        out.update({n: p.grad.clone() for n, p in blk.named_parameters() if p.grad is not None})
+        return out
+
+    saved = block_fn._POISON
+    try:
+        block_fn._POISON = False
+        plain = run()
+        block_fn._POISON = True
+        poisoned = run()
+    finally:
+        block_fn._POISON = saved
+    assert plain.keys() == poisoned.keys()
+    for k in plain:
+        assert torch.isfinite(poisoned[k]).all(), f"{k}: NaN from an unwritten buffer"
+        assert torch.equal(plain[k], poisoned[k]), f"{k}: differs with poisoned buffers"
