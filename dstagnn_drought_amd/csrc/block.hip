@@ -180,7 +180,7 @@ int check_dims(const dstagnn_block_dims* d) {
   if (d->K > DSTAGNN_MAX_K) { set_last_error("K > DSTAGNN_MAX_K"); return DSTAGNN_E_SHAPE; }
   if (d->T < 7) { set_last_error("T must be >= 7 (GTU kernel 7, fcmy 3T-12)"); return DSTAGNN_E_SHAPE; }
   if (d->cheb_sparse && !cheb_sparse_ok(d->C * d->T)) {
-    set_last_error("cheb_sparse requires C*T <= 1024");
+    set_last_error("cheb_sparse requires 0 < C*T <= 2^20");
     return DSTAGNN_E_SHAPE;
   }
   if (d->F != 1 && d->F != d->C) {

@@ -61,7 +61,8 @@ typedef struct dstagnn_block_dims {
   uint64_t seed;           /* dropout RNG seed (counter-based hash, per call)     */
   int cheb_sparse;         /* 1: aggregate over the CSC/CSR support in dstagnn_graph
                               (T_k elementwise recurrence => ~3 nnz/column, quirk 4);
-                              0: dense (N,N) T_k.  Requires C*T <= 1024.            */
+                              0: dense (N,N) T_k.  Rows of any length C*T <= 2^20
+                              (walked in 1024-element chunks).                      */
 } dstagnn_block_dims;
 
 /* Parameter pointers in state_dict order.  For the first block
