@@ -61,26 +61,27 @@ constexpr int kU = 8;
 // LDS layout (floats), shared by the kernel and the host size computation
 struct TailFwdLds {
   int SP, CP, P, gs, rl, xs, red, mus, rss, wl, total;
-  __host__ __device__ TailFwdLds(int C, int T, bool stage_w, bool has_g = true) {
+  __host__ __device__ TailFwdLds(int C, int T, bool stage_w, bool has_g = true, int nt = kNT) {
     const int S = 3 * T - 12;
-    SP = S + 1; CP = C + 1; P = T < kNT ? kNT / T : 1;
+    SP = S + 1; CP = C + 1; P = T < nt ? nt / T : 1;
     gs = 0; rl = gs + (has_g ? C * SP : 0); xs = rl + C * T; red = xs + T * CP;
-    mus = red + (P * T > kNT ? P * T : kNT); rss = mus + T; wl = rss + T;
+    mus = red + (P * T > nt ? P * T : nt); rss = mus + T; wl = rss + T;
     total = wl + (stage_w ? T * SP : 0);
   }
 };
 
 // sum over c of v[c*T + t] for every t, into out[t] (lanes: t = l % T, part = l / T)
+template <int NT>
 __device__ __forceinline__ void col_sums_over_c(const float* v, int C, int T, int P, float* red, float* out,
                                                 int tid) {
-  for (int l = tid; l < P * T; l += kNT) {
+  for (int l = tid; l < P * T; l += NT) {
     const int t = l % T, part = l / T;
     float acc = 0.f;
     for (int c = part; c < C; c += P) acc += v[c * T + t];
     red[l] = acc;
   }
   __syncthreads();
-  for (int t = tid; t < T; t += kNT) {
+  for (int t = tid; t < T; t += NT) {
     float acc = 0.f;
     for (int q = 0; q < P; ++q) acc += red[q * T + t];
     out[t] = acc;
@@ -90,11 +91,11 @@ __device__ __forceinline__ void col_sums_over_c(const float* v, int C, int T, in
 
 // PH: 0 = fused, 2 = split path: from the GEMM's tc (in tco) to the output (the gates run
 // in gtu_gates_kernel)
-template <int KC, int KT, bool WL, int PH = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void gtu_tail_fwd_kernel(GtuTailArgs a) {
+template <int KC, int KT, bool WL, int PH = 0, int NT = kNT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) void gtu_tail_fwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C, CS = C * S;
-  const TailFwdLds L(C, T, WL, PH != 2);
+  const TailFwdLds L(C, T, WL, PH != 2, NT);
   const int SP = L.SP, CP = L.CP;
   float* Gs = lds + L.gs;    // [c][SP]
   float* rl = lds + L.rl;    // [c][t]
@@ -107,16 +108,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
   const int WS = WL ? SP : S;
   const int tid = threadIdx.x;
   if (WL)
-    for (int e = tid; e < T * S; e += kNT) Wl[(e / S) * SP + e % S] = a.fcmy_w[e];
+    for (int e = tid; e < T * S; e += NT) Wl[(e / S) * SP + e % S] = a.fcmy_w[e];
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     const int64_t base = bn * CT;
     // gates, element (s, c) with c fastest: coalesced conv-row reads
     #pragma unroll 1
-    for (int e0 = 0; e0 < (PH == 2 ? 0 : CS); e0 += kNT * kU) {
+    for (int e0 = 0; e0 < (PH == 2 ? 0 : CS); e0 += NT * kU) {
       float pv[kU], qv[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = min(e0 + tid + kNT * u, CS - 1);
+        const int e = min(e0 + tid + NT * u, CS - 1);
         const int sidx = e / C, c = e - sidx * C;
         int gi, t;
         gate_index(sidx, T, &gi, &t);
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = e0 + tid + kNT * u;
+        const int e = e0 + tid + NT * u;
         if (e < CS) {
           const int sidx = e / C, c = e - sidx * C;
           Gs[c * SP + sidx] = fast_tanh(pv[u]) * fast_sigmoid(qv[u]);
@@ -138,23 +139,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
       }
     }
     if (!a.first)
-      for (int e = tid; e < CT; e += kNT) Xs[(e / C) * CP + e % C] = a.X[base + e];  // X rows (t, c)
+      for (int e = tid; e < CT; e += NT) Xs[(e / C) * CP + e % C] = a.X[base + e];  // X rows (t, c)
     __syncthreads();
     if (PH != 2)
-      for (int e = tid; e < CS; e += kNT) a.G[bn * CS + e] = Gs[(e / S) * SP + e % S];  // [c][s], coalesced
+      for (int e = tid; e < CS; e += NT) a.G[bn * CS + e] = Gs[(e / S) * SP + e % S];  // [c][s], coalesced
     // fcmy + dropout + residual + ReLUs; element e = (c, t) of the (C, T) output
     #pragma unroll 1
-    for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
+    for (int e0 = 0; e0 < CT; e0 += NT * kU) {
       float xv[kU], tcv[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = min(e0 + tid + kNT * u, CT - 1);
+        const int e = min(e0 + tid + NT * u, CT - 1);
         xv[u] = a.first ? a.x[bn * T + e % T] : a.x[base + e];
         if (PH == 2) tcv[u] = a.tco[base + e];  // fcmy output (bias included) from the GEMM
       }
 #pragma unroll 1
       for (int u = 0; u < kU; ++u) {
-        const int e = e0 + tid + kNT * u;
+        const int e = e0 + tid + NT * u;
         if (e >= CT) continue;
         const int c = e / T, t = e - c * T;
         float tc;
@@ -183,10 +184,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
     }
     __syncthreads();
     // LayerNorm over C: mean, then the centred second moment (two fixed-order passes)
-    col_sums_over_c(rl, C, T, L.P, red, mus, tid);
-    for (int t = tid; t < T; t += kNT) mus[t] *= 1.f / C;
+    col_sums_over_c<NT>(rl, C, T, L.P, red, mus, tid);
+    for (int t = tid; t < T; t += NT) mus[t] *= 1.f / C;
     __syncthreads();
-    for (int l = tid; l < L.P * T; l += kNT) {
+    for (int l = tid; l < L.P * T; l += NT) {
       const int t = l % T, part = l / T;
       const float mean = mus[t];
       float acc = 0.f;
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
       red[l] = acc;
     }
     __syncthreads();
-    for (int t = tid; t < T; t += kNT) {
+    for (int t = tid; t < T; t += NT) {
       float var = 0.f;
       for (int q = 0; q < L.P; ++q) var += red[q * T + t];
       const float rs = rsqrtf(var * (1.f / C) + 1e-5f);
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
       a.rs[bn * T + t] = rs;
     }
     __syncthreads();
-    for (int e = tid; e < CT; e += kNT) {
+    for (int e = tid; e < CT; e += NT) {
       const int c = e / T, t = e - c * T;
       a.out[base + e] = (rl[e] - mus[t]) * rss[t] * a.ln_g[c] + a.ln_b[c];
     }
@@ -283,10 +284,10 @@ __global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int n
 // dG, the dX tile and the LN reduction scratch share one region (disjoint phases)
 struct TailBwdLds {
   int SP, CP, P, dxh, xhl, rr, dg, dxs, red, s1, s2, wl, total;
-  __host__ __device__ TailBwdLds(int C, int T, bool stage_w, bool has_g = true) {
+  __host__ __device__ TailBwdLds(int C, int T, bool stage_w, bool has_g = true, int nt = kNT) {
     const int S = 3 * T - 12, CT = C * T;
-    SP = S + 1; CP = C + 1; P = T < kNT ? kNT / T : 1;
-    const int nred = 2 * (P * T > kNT ? P * T : kNT);
+    SP = S + 1; CP = C + 1; P = T < nt ? nt / T : 1;
+    const int nred = 2 * (P * T > nt ? P * T : nt);
     int shared = has_g ? C * SP : 0;
     if (T * CP > shared) shared = T * CP;
     if (nred > shared) shared = nred;
@@ -297,11 +298,11 @@ struct TailBwdLds {
 
 // PH: 0 = fused, 1 = split path: LN / residual backward to dtc only (dG by a GEMM, the
 // gates backward in gtu_gates_bwd_kernel)
-template <int KC, int KT, bool WL, int PH = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void gtu_tail_bwd_kernel(GtuTailArgs a) {
+template <int KC, int KT, bool WL, int PH = 0, int NT = kNT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void gtu_tail_bwd_kernel(GtuTailArgs a) {
   extern __shared__ float lds[];
   const int C = KC ? KC : a.C, T = KT ? KT : a.T, S = 3 * T - 12, CT = C * T, C2 = 2 * C;
-  const TailBwdLds L(C, T, WL, PH == 0);
+  const TailBwdLds L(C, T, WL, PH == 0, NT);
   const int SP = L.SP, CP = L.CP;
   float* dxh = lds + L.dxh;   // CT  (LN dxhat, then dtc)
   float* xhl = lds + L.xhl;   // CT
@@ -315,18 +316,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   const float* Ws = WL ? Wl : a.fcmy_w;
   const int tid = threadIdx.x;
   if (WL)
-    for (int e = tid; e < T * S; e += kNT) Wl[e] = a.fcmy_w[e];
+    for (int e = tid; e < T * S; e += NT) Wl[e] = a.fcmy_w[e];
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     const int64_t base = bn * CT;
     const float* mu = a.mu + bn * T;
     const float* rsv = a.rs + bn * T;
     // LayerNorm over C backward
     #pragma unroll 1
-    for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
+    for (int e0 = 0; e0 < CT; e0 += NT * kU) {
       float dyv[kU], rv[kU], muv[kU], rsw[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = min(e0 + tid + kNT * u, CT - 1);
+        const int e = min(e0 + tid + NT * u, CT - 1);
         const int t = e % T;
         dyv[u] = a.dout[base + e];
         rv[u] = a.r[base + e];
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = e0 + tid + kNT * u;
+        const int e = e0 + tid + NT * u;
         if (e >= CT) continue;
         const int c = e / T;
         const float xh = (rv[u] - muv[u]) * rsw[u];
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       }
     }
     __syncthreads();
-    for (int l = tid; l < L.P * T; l += kNT) {  // sum_c dxhat and dxhat*xhat per t, P lane groups
+    for (int l = tid; l < L.P * T; l += NT) {  // sum_c dxhat and dxhat*xhat per t, P lane groups
       const int t = l % T, part = l / T;
       float s1 = 0.f, s2 = 0.f;
       for (int c = part; c < C; c += L.P) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       red[L.P * T + l] = s2;
     }
     __syncthreads();
-    for (int t = tid; t < T; t += kNT) {
+    for (int t = tid; t < T; t += NT) {
       float s1 = 0.f, s2 = 0.f;
       for (int q = 0; q < L.P; ++q) { s1 += red[q * T + t]; s2 += red[L.P * T + q * T + t]; }
       s1s[t] = s1 * (1.f / C); s2s[t] = s2 * (1.f / C);
@@ -362,11 +363,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     __syncthreads();
     // ReLUs, residual, dropout: dtc (kept in LDS, dxh reused) and the direct grads
     #pragma unroll 1
-    for (int e0 = 0; e0 < CT; e0 += kNT * kU) {
+    for (int e0 = 0; e0 < CT; e0 += NT * kU) {
       float tcov[kU], xv[kU], rsw[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = min(e0 + tid + kNT * u, CT - 1);
+        const int e = min(e0 + tid + NT * u, CT - 1);
         const int t = e % T;
         tcov[u] = a.tco[base + e];
 
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = e0 + tid + kNT * u;
+        const int e = e0 + tid + NT * u;
         if (e >= CT) continue;
         const int c = e / T, t = e - c * T;
         float dr = rsw[u] * (dxh[e] - s1s[t] - xhl[e] * s2s[t]);
@@ -397,10 +398,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       }
     }
     __syncthreads();
-    for (int e = tid; e < CT; e += kNT) a.dX[base + e] = dXs[(e / C) * CP + e % C];  // coalesced
+    for (int e = tid; e < CT; e += NT) a.dX[base + e] = dXs[(e / C) * CP + e % C];  // coalesced
     __syncthreads();  // dXs shares its LDS with dGs
     if (a.first) {
-      for (int t = tid; t < T; t += kNT) {
+      for (int t = tid; t < T; t += NT) {
         float sum = 0.f;
         for (int c = 0; c < C; ++c) sum += a.res_w[c] * xhl[c * T + t];
         a.dx[bn * T + t] = sum;
@@ -412,7 +413,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
     // fcmy backward: dG[c, s] = sum_t dtc[c, t] W[t, s]
     #pragma unroll 1
-    for (int e = tid; e < (PH == 0 ? C * S : 0); e += kNT) {
+    for (int e = tid; e < (PH == 0 ? C * S : 0); e += NT) {
       const int c = e / S, s = e - c * S;
       float g = 0.f;
       for (int t = 0; t < T; ++t) g = fmaf(dxh[c * T + t], Ws[t * S + s], g);
@@ -430,11 +431,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * E;
       const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
       #pragma unroll 1
-      for (int e0 = 0; e0 < E; e0 += kNT * kU) {
+      for (int e0 = 0; e0 < E; e0 += NT * kU) {
         float pv[kU], qv[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-          const int e = min(e0 + tid + kNT * u, E - 1);
+          const int e = min(e0 + tid + NT * u, E - 1);
           const int tp = e / C2, o = e - tp * C2;
           const int t = min(max(tp - (ks - 1), 0), Tg - 1);
           const int c = o < C ? o : o - C;
@@ -443,7 +444,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-          const int e = e0 + tid + kNT * u;
+          const int e = e0 + tid + NT * u;
           if (e >= E) continue;
           const int tp = e / C2, o = e - tp * C2;
           const int t = tp - (ks - 1);
@@ -462,11 +463,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   }
 }
 
-size_t fwd_lds(const GtuTailArgs& a, bool wl, bool has_g = true) {
-  return sizeof(float) * (size_t)TailFwdLds(a.C, a.T, wl, has_g).total;
+size_t fwd_lds(const GtuTailArgs& a, bool wl, bool has_g = true, int nt = kNT) {
+  return sizeof(float) * (size_t)TailFwdLds(a.C, a.T, wl, has_g, nt).total;
 }
-size_t bwd_lds(const GtuTailArgs& a, bool wl, bool has_g = true) {
-  return sizeof(float) * (size_t)TailBwdLds(a.C, a.T, wl, has_g).total;
+size_t bwd_lds(const GtuTailArgs& a, bool wl, bool has_g = true, int nt = kNT) {
+  return sizeof(float) * (size_t)TailBwdLds(a.C, a.T, wl, has_g, nt).total;
 }
 
 unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 65536); }
@@ -474,12 +475,12 @@ unsigned node_grid(int64_t BN) { return (unsigned)std::min<int64_t>(BN, 65536); 
 constexpr size_t kLdsMax = 160 * 1024;  // gfx950 LDS per workgroup
 
 template <typename K>
-int launch_node_kernel(K kernel, size_t lds, const GtuTailArgs& a, hipStream_t st) {
+int launch_node_kernel(K kernel, size_t lds, const GtuTailArgs& a, hipStream_t st, int nt = kNT) {
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) { set_last_error(std::string("gtu_tail LDS: ") + hipGetErrorString(e)); return (int)e; }
   }
-  hipLaunchKernelGGL(kernel, dim3(node_grid(a.BN)), dim3(kNT), lds, st, a);
+  hipLaunchKernelGGL(kernel, dim3(node_grid(a.BN)), dim3(nt), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -516,6 +517,14 @@ bool tail_split_bwd(const GtuTailArgs& a) {
   return bwd_lds(a, true) > 32 * 1024 || a.T >= split_t;
 }
 
+// threads per node in the split path's residual / LayerNorm kernels: a long series' node
+// tile (C*T = 4608 at GAMBIA) holds ~74 KB of LDS, so only two workgroups fit a CU; 256
+// threads each keep 8 waves per CU in flight instead of 2 (DSTAGNN_TAIL_NT=64 for A/B)
+int split_nt() {
+  static const int nt = getenv("DSTAGNN_TAIL_NT") ? atoi(getenv("DSTAGNN_TAIL_NT")) : 256;
+  return nt == 64 ? 64 : 256;
+}
+
 bool gtu_tail_bwd_split(int C, int T) {
   GtuTailArgs a;
   a.C = C; a.T = T;
@@ -535,7 +544,9 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
       DS_CHECK_LAUNCH();
     }
     DS_TRY(rows_gemm(a.G, S, a.fcmy_w, idx1(1), idx1(S), a.tco, a.T, a.BN * a.C, a.T, S, a.fcmy_b, st));
-    return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2>, fwd_lds(a, false, false), a, st);
+    if (split_nt() == 64)
+      return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2, 64>, fwd_lds(a, false, false, 64), a, st, 64);
+    return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2, 256>, fwd_lds(a, false, false, 256), a, st, 256);
   }
   const size_t lds = fwd_lds(a, true);
   if (a.C == 32 && a.T == 12) return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true>, lds, a, st);
@@ -548,7 +559,10 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
     if (!a.dG) { set_last_error("gtu_tail: split backward needs the dG scratch"); return DSTAGNN_E_ARG; }
     const int S = 3 * a.T - 12;
     if (bwd_lds(a, false, false) > kLdsMax) { set_last_error("gtu_tail: C*T too large for LDS"); return DSTAGNN_E_SHAPE; }
-    DS_TRY(launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false, 1>, bwd_lds(a, false, false), a, st));
+    if (split_nt() == 64)
+      DS_TRY(launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false, 1, 64>, bwd_lds(a, false, false, 64), a, st, 64));
+    else
+      DS_TRY(launch_node_kernel(gtu_tail_bwd_kernel<0, 0, false, 1, 256>, bwd_lds(a, false, false, 256), a, st, 256));
     DS_TRY(rows_gemm(a.dtc, a.T, a.fcmy_w, idx1(S), idx1(1), a.dG, S, a.BN * a.C, S, a.T, nullptr, st));
     const int nchunk = (a.T + 6 + kGsW - 1) / kGsW;  // rows of the longest padded output (ks = 7)
     const int64_t nwg = a.BN * 3 * nchunk;
