@@ -525,6 +525,13 @@ int split_nt() {
   return nt == 64 ? 64 : 256;
 }
 
+// threads per node of the fused C=32/T=12 kernels (DSTAGNN_TAIL_FUSED_NT = 64 | 128 | 256):
+// 256 measured 0.868 vs 0.873 ms/step for 64 (PEMS08 block, 2 x 200 steps each)
+int fused_nt() {
+  static const int nt = getenv("DSTAGNN_TAIL_FUSED_NT") ? atoi(getenv("DSTAGNN_TAIL_FUSED_NT")) : 256;
+  return nt;
+}
+
 bool gtu_tail_bwd_split(int C, int T) {
   GtuTailArgs a;
   a.C = C; a.T = T;
@@ -549,7 +556,13 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
     return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2, 256>, fwd_lds(a, false, false, 256), a, st, 256);
   }
   const size_t lds = fwd_lds(a, true);
-  if (a.C == 32 && a.T == 12) return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true>, lds, a, st);
+  if (a.C == 32 && a.T == 12) {
+    switch (fused_nt()) {
+      case 128: return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true, 0, 128>, fwd_lds(a, true, true, 128), a, st, 128);
+      case 256: return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true, 0, 256>, fwd_lds(a, true, true, 256), a, st, 256);
+      default: return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true>, lds, a, st);
+    }
+  }
   return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, true>, lds, a, st);
 }
 
@@ -573,6 +586,12 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
     return 0;
   }
   const size_t lds = bwd_lds(a, true);
-  if (a.C == 32 && a.T == 12 && !generic) return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
+  if (a.C == 32 && a.T == 12 && !generic) {
+    switch (fused_nt()) {
+      case 128: return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true, 0, 128>, bwd_lds(a, true, true, 128), a, st, 128);
+      case 256: return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true, 0, 256>, bwd_lds(a, true, true, 256), a, st, 256);
+      default: return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true>, lds, a, st);
+    }
+  }
   return launch_node_kernel(gtu_tail_bwd_kernel<0, 0, true>, lds, a, st);
 }
