@@ -18,6 +18,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -181,17 +183,32 @@ def cpu_baseline(budget_s=12.0):
                       f"{dt:.1f} s"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--hot-iters", type=int, default=50)
-    ap.add_argument("--no-extras", action="store_true", help="skip the first-block / full-model lines")
-    args = ap.parse_args()
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
+
+def self_launch(n):
+    """`bench.py --gpus N` run without a launcher: start N ranks (one process per GPU) with
+    torch.distributed.run on 127.0.0.1 and exit with its status.  Runs before anything
+    touches the GPU (a child process, never an exec).  The same as the driver's own
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`
+    (reference: xmp.spawn(main, nprocs=8), train_DSTAGNN_my.py:195-197)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    log(f"self-launch: {n} ranks via torch.distributed.run")
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(gpus):
+    """(rank, world, local) of this process; initialises the process group for world > 1.
+    WORLD_SIZE (set by the launcher) must equal --gpus: a scaling run that silently measured
+    another world size would be worse than a failure."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # DSTAGNN_DIST_BACKEND=gloo + DSTAGNN_DEVICE_MOD=1 rehearse the multi-rank path on a single
@@ -200,12 +217,46 @@ def main():
     local = local % int(os.environ.get("DSTAGNN_DEVICE_MOD", "1000000"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
         if backend == "nccl":
+            torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    return rank, world, local
+
+
+def launch_probe(rank, world):
+    """--launch-probe: the launcher and the collective only (no GPU work; CPU tests run it
+    over gloo): every rank contributes its rank, rank 0 prints what it saw."""
+    t = torch.tensor([float(rank), 1.0])
+    if world > 1:
+        dist.all_reduce(t)
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": world, "ranks_seen": int(t[1]),
+                          "rank_sum": int(t[0])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hot-iters", type=int, default=50)
+    ap.add_argument("--no-extras", action="store_true", help="skip the first-block / full-model lines")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
+    rank, world, local = init_ranks(args.gpus)
+    if args.launch_probe:
+        return launch_probe(rank, world)
     dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
 
     from dstagnn_drought_amd import _lib
     from dstagnn_drought_amd.block_fn import make_dims, workspace_sizes, _fill, graph_struct, use_sparse
@@ -222,7 +273,7 @@ def main():
     reducer = None
     if world > 1:
         from dstagnn_drought_amd.dp import GradAllReducer, mask_support_of
-        reducer = GradAllReducer(blk.named_parameters(), mask_support=mask_support_of(blk))
+        reducer = GradAllReducer(blk.named_parameters(), mask_support=mask_support_of(blk)).attach(blk)
 
     def step():
         for p in params:

@@ -224,6 +224,7 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
         _lib.check(rc, "dstagnn_block_backward")
         ctx.save_buf = None
         if ctx.direct_params is not None:
+            fresh = True
             for prm, g in zip(ctx.direct_params, grads):
                 if g is None or not prm.requires_grad:
                     continue
@@ -231,7 +232,13 @@ class DSTAGNNBlockFunction(torch.autograd.Function):
                     prm.grad = g
                 else:
                     prm.grad.add_(g)
+                    fresh = False
             grads = [None] * len(grads)
+            # DP (dp.GradAllReducer.attach): this block's gradients are final and packed in
+            # ONE flat buffer -> its all-reduce starts now, beside the rest of the backward
+            hook = ctx.meta.get("grads_ready")
+            if hook is not None and fresh:
+                hook(flat)
         return (None, None, d_x, d_ra, None, *grads)
 
 

@@ -329,7 +329,7 @@ __device__ float g_zero_page[64];  // k >= K lanes of the last tile fetch zeros 
 // in flight into stage t+2 and drains it (vmcnt(0)) before every read.  The asm saves and
 // restores M0 (compiler-owned); all ordering is by the explicit waits + barrier below.
 // four DMAs into consecutive 1 KiB LDS slots under one M0: the instruction offset moves
-// both the LDS destination and the global source (probed: scripts/glds_probe.hip), so the
+// both the LDS destination and the global source (probed: tools/glds_probe.hip), so the
 // VGPR offsets carry -1024*i and the SGPR base is pre-lowered by 4 KiB to keep them >= 0.
 __device__ __forceinline__ void glds4_saddr(const float* base_m4k, uint32_t o0, uint32_t o1, uint32_t o2,
                                             uint32_t o3, uint32_t lds_addr) {
@@ -624,10 +624,10 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   k.Cout = g.Cout ? g.Cout + g.c_off : nullptr;
   k.ws = ws;
 
-  // optional overrides for tuning sweeps (scripts/gemm_sweep.py)
+  // optional overrides for tuning sweeps (tools/gemm_sweep.py)
   static const int env_cfg = getenv("DSTAGNN_GEMM_CFG") ? atoi(getenv("DSTAGNN_GEMM_CFG")) : -1;
   static const int env_split = getenv("DSTAGNN_GEMM_SPLITK") ? atoi(getenv("DSTAGNN_GEMM_SPLITK")) : 0;
-  // Tile choice, from the measured sweep (scripts/gemm_sweep.py, profiles/): at these
+  // Tile choice, from the measured sweep (tools/gemm_sweep.py, profiles/): at these
   // sizes a block's latency (setup, first-tile load, epilogue) dominates, so the small
   // 64x64 tile (most blocks, 4 resident per CU) wins unless N is skinny (<= 32: 128x32)
   // or the grid is large enough for 128x128 tiles to fill the chip several times over.

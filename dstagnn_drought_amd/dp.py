@@ -11,6 +11,8 @@ Design for MI355X / xGMI:
   * cheb_conv_SAt.mask.k gradients are non-zero only on adj_pa's support
     (dM_k = A_pa o sum_b dz), so only those nnz values travel (92 % of the bytes at
     the SYN config); the off-support zeros are restored locally;
+  * overlap: with attach(), each block's flat gradient buffer is all-reduced asynchronously
+    the moment that block's backward finishes, beside the remaining blocks' backward;
   * the reference shards nothing (all replicas see the same batch, quirk 15): here each
     rank takes a disjoint slice of the global batch (shard_batch).
 """
@@ -45,6 +47,25 @@ class GradAllReducer:
                 idx = torch.nonzero(sup[n].reshape(-1).to(p.device), as_tuple=False).reshape(-1)
             self.items.append((n, p, idx))
         self.bucket_elems = max(1, bucket_bytes // 4)
+        self._inflight = []  # (flat gradient buffer, async work) started during the backward
+
+    def attach(self, model):
+        """Overlap the exchange with the backward: every DSTAGNN_block of `model` in
+        direct-grad mode hands its flat gradient buffer over the moment its backward is done
+        (block_fn: meta["grads_ready"]), and its all-reduce is issued asynchronously there
+        (RCCL runs it on its own stream beside the next block's backward kernels).
+        all_reduce() then waits for those and reduces what is left (the head's grads)."""
+        from .model import DSTAGNN_block
+        for m in model.modules():
+            if isinstance(m, DSTAGNN_block):
+                m.grads_ready = self.on_grads_ready
+        return self
+
+    def on_grads_ready(self, flat):
+        if flat.numel() * 4 > self.dense_limit:
+            return  # the masks are sent as their support by all_reduce()
+        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._inflight.append((flat, work))
 
     def _payload(self, p, idx):
         g = p.grad.reshape(-1)
@@ -71,9 +92,17 @@ class GradAllReducer:
 
     def all_reduce(self):
         world = dist.get_world_size(self.group)
+        done = set()
+        for flat, work in self._inflight:  # started during the backward (attach)
+            work.wait()
+            flat.div_(world)
+            done.add(flat.data_ptr())
+        self._inflight.clear()
         live = [(n, p, idx) for n, p, idx in self.items if p.grad is not None]
         bases, taken = self._flat_groups(live)
         for b in bases:
+            if b.data_ptr() in done:
+                continue
             dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group)
             b.div_(world)
         live = [it for it in live if id(it[1]) not in taken]

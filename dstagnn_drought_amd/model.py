@@ -144,6 +144,18 @@ class GTU(nn.Module):
         self.con2out = nn.Conv2d(in_channels, 2 * in_channels, kernel_size=(1, kernel_size), stride=(1, time_strides))
 
 
+def _rank_seed(seed):
+    """Per-forward dropout seed, mixed with the data-parallel rank.  Every rank draws the same
+    value from torch's global RNG (all ranks keep one RNG state: the epoch permutation must be
+    identical), so without the mix every replica would drop the same positions of its own
+    shard; the reference's 8 replicas see the same batch (quirk 15), here they do not."""
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        r = torch.distributed.get_rank()
+        if r:
+            seed = (seed ^ ((r * 0x9E3779B97F4A7C15) & ((1 << 64) - 1))) & ((1 << 62) - 1)
+    return seed
+
+
 class DSTAGNN_block(nn.Module):
     """One spatial-temporal block (model/DSTAGNN_my.py:199-253), forward/backward on the HIP path."""
 
@@ -179,6 +191,7 @@ class DSTAGNN_block(nn.Module):
         self.nb_time_filter = nb_time_filter
         self.sparse_cheb = True  # use the CSC/CSR support path when the support is sparse
         self.direct_grads = False  # see set_direct_grads
+        self.grads_ready = None    # DP hook: called with the block's flat gradient buffer
 
     def forward(self, x, res_att):
         B, N, Fd, T = x.shape
@@ -194,7 +207,9 @@ class DSTAGNN_block(nn.Module):
         # a fresh dropout seed per training forward, drawn from torch's global RNG (no draw
         # when dropout is off: like F.dropout(p=0), which consumes no random numbers)
         drop = self.training and meta.get("drop_p", 0.0) > 0.0
-        meta["seed"] = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop else 0
+        meta["seed"] = _rank_seed(int(torch.randint(0, 2 ** 62, (1,)).item())) if drop else 0
+        if self.grads_ready is not None:
+            meta["grads_ready"] = self.grads_ready
         names, params = self._param_list()
         graph = self._graph()
         return DSTAGNNBlockFunction.apply(meta, names, x.float(), res_att, graph, *params)

@@ -187,7 +187,9 @@ def fit(net, train_x, train_y, val_x, val_y, *, epochs, start_epoch=0, batch_siz
     rank, world = _world()
     criterion = nn.SmoothL1Loss().to(train_x.device)
     optimizer = torch.optim.Adam(net.parameters(), lr=lr)
-    reducer = GradAllReducer(net.named_parameters(), mask_support=mask_support_of(net)) if world > 1 else None
+    reducer = None
+    if world > 1:  # block gradients all-reduced beside the backward (attach)
+        reducer = GradAllReducer(net.named_parameters(), mask_support=mask_support_of(net)).attach(net)
     loader = DeviceBatches(train_x, train_y, batch_size, True, rank, world)
 
     def optimizer_step(reduce=True):  # xm.optimizer_step
@@ -227,6 +229,19 @@ def fit(net, train_x, train_y, val_x, val_y, *, epochs, start_epoch=0, batch_siz
     return best_epoch, best_val, history
 
 
+def load_best(net, path):
+    """train_DSTAGNN_my.py:184 (torch.load of the best checkpoint).  Only rank 0 wrote the file
+    and only rank 0 reads it; the other ranks receive its tensors by broadcast (no shared
+    filesystem assumed)."""
+    rank, world = _world()
+    if rank == 0:
+        net.load_state_dict(torch.load(path, weights_only=True))
+    if world > 1:
+        with torch.no_grad():
+            for t in net.state_dict().values():
+                dist.broadcast(t, src=0)
+
+
 def run(config_path, *, epochs=None, double_step=True, dropout=None, max_batches=None, root='myexperiments',
         log=print):
     """Whole script: data, graphs, model, training, best-checkpoint test loss."""
@@ -257,10 +272,7 @@ def run(config_path, *, epochs=None, double_step=True, dropout=None, max_batches
                                         start_epoch=int(tc['start_epoch']), batch_size=bs,
                                         lr=float(tc['learning_rate']), params_path=params_path,
                                         double_step=double_step, max_batches=max_batches, log=log)
-    if world > 1:
-        dist.barrier()
-    sd = torch.load(os.path.join(params_path, f'epoch_{best_epoch}.params'), weights_only=True)
-    net.load_state_dict(sd)
+    load_best(net, os.path.join(params_path, f'epoch_{best_epoch}.params'))
     net.eval()
     test_loss = eval_batches(net, test_x, test_y, bs, nn.SmoothL1Loss())
     if rank == 0:

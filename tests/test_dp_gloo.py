@@ -105,7 +105,7 @@ def test_shard_batch_partitions():
     assert torch.equal(torch.cat(parts), t)
 
 
-def _flat_worker(rank, world, port, q):
+def _flat_worker(rank, world, port, q, early=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -120,7 +120,11 @@ def _flat_worker(rank, world, port, q):
         extra.grad = torch.full((7,), float(rank + 1))
         named = [(f"p{i}", p) for i, p in enumerate(params)] + [("extra", extra)]
         red = GradAllReducer(named)
+        if early:  # the block's backward handing its flat buffer over (attach / grads_ready)
+            red.on_grads_ready(flat)
+            assert len(red._inflight) == 1
         n = red.all_reduce()
+        assert not red._inflight
         mean = sum(r + 1 for r in range(world)) / world
         ok = torch.allclose(flat, torch.arange(25, dtype=torch.float32) * mean) and \
             torch.allclose(extra.grad, torch.full((7,), mean)) and params[0].grad.data_ptr() == flat.data_ptr()
@@ -129,12 +133,13 @@ def _flat_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_flat_gradient_buffer_reduced_in_place():
+@pytest.mark.parametrize("early", [False, True])
+def test_flat_gradient_buffer_reduced_in_place(early):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_flat_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_flat_worker, args=(r, world, port, q, early)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=120) for _ in range(world)]

@@ -9,7 +9,7 @@ Adam steps at lr 1e-3 every parameter tensor agrees to <= 1e-4 * max(1, |p|) (me
 LayerNorm-over-C backward (model/DSTAGNN_my.py:252), which cancels exactly wherever the ReLUs
 pass (sum_c dLN/dx_c = 0); as training proceeds it becomes rounding-level and Adam's
 normalised step turns fp32 summation-order noise into O(lr) moves.  (Its gradient itself
-matches the oracle to 1e-6 relative — scripts/dbg_train_grad.py, train mode, at init.)
+matches the oracle to 1e-6 relative — tools/dbg_train_grad.py, train mode, at init.)
 It is held to lr * steps / 4.
 """
 import os

@@ -127,7 +127,15 @@ def _worker(rank, world, port, bs, q, outdir):
         torch.manual_seed(5)
         best, bv, hist = TR.fit(net, x, y, vx, vy, epochs=2, batch_size=bs, lr=1e-2, params_path=outdir,
                                 log=lambda *_: None)
-        q.put((rank, {k: v.numpy().copy() for k, v in net.state_dict().items()}, [h["val_loss"] for h in hist], best))
+        final = {k: v.numpy().copy() for k, v in net.state_dict().items()}
+        # the best checkpoint: rank 0 reads the file, rank 1 gets it by broadcast
+        if rank == 1:
+            with torch.no_grad():
+                for p in net.parameters():
+                    p.zero_()
+        TR.load_best(net, os.path.join(outdir, f"epoch_{best}.params"))
+        loaded = {k: v.numpy().copy() for k, v in net.state_dict().items()}
+        q.put((rank, final, [h["val_loss"] for h in hist], best, loaded))
     finally:
         dist.destroy_process_group()
 
@@ -151,10 +159,13 @@ def test_dp_world2_equals_single_process(tmp_path):
     torch.manual_seed(5)
     best, bv, hist = TR.fit(net, x, y, vx, vy, epochs=2, batch_size=8, lr=1e-2, params_path=_tmp(),
                             log=lambda *_: None)
-    for rank, sd, vals, b in res:
+    for rank, sd, vals, b, loaded in res:
         for k, v in net.state_dict().items():
             assert torch.allclose(torch.from_numpy(sd[k]), v, atol=2e-6), (rank, k)
         assert b == best
+        ck = torch.load(os.path.join(str(tmp_path), f"epoch_{b}.params"), weights_only=True)
+        for k, v in ck.items():
+            assert torch.equal(torch.from_numpy(loaded[k]), v), (rank, k)
     # validation batches are split over the ranks and reduced: both ranks report the same
     # mean (batch size 4 there vs 8 here, so only the two ranks are compared)
     assert res[0][2] == pytest.approx(res[1][2], rel=1e-12)

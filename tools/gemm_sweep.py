@@ -4,8 +4,8 @@ GEMM shapes (PEMS08, B=32).  Each (tile config, implementation) runs in its own 
 because the overrides (DSTAGNN_GEMM_CFG / DSTAGNN_GEMM_IMPL) are read once per process;
 every run is checked against torch.bmm.
 
-    python scripts/gemm_sweep.py            # full sweep, prints a table
-    python scripts/gemm_sweep.py --child    # (internal) one config
+    python tools/gemm_sweep.py            # full sweep, prints a table
+    python tools/gemm_sweep.py --child    # (internal) one config
 """
 import argparse
 import ctypes

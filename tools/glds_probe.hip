@@ -3,7 +3,7 @@
 //     global source?  (LDS slot written by lane l of an instruction with offset 1024)
 //  2. issue cost: cycles per DMA instruction for (a) M0 save/set/restore around every
 //     instruction, (b) one M0 per batch of 4 with the LDS step carried by the offset.
-//   hipcc -O3 --offload-arch=gfx950 scripts/glds_probe.hip -o build/glds_probe && build/glds_probe
+//   hipcc -O3 --offload-arch=gfx950 tools/glds_probe.hip -o build/glds_probe && build/glds_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>

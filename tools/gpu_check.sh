@@ -26,7 +26,7 @@ for s in "${S[@]}"; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    sweep)  run gemm_sweep 600 python scripts/gemm_sweep.py ;;
+    sweep)  run gemm_sweep 600 python tools/gemm_sweep.py ;;
     *) echo "unknown step $s" ;;
   esac
 done

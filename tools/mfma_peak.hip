@@ -1,6 +1,6 @@
 // Achievable fp32-MFMA rate on this part (v_mfma_f32_32x32x2_f32), as a calibration for
 // the GEMM roofline: NACC independent accumulators per wave, WPB waves per workgroup.
-//   hipcc -O3 --offload-arch=gfx950 scripts/mfma_peak.hip -o build/mfma_peak && build/mfma_peak
+//   hipcc -O3 --offload-arch=gfx950 tools/mfma_peak.hip -o build/mfma_peak && build/mfma_peak
 #include <hip/hip_runtime.h>
 #include <cstdio>
 

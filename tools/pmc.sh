@@ -15,7 +15,7 @@ pass() {  # name, counters..., -- cmd
   echo "== rc=$rc"; tail -3 gpurun_out/pmc/$name.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-GEMM="python3 scripts/gemm_sweep.py --child --iters 5 --only preconv"
+GEMM="python3 tools/gemm_sweep.py --child --iters 5 --only preconv"
 pass fetch FETCH_SIZE -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --hot-iters 5
 pass write WRITE_SIZE -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --hot-iters 5
 pass sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- $GEMM

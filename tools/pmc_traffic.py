@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """HBM traffic of the hot kernel from the separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
-(scripts/pmc.sh) -> profiles/hot_kernel_traffic.json, read by bench.py's roofline.traffic.
+(tools/pmc.sh) -> profiles/hot_kernel_traffic.json, read by bench.py's roofline.traffic.
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch (TCC_EA0 request counters).  The guide's
 ½-count correction (MI355X_MICROARCH.md, HBM section) is calibrated for 16-B-per-lane streaming

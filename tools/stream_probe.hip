@@ -1,5 +1,5 @@
 // Host cost of launches on one stream vs alternating streams, and of event fork/join.
-//   hipcc -O3 --offload-arch=gfx950 scripts/stream_probe.hip -o build/stream_probe
+//   hipcc -O3 --offload-arch=gfx950 tools/stream_probe.hip -o build/stream_probe
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
