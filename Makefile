@@ -7,8 +7,22 @@ OBJ := $(patsubst dstagnn_drought_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := dstagnn_drought_amd/libdstagnn.so
 # host build of the EMD solver for the CPU tests only (the package never loads it)
 EMD_HOST := tests/native/libemd_host.so
+# the PyTorch-ROCm operator library (TORCH_LIBRARY(dstagnn, ...)) over libdstagnn.so
+EXT := dstagnn_drought_amd/_C.so
+PY ?= python3
+TORCH_DIR := $(shell $(PY) -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
+TORCH_ABI := $(shell $(PY) -c "import torch; print(int(torch._C._GLIBCXX_USE_CXX11_ABI))" 2>/dev/null)
+EXT_FLAGS := -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI=$(TORCH_ABI) \
+	-I/opt/rocm/include -I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include -Wno-unused-result
+EXT_LIBS := -L$(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip \
+	-Ldstagnn_drought_amd -ldstagnn -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
 
-all: $(LIB) $(EMD_HOST)
+all: $(LIB) $(EXT) $(EMD_HOST)
+
+$(EXT): dstagnn_drought_amd/csrc/torch_ops.cpp include/dstagnn.h $(LIB)
+	@mkdir -p build
+	$(HIPCC) $(EXT_FLAGS) -x c++ -c $< -o build/torch_ops.o
+	$(HIPCC) -shared -o $@ build/torch_ops.o $(EXT_LIBS)
 
 $(EMD_HOST): tests/native/emd_host.cpp dstagnn_drought_amd/csrc/emd_simplex.hpp
 	g++ -O2 -std=c++17 -fPIC -shared -Wall -o $@ $<
@@ -21,6 +35,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 clean:
-	rm -rf build $(LIB) $(EMD_HOST)
+	rm -rf build $(LIB) $(EXT) $(EMD_HOST)
 
 .PHONY: all clean

@@ -15,7 +15,6 @@ live with HIP events on the stream it runs on; `cpu_baseline` is the CPU oracle
 this host's cores on a bounded sample.
 """
 import argparse
-import ctypes
 import json
 import os
 import socket
@@ -259,7 +258,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from dstagnn_drought_amd import _lib
-    from dstagnn_drought_amd.block_fn import make_dims, workspace_sizes, _fill, graph_struct, use_sparse
+    from dstagnn_drought_amd import block_fn as bf
 
     blk, cheb, apa = build_block(dev)
     c = CFG
@@ -308,26 +307,14 @@ def main():
     value = world * B * args.steps / elapsed
 
     # ---- dominant kernel: the pre_conv fwd GEMM (gemm_f32_hot_kernel), HIP events on its stream
-    meta = dict(blk.meta, train=True, seed=1)
-    graph = blk.cheb_conv_SAt.graph(blk.adj_pa)
-    dims = make_dims(x, meta, _lib.RES_BCAST, True, 1, use_sparse(graph, meta, c["T"]))
-    sv, sc = workspace_sizes(dims)
-    save = torch.empty(sv, dtype=torch.uint8, device=dev)
-    scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
-    names, ps = zip(*blk.named_parameters())
-    pstruct = _fill(_lib.BlockParams(), names, ps)
-    gstruct = graph_struct(graph)
-    out = torch.empty(B, c["N"], c["C"], c["T"], device=dev)
-    re_at = torch.empty(B, c["C"], c["n_heads"], c["T"], c["T"], device=dev)
-    lib = _lib.load()
-    st = _lib.stream_handle(dev)
-    args_common = (ctypes.byref(dims), ctypes.byref(pstruct), ctypes.byref(gstruct), _lib.ptr(x), _lib.ptr(res),
-                   _lib.ptr(out), _lib.ptr(re_at), _lib.ptr(save), sv, _lib.ptr(scratch), sc)
-    _lib.check(lib.dstagnn_block_forward(*args_common, st), "forward")
-    ms = ctypes.c_float(0)
-    _lib.check(lib.dstagnn_block_time_stage(*args_common, 10, 3, ctypes.byref(ms), st), "hot warmup")
-    _lib.check(lib.dstagnn_block_time_stage(*args_common, 10, args.hot_iters, ctypes.byref(ms), st), "hot timing")
-    hot_ms = ms.value
+    ops = _lib.load()
+    names, ps, slots = blk._param_list()
+    graph = blk._graph()
+    sparse = bf.use_sparse(graph, blk.meta, c["T"])
+    targs = (x, res, list(ps), slots, bf.graph_list(graph, sparse), bf.cfg_of(blk.meta), 0.05, 1,
+             bf.flags_of(True, sparse, False))
+    ops.block_time_stage(*targs, 10, 3)
+    hot_ms = ops.block_time_stage(*targs, 10, args.hot_iters)
     M, Nn, Kk = B * c["N"], c["d_model"], c["C"] * c["T"]
     hot_flops = 2.0 * M * Nn * Kk
     achieved = hot_flops / (hot_ms * 1e-3) / 1e12

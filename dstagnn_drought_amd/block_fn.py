@@ -1,86 +1,62 @@
-"""torch.autograd.Function over the HIP block (libdstagnn.so).
+"""Host side of the HIP DSTAGNN_block: the call into ``torch.ops.dstagnn.block``.
 
-One forward call and one backward call per DSTAGNN_block: every stage of
-model/DSTAGNN_my.py:225-253 and its gradient runs in our own gfx950 kernels,
-launched on torch's current HIP stream.  PyTorch only provides the device
-memory (caching allocator) and the stream.
+``dstagnn::block`` (csrc/torch_ops.cpp) is ONE C++ autograd node per block: its forward is
+one ``dstagnn_block_forward`` call and its backward one ``dstagnn_block_backward`` call, so
+every stage of model/DSTAGNN_my.py:225-253 and its gradient runs in our own gfx950 kernels
+on torch's current HIP stream.  PyTorch only provides the device memory (caching
+allocator), the stream and the autograd engine.  This module maps the reference's
+parameter names onto the library's parameter slots and builds the call's arguments.
 """
-import ctypes
 import os
 
 import torch
 
 from . import _lib
 
-# block-local state_dict name -> (struct field, index or None)
-PARAM_MAP = {
-    "pre_conv.weight": ("pre_conv_w", None), "pre_conv.bias": ("pre_conv_b", None),
-    "EmbedT.pos_embed.weight": ("embT_pos", None), "EmbedT.norm.weight": ("embT_g", None),
-    "EmbedT.norm.bias": ("embT_b", None),
-    "EmbedS.pos_embed.weight": ("embS_pos", None), "EmbedS.norm.weight": ("embS_g", None),
-    "EmbedS.norm.bias": ("embS_b", None),
-    "TAt.W_Q.weight": ("tat_wq", None), "TAt.W_K.weight": ("tat_wk", None), "TAt.W_V.weight": ("tat_wv", None),
-    "TAt.fc.weight": ("tat_fc", None), "TAt.layer_norm.weight": ("tat_ln_g", None),
-    "TAt.layer_norm.bias": ("tat_ln_b", None),
-    "SAt.W_Q.weight": ("sat_wq", None), "SAt.W_K.weight": ("sat_wk", None),
-    "gtu3.con2out.weight": ("gtu_w", 0), "gtu3.con2out.bias": ("gtu_b", 0),
-    "gtu5.con2out.weight": ("gtu_w", 1), "gtu5.con2out.bias": ("gtu_b", 1),
-    "gtu7.con2out.weight": ("gtu_w", 2), "gtu7.con2out.bias": ("gtu_b", 2),
-    "residual_conv.weight": ("res_w", None), "residual_conv.bias": ("res_b", None),
-    "fcmy.0.weight": ("fcmy_w", None), "fcmy.0.bias": ("fcmy_b", None),
-    "ln.weight": ("ln_g", None), "ln.bias": ("ln_b", None),
-}
+# block-local state_dict name -> slot in dstagnn_block_params (include/dstagnn.h: the struct
+# is an array of 44 pointers in this order)
+_FIELDS = ["pre_conv.weight", "pre_conv.bias", "EmbedT.pos_embed.weight", "EmbedT.norm.weight",
+           "EmbedT.norm.bias", "EmbedS.pos_embed.weight", "EmbedS.norm.weight", "EmbedS.norm.bias",
+           "TAt.W_Q.weight", "TAt.W_K.weight", "TAt.W_V.weight", "TAt.fc.weight", "TAt.layer_norm.weight",
+           "TAt.layer_norm.bias", "SAt.W_Q.weight", "SAt.W_K.weight"]
+PARAM_SLOT = {n: i for i, n in enumerate(_FIELDS)}
 for _k in range(_lib.MAX_K):
-    PARAM_MAP[f"cheb_conv_SAt.Theta.{_k}"] = ("theta", _k)
-    PARAM_MAP[f"cheb_conv_SAt.mask.{_k}"] = ("mask", _k)
+    PARAM_SLOT[f"cheb_conv_SAt.Theta.{_k}"] = 16 + _k
+    PARAM_SLOT[f"cheb_conv_SAt.mask.{_k}"] = 16 + _lib.MAX_K + _k
+for _q, _ks in enumerate((3, 5, 7)):
+    PARAM_SLOT[f"gtu{_ks}.con2out.weight"] = 32 + _q
+    PARAM_SLOT[f"gtu{_ks}.con2out.bias"] = 35 + _q
+PARAM_SLOT.update({"residual_conv.weight": 38, "residual_conv.bias": 39, "fcmy.0.weight": 40, "fcmy.0.bias": 41,
+                   "ln.weight": 42, "ln.bias": 43})
 
 # parameters a block of each kind never touches (quirk 11: their .grad stays None)
 UNUSED_INNER = ("EmbedT.", "residual_conv.")
 
-
-def _fill(struct, names, tensors):
-    for n, t in zip(names, tensors):
-        if t is None:
-            continue
-        field, i = PARAM_MAP[n]
-        if i is None:
-            setattr(struct, field, t.data_ptr())
-        else:
-            getattr(struct, field)[i] = t.data_ptr()
-    return struct
+# DSTAGNN_POISON=1: every buffer the library writes starts as NaN (a read of memory the
+# kernels never wrote shows up as NaN instead of as whatever the allocator handed back)
+_POISON = os.environ.get("DSTAGNN_POISON", "0") == "1"
 
 
-def res_mode_of(res_att, F):
+def slots_of(names):
+    return [PARAM_SLOT[n] for n in names]
+
+
+def res_arg(res_att, F):
+    """res_att as the op takes it: None for the int 0 the first block receives
+    (DSTAGNN_submodule.forward:273), else a contiguous float tensor.  Shape errors are
+    raised by the op with the reference's message."""
     if not torch.is_tensor(res_att):
         if res_att != 0:
             raise RuntimeError("res_att must be 0 or a tensor (model/DSTAGNN_my.py:37)")
-        return _lib.RES_NONE
-    if res_att.dim() != 5:
-        raise RuntimeError(f"res_att must be 5-D (B,F|1,h,T,T), got {tuple(res_att.shape)}")
-    if res_att.shape[1] == F:
-        return _lib.RES_FULL
-    if res_att.shape[1] == 1:
-        return _lib.RES_BCAST
-    raise RuntimeError(f"The size of tensor a ({F}) must match the size of tensor b ({res_att.shape[1]}) "
-                       "at non-singleton dimension 1")
+        return None
+    return res_att.float().contiguous()
 
 
-def make_dims(x, meta, res_mode, train, seed, sparse=0):
-    B, N, F, T = x.shape
-    return _lib.BlockDims(B, N, F, T, meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"],
-                          meta["C"], res_mode, 1 if train else 0, float(meta.get("drop_p", 0.05)), seed, int(sparse))
-
-
-def graph_struct(graph):
-    """dstagnn_graph from a dict of device tensors: cheb (K,N,N), adj_pa (N,N) and, for the
-    sparse path, int32 csc_ptr / csc_row / csr_ptr / csr_col of the union support."""
-    g = _lib.Graph()
-    g.cheb = graph["cheb"].data_ptr()
-    g.adj_pa = graph["adj_pa"].data_ptr()
-    if graph.get("csc_row") is not None:
-        g.nnz = int(graph["csc_row"].numel())
-        for k in ("csc_ptr", "csc_row", "csr_ptr", "csr_col"):
-            setattr(g, k, graph[k].data_ptr())
+def graph_list(graph, sparse):
+    """[cheb (K,N,N), adj_pa (N,N)] + the int32 CSC/CSR union support for the sparse path."""
+    g = [graph["cheb"], graph["adj_pa"]]
+    if sparse:
+        g += [graph["csc_ptr"], graph["csc_row"], graph["csr_ptr"], graph["csr_col"]]
     return g
 
 
@@ -93,164 +69,27 @@ def use_sparse(graph, meta, T):
     return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= (1 << 20)
 
 
-_SIZES = {}
-# DSTAGNN_POISON=1: every buffer the library writes starts as NaN (a read of memory the
-# kernels never wrote shows up as NaN instead of as whatever the allocator handed back)
-_POISON = os.environ.get("DSTAGNN_POISON", "0") == "1"
+def cfg_of(meta):
+    return [meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"], meta["C"]]
 
 
-def workspace_sizes(dims):
-    key = bytes(dims)
-    r = _SIZES.get(key)
-    if r is None:
-        lib = _lib.load()
-        sv, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
-        _lib.check(lib.dstagnn_block_sizes(ctypes.byref(dims), ctypes.byref(sv), ctypes.byref(sc)),
-                   "dstagnn_block_sizes")
-        r = _SIZES[key] = (sv.value, sc.value)
-    return r
+def flags_of(train, sparse, direct):
+    return ((_lib.F_TRAIN if train else 0) | (_lib.F_SPARSE if sparse else 0) | (_lib.F_DIRECT if direct else 0)
+            | (_lib.F_POISON if _POISON else 0))
 
 
-# host-side caches for the per-call argument structs (the block is launch-bound on the host
-# at the benchmark size): keyed by the device pointers they hold
-_PSTRUCT = {}
-_GSTRUCT = {}
-
-
-def _params_struct(names, params):
-    key = (names, tuple(t.data_ptr() for t in params))
-    st = _PSTRUCT.get(key)
-    if st is None:
-        if len(_PSTRUCT) > 64:
-            _PSTRUCT.clear()
-        st = _PSTRUCT[key] = _fill(_lib.BlockParams(), names, params)
-    return st
-
-
-def _graph_struct_cached(graph):
-    key = tuple((k, v.data_ptr(), v.numel()) for k, v in graph.items() if v is not None)
-    st = _GSTRUCT.get(key)
-    if st is None:
-        if len(_GSTRUCT) > 64:
-            _GSTRUCT.clear()
-        st = _GSTRUCT[key] = graph_struct(graph)
-    return st
-
-
-_GLAYOUT = {}
-
-
-def _grad_layout(names, params, first):
-    """(used mask, total elements) of the flat gradient buffer: the used parameters' gradients
-    packed back to back in parameter order (adjacent Q|K|V, Q'|K', Theta_k slots let the
-    library write the stacked weight gradients in place)."""
-    key = (names, tuple(tuple(t.shape) for t in params), first)
-    lay = _GLAYOUT.get(key)
-    if lay is None:
-        used = tuple(first or not n.startswith(UNUSED_INNER) for n in names)
-        total = sum(t.numel() for t, u in zip(params, used) if u)
-        lay = _GLAYOUT[key] = (used, total)
-    return lay
-
-
-class DSTAGNNBlockFunction(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, meta, names, x, res_att, graph, *params):
-        lib = _lib.load()
-        ctx.set_materialize_grads(False)
-        dev = x.device
-        x = x.contiguous()
-        B, N, F, T = x.shape
-        mode = res_mode_of(res_att if res_att is not None else 0, F)
-        ra = res_att.contiguous() if mode != _lib.RES_NONE else None
-        train = bool(meta.get("train", False))
-        seed = int(meta.get("seed", 0))
-        dims = make_dims(x, meta, mode, train, seed, use_sparse(graph, meta, T))
-        sv, sc = workspace_sizes(dims)
-        save = torch.empty(sv, dtype=torch.uint8, device=dev)
-        scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
-        out = torch.empty(B, N, meta["C"], T, dtype=torch.float32, device=dev)
-        re_at = torch.empty(B, F, meta["n_heads"], T, T, dtype=torch.float32, device=dev)
-        if _POISON:
-            for t in (save, scratch, out, re_at):
-                t.fill_(0xFF)  # all-ones bytes = NaN floats
-        p = _params_struct(names, params)
-        g = _graph_struct_cached(graph)
-        rc = lib.dstagnn_block_forward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
-                                       _lib.ptr(ra), _lib.ptr(out), _lib.ptr(re_at), _lib.ptr(save), sv,
-                                       _lib.ptr(scratch), sc, _lib.stream_handle(dev))
-        _lib.check(rc, "dstagnn_block_forward")
-        del scratch
-        ctx.meta, ctx.names, ctx.mode, ctx.dims, ctx.graph = meta, names, mode, dims, graph
-        ctx.save_buf, ctx.sizes = save, (sv, sc)
-        ctx.save_for_backward(x, ra if ra is not None else torch.empty(0, device=dev), *params)
-        # direct-grad mode (set_direct_grads): the backward stores the parameter gradients in
-        # .grad itself instead of returning them through 36 AccumulateGrad nodes
-        ctx.direct_params = params if meta.get("direct_grads") else None
-        return out, re_at
-
-    @staticmethod
-    def backward(ctx, d_out, d_re_at):
-        lib = _lib.load()
-        x, ra, *params = ctx.saved_tensors
-        dev = x.device
-        names, mode, dims = ctx.names, ctx.mode, ctx.dims
-        if d_out is None:
-            d_out = torch.zeros(dims.B, dims.N, dims.C, dims.T, device=dev)
-        d_out = d_out.contiguous()
-        d_re_at = d_re_at.contiguous() if d_re_at is not None else None
-        first = dims.F == 1
-        # every parameter gradient is a view of ONE flat buffer: one allocation per
-        # backward instead of one per parameter (autograd adopts the views as .grad)
-        used, total = _grad_layout(names, params, first)
-        flat = torch.empty(total, dtype=torch.float32, device=dev)
-        views = iter(torch._utils._unflatten_dense_tensors(flat, [t for t, u in zip(params, used) if u]))
-        grads = [next(views) if u else None for u in used]
-        gs = _fill(_lib.BlockGrads(), names, grads)
-        p = _params_struct(names, params)
-        g = _graph_struct_cached(ctx.graph)
-        d_x = torch.empty_like(x)
-        d_ra = torch.empty_like(ra) if mode != _lib.RES_NONE else None
-        sv, sc = ctx.sizes
-        scratch = torch.empty(sc, dtype=torch.uint8, device=dev)
-        if _POISON:
-            for t in (scratch, flat, d_x) + ((d_ra,) if d_ra is not None else ()):
-                t.fill_(float("nan") if t.is_floating_point() else 0xFF)
-        rc = lib.dstagnn_block_backward(ctypes.byref(dims), ctypes.byref(p), ctypes.byref(g), _lib.ptr(x),
-                                        _lib.ptr(ra if mode != _lib.RES_NONE else None), _lib.ptr(d_out),
-                                        _lib.ptr(d_re_at), _lib.ptr(d_x), _lib.ptr(d_ra), ctypes.byref(gs),
-                                        _lib.ptr(ctx.save_buf), sv, _lib.ptr(scratch), sc,
-                                        _lib.stream_handle(dev))
-        _lib.check(rc, "dstagnn_block_backward")
-        ctx.save_buf = None
-        if ctx.direct_params is not None:
-            fresh = True
-            for prm, g in zip(ctx.direct_params, grads):
-                if g is None or not prm.requires_grad:
-                    continue
-                if prm.grad is None:
-                    prm.grad = g
-                else:
-                    prm.grad.add_(g)
-                    fresh = False
-            grads = [None] * len(grads)
-            # DP (dp.GradAllReducer.attach): this block's gradients are final and packed in
-            # ONE flat buffer -> its all-reduce starts now, beside the rest of the backward
-            hook = ctx.meta.get("grads_ready")
-            if hook is not None and fresh:
-                hook(flat)
-        return (None, None, d_x, d_ra, None, *grads)
+def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False):
+    """(out, re_at) = dstagnn::block(...) — autograd-tracked."""
+    ops = _lib.load()
+    x = x.float().contiguous()
+    sparse = use_sparse(graph, meta, x.shape[3])
+    return ops.block(x, res_arg(res_att, x.shape[2]), list(params), slots, graph_list(graph, sparse), cfg_of(meta),
+                     float(meta.get("drop_p", 0.05)), int(seed), flags_of(train, sparse, direct))
 
 
 def dropout_masks(meta, x_shape, seed):
     """The exact keep-masks (scaled by 1/(1-p)) the HIP forward draws for `seed`:
     (mask after EmbedS (B,N,D), mask after fcmy (B,N,C,T)) — for parity tests."""
-    lib = _lib.load()
-    B, N, F, T = x_shape
-    dims = _lib.BlockDims(B, N, F, T, meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"],
-                          meta["C"], 0, 1, float(meta.get("drop_p", 0.05)), seed)
-    m0 = torch.empty(B, N, meta["d_model"], device="cuda")
-    m1 = torch.empty(B, N, meta["C"], T, device="cuda")
-    _lib.check(lib.dstagnn_dropout_mask(ctypes.byref(dims), 0, _lib.ptr(m0), _lib.stream_handle()), "mask0")
-    _lib.check(lib.dstagnn_dropout_mask(ctypes.byref(dims), 1, _lib.ptr(m1), _lib.stream_handle()), "mask1")
-    return m0, m1
+    ops = _lib.load()
+    like = torch.empty(0, device="cuda")
+    return ops.dropout_masks(like, list(x_shape), cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed))

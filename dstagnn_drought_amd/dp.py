@@ -51,19 +51,43 @@ class GradAllReducer:
 
     def attach(self, model):
         """Overlap the exchange with the backward: every DSTAGNN_block of `model` in
-        direct-grad mode hands its flat gradient buffer over the moment its backward is done
-        (block_fn: meta["grads_ready"]), and its all-reduce is issued asynchronously there
-        (RCCL runs it on its own stream beside the next block's backward kernels).
-        all_reduce() then waits for those and reduces what is left (the head's grads)."""
+        direct-grad mode hands its gradients over the moment its backward node has run (a
+        post-hook on the dstagnn::block node, model.DSTAGNN_block.grads_ready); their flat
+        buffer's all-reduce is issued asynchronously there (RCCL runs it on its own stream
+        beside the next block's backward kernels).  all_reduce() then waits for those and
+        reduces what is left (the head's grads)."""
         from .model import DSTAGNN_block
         for m in model.modules():
             if isinstance(m, DSTAGNN_block):
                 m.grads_ready = self.on_grads_ready
         return self
 
-    def on_grads_ready(self, flat):
-        if flat.numel() * 4 > self.dense_limit:
-            return  # the masks are sent as their support by all_reduce()
+    @staticmethod
+    def block_flat_grad(block):
+        """The one flat buffer the HIP backward packed this block's gradients into (their
+        common ``_base``), or None when the gradients are not exactly that (accumulated into
+        pre-existing tensors, or not written directly)."""
+        if not block.direct_grads:
+            return None  # AccumulateGrad has not run yet when the node's post-hook fires
+        base, n = None, 0
+        for p in block.parameters():
+            g = p.grad
+            if g is None:
+                continue
+            b = g._base
+            if b is None or (base is not None and b is not base):
+                return None
+            base, n = b, n + g.numel()
+        if base is None or n != base.numel() or not base.is_contiguous():
+            return None
+        return base
+
+    def on_grads_ready(self, block):
+        flat = self.block_flat_grad(block)
+        if flat is None or flat.numel() * 4 > self.dense_limit:
+            return  # reduced by all_reduce() (masks as their support only on the large graphs)
+        if any(f.data_ptr() == flat.data_ptr() for f, _ in self._inflight):
+            return
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._inflight.append((flat, work))
 

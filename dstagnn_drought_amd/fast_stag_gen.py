@@ -42,15 +42,9 @@ def distances_device(coords, feats, max_distance=10.0, device=None):
     if c.dim() == 1:
         c = c[:, None]
     c, f = c.contiguous(), f.contiguous()
-    N = c.shape[0]
-    if f.shape[0] != N:
+    if f.shape[0] != c.shape[0]:
         raise ValueError("coords and features disagree on the node count")
-    sta = torch.empty(N, N, dtype=torch.float64, device=dev)
-    lib = _lib.load()
-    _lib.check(lib.dstagnn_fast_stag_distances(_lib.ptr(c), N, c.shape[1], _lib.ptr(f), f.shape[1],
-                                               float(max_distance), _lib.ptr(sta), _lib.stream_handle(dev)),
-               "dstagnn_fast_stag_distances")
-    return sta
+    return _lib.load().fast_stag_distances(c, f, float(max_distance))
 
 
 def calculate_distances(coords, data_reduced, max_distance=10.0, device=None):

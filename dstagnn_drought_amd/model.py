@@ -5,9 +5,9 @@ identical state_dict keys) and construction order (hence the
 identical RNG-driven make_model init, quirk 9) as the reference.  The compute
 of DSTAGNN_block — temporal attention, pre_conv, spatial attention,
 cheb_conv_withSAt, the three GTUs, fcmy, residual and LayerNorms, forward AND
-backward — runs in libdstagnn.so (hand-written gfx950 kernels) through
-DSTAGNNBlockFunction.  There is no CPU/eager fallback: a block called on a
-non-HIP tensor raises.
+backward — runs in libdstagnn.so (hand-written gfx950 kernels) through ONE
+C++ autograd op per block, ``torch.ops.dstagnn.block`` (csrc/torch_ops.cpp).
+There is no CPU/eager fallback: a block called on a non-HIP tensor raises.
 
 Differences from the reference that do not change results:
   * adj_pa and the Chebyshev polynomials are non-persistent buffers (they follow
@@ -18,7 +18,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .block_fn import DSTAGNNBlockFunction
+from .block_fn import block_call, slots_of
 from .head_fn import DSTAGNNHeadFunction
 from .graph import cheb_polynomial, scaled_Laplacian
 
@@ -191,7 +191,7 @@ class DSTAGNN_block(nn.Module):
         self.nb_time_filter = nb_time_filter
         self.sparse_cheb = True  # use the CSC/CSR support path when the support is sparse
         self.direct_grads = False  # see set_direct_grads
-        self.grads_ready = None    # DP hook: called with the block's flat gradient buffer
+        self.grads_ready = None    # DP hook: called with the block once its gradients are final
 
     def forward(self, x, res_att):
         B, N, Fd, T = x.shape
@@ -208,11 +208,17 @@ class DSTAGNN_block(nn.Module):
         # when dropout is off: like F.dropout(p=0), which consumes no random numbers)
         drop = self.training and meta.get("drop_p", 0.0) > 0.0
         meta["seed"] = _rank_seed(int(torch.randint(0, 2 ** 62, (1,)).item())) if drop else 0
-        if self.grads_ready is not None:
-            meta["grads_ready"] = self.grads_ready
-        names, params = self._param_list()
-        graph = self._graph()
-        return DSTAGNNBlockFunction.apply(meta, names, x.float(), res_att, graph, *params)
+        names, params, slots = self._param_list()
+        out, re_at = block_call(x, res_att, params, slots, self._graph(), meta, meta["train"], meta["seed"],
+                                self.direct_grads)
+        if self.grads_ready is not None and out.requires_grad:
+            # DP overlap (dp.GradAllReducer.attach): once this block's backward node has run,
+            # its parameter gradients are final — hand them over from a post-hook on the node
+            out.grad_fn.register_hook(self._post_backward)
+        return out, re_at
+
+    def _post_backward(self, grad_inputs, grad_outputs):
+        self.grads_ready(self)
 
     # host-side caches (the launch path is host-bound at these sizes): the parameter list
     # (Parameter objects survive .to()/.cuda()) and the graph dict (rebuilt when a buffer
@@ -228,9 +234,9 @@ class DSTAGNN_block(nn.Module):
                 mod_name, _, attr = n.rpartition(".")
                 mod = self.get_submodule(mod_name) if mod_name else self
                 slots.append((mod, attr, mod._parameters[attr]))
-            c = (tuple(names), tuple(params), tuple(slots))
+            c = (tuple(names), tuple(params), tuple(slots), slots_of(names))
             self.__dict__["_plist"] = c
-        return c[0], c[1]
+        return c[0], c[1], c[3]
 
     def _graph(self):
         cc = self.cheb_conv_SAt

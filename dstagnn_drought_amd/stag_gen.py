@@ -66,11 +66,7 @@ def wasserstein_distance(p, q, D, device=None):
         raise ValueError("wasserstein_distance: p, q must be (B,T) and D (B,T,T)")
     p, q = p.to(dev).contiguous(), q.to(dev).contiguous()
     D = D.reshape(B, T, T).to(dev).contiguous()
-    out = torch.empty(B, dtype=torch.float64, device=dev)
-    st = torch.empty(B, dtype=torch.int32, device=dev)
-    lib = _lib.load()
-    _lib.check(lib.dstagnn_emd_dense(_lib.ptr(p), _lib.ptr(q), _lib.ptr(D), T, B, _lib.ptr(out), _lib.ptr(st),
-                                     _lib.stream_handle(dev)), "dstagnn_emd_dense")
+    out, st = _lib.load().emd_dense(p, q, D)
     _raise_status(st.cpu().numpy(), "wasserstein_distance")
     r = out.cpu().numpy()
     return float(r[0]) if single else r
@@ -88,12 +84,7 @@ class NodeData:
             raise ValueError("data must be (T, N, F)")
         self.T, self.N, self.F = (int(s) for s in d.shape)
         self.device = dev
-        self.xhat = torch.empty(self.N, self.T, self.F, dtype=torch.float64, device=dev)
-        self.p = torch.empty(self.N, self.T, dtype=torch.float64, device=dev)
-        self.psum = torch.empty(self.N, dtype=torch.float64, device=dev)
-        lib = _lib.load()
-        _lib.check(lib.dstagnn_stag_prep(_lib.ptr(d), self.T, self.N, self.F, _lib.ptr(self.xhat), _lib.ptr(self.p),
-                                         _lib.ptr(self.psum), _lib.stream_handle(dev)), "dstagnn_stag_prep")
+        self.xhat, self.p, self.psum = _lib.load().stag_prep(d)
 
     def emd_pairs(self, pairs, with_pivots=False):
         """EMD of node pairs (P, 2) int (numpy or tensor) -> device fp64 (P,), status (P,)."""
@@ -101,15 +92,7 @@ class NodeData:
         pr = pr.to(device=self.device, dtype=torch.int32).reshape(-1, 2).contiguous()
         if pr.numel() and (int(pr.min()) < 0 or int(pr.max()) >= self.N):
             raise IndexError("node pair index out of range")
-        P = pr.shape[0]
-        out = torch.empty(P, dtype=torch.float64, device=self.device)
-        st = torch.empty(P, dtype=torch.int32, device=self.device)
-        piv = torch.empty(P, dtype=torch.int64, device=self.device) if with_pivots else None
-        lib = _lib.load()
-        _lib.check(lib.dstagnn_stag_emd_pairs(_lib.ptr(self.xhat), _lib.ptr(self.p), _lib.ptr(self.psum), self.T,
-                                              self.N, self.F, _lib.ptr(pr), P, _lib.ptr(out), _lib.ptr(st),
-                                              _lib.ptr(piv), _lib.stream_handle(self.device)),
-                   "dstagnn_stag_emd_pairs")
+        out, st, piv = _lib.load().stag_emd_pairs(self.xhat, self.p, self.psum, pr, bool(with_pivots))
         return (out, st, piv) if with_pivots else (out, st)
 
 
@@ -151,13 +134,7 @@ def adjacency(sta, sparsity, device=None):
 
 
 def _topk(s, k, mode):
-    N = s.shape[0]
-    A = torch.empty(N, N, dtype=torch.float64, device=s.device)
-    R = torch.empty_like(A)
-    nbr = torch.empty(N, k, dtype=torch.int32, device=s.device)
-    lib = _lib.load()
-    _lib.check(lib.dstagnn_graph_topk(_lib.ptr(s), N, k, mode, _lib.ptr(A), _lib.ptr(R), _lib.ptr(nbr),
-                                      _lib.stream_handle(s.device)), "dstagnn_graph_topk")
+    A, R, nbr = _lib.load().graph_topk(s.contiguous(), int(k), int(mode))
     return A.cpu().numpy(), R.cpu().numpy(), nbr.cpu().numpy()
 
 

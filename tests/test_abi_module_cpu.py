@@ -1,5 +1,6 @@
-"""CPU: C-ABI library loads and exports every symbol include/dstagnn.h declares; the Python
-surface mirrors the reference (state_dict keys, make_model init RNG order, error behaviour)."""
+"""CPU: the C-ABI library loads and exports every symbol include/dstagnn.h declares; the
+PyTorch-ROCm operator library registers every dstagnn:: op; the Python surface mirrors the
+reference (state_dict keys, make_model init RNG order, error behaviour)."""
 import ctypes
 import json
 import os
@@ -18,9 +19,21 @@ def header_functions():
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(dstagnn_\w+)\s*\(", src, re.M)))
 
 
-def test_library_exports_header_symbols():
+class BlockDims(ctypes.Structure):  # struct dstagnn_block_dims (include/dstagnn.h)
+    _fields_ = [(n, ctypes.c_int) for n in ("B", "N", "F", "T", "n_heads", "d_k", "d_v", "d_model", "K", "C",
+                                            "res_mode", "train")] + \
+        [("drop_p", ctypes.c_float), ("seed", ctypes.c_uint64), ("cheb_sparse", ctypes.c_int)]
+
+
+def c_abi():
     from dstagnn_drought_amd import _lib
-    lib = _lib.load()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.dstagnn_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def test_library_exports_header_symbols():
+    lib = c_abi()
     names = header_functions()
     assert len(names) >= 9, names
     for n in names:
@@ -28,14 +41,31 @@ def test_library_exports_header_symbols():
     assert lib.dstagnn_version() >= 1
 
 
-def test_block_sizes_and_shape_errors():
+OPS = ["block", "block_fwd", "block_bwd", "block_time_stage", "dropout_masks", "cheb_sat_fwd", "cheb_sat_bwd",
+       "gemm_f32", "head_fwd", "head_bwd", "stag_prep", "stag_emd_pairs", "stag_emd_lds_bytes", "emd_dense",
+       "fast_stag_distances", "graph_topk", "version"]
+
+
+def test_torch_ops_registered():
     from dstagnn_drought_amd import _lib
-    lib = _lib.load()
-    d = _lib.BlockDims(32, 170, 32, 12, 3, 32, 32, 512, 3, 32, 1, 1, 0.05, 0)
+    ops = _lib.load()
+    for n in OPS:
+        assert hasattr(ops, n), f"torch.ops.dstagnn.{n} missing"
+    assert ops.version() >= 1
+    assert ops.stag_emd_lds_bytes(287, 4) > 0
+    # the autograd op refuses CPU tensors loudly (no CPU path)
+    with pytest.raises(RuntimeError):
+        ops.block(torch.zeros(1, 4, 1, 12), None, [], [], [torch.zeros(3, 4, 4), torch.zeros(4, 4)],
+                  [3, 8, 8, 16, 3, 8], 0.05, 0, 0)
+
+
+def test_block_sizes_and_shape_errors():
+    lib = c_abi()
+    d = BlockDims(32, 170, 32, 12, 3, 32, 32, 512, 3, 32, 1, 1, 0.05, 0)
     sv, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
     assert lib.dstagnn_block_sizes(ctypes.byref(d), ctypes.byref(sv), ctypes.byref(sc)) == 0
     assert sv.value > 32 * 3 * 170 * 170 * 4 * 2  # P and W
-    bad = _lib.BlockDims(1, 16, 4, 12, 2, 8, 8, 16, 2, 8, 0, 0, 0.05, 0)  # GAMBIA in_channels=4 (quirk 8)
+    bad = BlockDims(1, 16, 4, 12, 2, 8, 8, 16, 2, 8, 0, 0, 0.05, 0)  # GAMBIA in_channels=4 (quirk 8)
     rc = lib.dstagnn_block_sizes(ctypes.byref(bad), ctypes.byref(sv), ctypes.byref(sc))
     assert rc == 10001
     assert b"must match" in lib.dstagnn_last_error()

@@ -120,9 +120,16 @@ def _flat_worker(rank, world, port, q, early=False):
         extra.grad = torch.full((7,), float(rank + 1))
         named = [(f"p{i}", p) for i, p in enumerate(params)] + [("extra", extra)]
         red = GradAllReducer(named)
-        if early:  # the block's backward handing its flat buffer over (attach / grads_ready)
-            red.on_grads_ready(flat)
+        if early:  # a direct-grad block's backward node handing its gradients over (attach)
+            blk = torch.nn.Module()
+            blk.ps = torch.nn.ParameterList(params)
+            blk.direct_grads = True
+            assert GradAllReducer.block_flat_grad(blk) is flat
+            red.on_grads_ready(blk)
+            red.on_grads_ready(blk)  # a second hand-over of the same buffer is ignored
             assert len(red._inflight) == 1
+            blk.direct_grads = False
+            assert GradAllReducer.block_flat_grad(blk) is None
         n = red.all_reduce()
         assert not red._inflight
         mean = sum(r + 1 for r in range(world)) / world

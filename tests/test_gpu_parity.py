@@ -1,4 +1,4 @@
-"""GPU parity: the HIP path (libdstagnn.so through its C-ABI / the autograd Function)
+"""GPU parity: the HIP path (libdstagnn.so through the torch.ops.dstagnn operators)
 against the reference's golden vectors and the CPU oracle.
 
 Tolerance (north_star: "outputs matching the CPU reference within 1e-4 fp32"):
@@ -6,7 +6,6 @@ Tolerance (north_star: "outputs matching the CPU reference within 1e-4 fp32"):
 i.e. 1e-4 absolute for O(1) tensors and 1e-4 relative to the tensor's scale for large
 gradients (sums over up to B*N*T terms in a different order than the reference).
 """
-import ctypes
 import json
 import os
 
@@ -43,19 +42,8 @@ def load(golden_dir, name):
 def _gemm(A, B, C, M, N, K, am, ak, bk, bn, cm, cn, batch=1, az=(0, 0, 0), bz=(0, 0, 0), cz=(0, 0, 0),
           alpha=1.0, beta=0.0, bias=None, relu=0, scratch_mb=64):
     from dstagnn_drought_amd import _lib
-    lib = _lib.load()
-    d = _lib.GemmDesc()
-    d.M, d.N, d.K, d.batch = M, N, K, batch
-    d.A, d.B, d.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
-    d.a_m, d.a_k, d.a_z = _lib.idx(*am), _lib.idx(*ak), _lib.idx(*az)
-    d.b_k, d.b_n, d.b_z = _lib.idx(*bk), _lib.idx(*bn), _lib.idx(*bz)
-    d.c_m, d.c_n, d.c_z = _lib.idx(*cm), _lib.idx(*cn), _lib.idx(*cz)
-    d.alpha, d.beta = alpha, beta
-    d.bias = bias.data_ptr() if bias is not None else None
-    d.bias_stride = 1
-    d.relu = relu
-    ws = torch.empty(scratch_mb << 20, dtype=torch.uint8, device="cuda")
-    _lib.check(lib.dstagnn_gemm_f32(ctypes.byref(d), _lib.ptr(ws), ws.numel(), _lib.stream_handle()), "gemm")
+    _lib.load().gemm_f32(A, B, C, [M, N, K, batch], _lib.gemm_maps(am, ak, az, bk, bn, bz, cm, cn, cz), [0, 0, 0],
+                         alpha, beta, bias, 1, bool(relu))
     torch.cuda.synchronize()
 
 
@@ -107,9 +95,8 @@ def test_gemm_transposed_batched_two_level():
 def test_cheb_sat_golden(golden_dir, name, sparse):
     _need_gpu()
     from dstagnn_drought_amd import _lib
-    from dstagnn_drought_amd.block_fn import graph_struct
     from dstagnn_drought_amd.model import support_index
-    lib = _lib.load()
+    ops = _lib.load()
     g = load(golden_dir, name)
     m = json.loads(str(g["meta"]))
     B, N, F, T, K, C = m["B"], m["N"], m["F"], m["T"], m["K"], m["C"]
@@ -120,28 +107,13 @@ def test_cheb_sat_golden(golden_dir, name, sparse):
     cheb = cu(np.stack([g[f"cheb_{k}"] for k in range(K)]))
     apa = cu(g["adj_pa"])
     csc_ptr, csc_row, csr_ptr, csr_col = [t.cuda() for t in support_index(cheb.cpu())]
-    gs = graph_struct({"cheb": cheb, "adj_pa": apa, "csc_ptr": csc_ptr, "csc_row": csc_row, "csr_ptr": csr_ptr,
-                       "csr_col": csr_col})
-    out = torch.empty(B, N, C, T, device="cuda")
-    P = torch.empty(B, K, N, N, device="cuda")
-    W = torch.empty_like(P)
-    xth = torch.empty(B, N, K, C, T, device="cuda")
-    ws = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
-    st = _lib.stream_handle()
-    pt = _lib.ptr
-    _lib.check(lib.dstagnn_cheb_sat_forward(B, N, F, T, K, C, sparse, pt(x), pt(sat), pt(thcat), pt(mcat),
-                                            ctypes.byref(gs), pt(out), pt(P), pt(W), pt(xth), pt(ws), ws.numel(), st),
-               "cheb fwd")
+    graph = [cheb, apa, csc_ptr, csc_row, csr_ptr, csr_col]
+    out, P, W, xth = ops.cheb_sat_fwd(x, sat, thcat, mcat, graph, C, bool(sparse))
     torch.cuda.synchronize()
+    assert tuple(out.shape) == (B, N, C, T) and (W.numel() == 0) == bool(sparse)
     close(out, g["out"], what="out")
     dout = cu(g["g_out"])
-    dx = torch.empty_like(x)
-    dsat = torch.empty_like(sat)
-    dth = torch.empty_like(thcat)
-    dm = torch.empty_like(mcat)
-    _lib.check(lib.dstagnn_cheb_sat_backward(B, N, F, T, K, C, sparse, pt(x), pt(thcat), ctypes.byref(gs), pt(out),
-                                             pt(P), pt(W), pt(xth), pt(dout), pt(dx), pt(dsat), pt(dth), pt(dm),
-                                             pt(ws), ws.numel(), st), "cheb bwd")
+    dx, dsat, dth, dm = ops.cheb_sat_bwd(x, thcat, graph, out, P, W, xth, dout, C, bool(sparse))
     torch.cuda.synchronize()
     close(dx, g["grad_x"], what="grad_x")
     close(dsat, g["grad_spatial_attention"], what="grad_sat")

@@ -8,7 +8,6 @@ every run is checked against torch.bmm.
     python tools/gemm_sweep.py --child    # (internal) one config
 """
 import argparse
-import ctypes
 import json
 import os
 import subprocess
@@ -63,8 +62,7 @@ if os.environ.get("DSTAGNN_SWEEP_LARGE"):
 def child(iters, only=None):
     import torch
     from dstagnn_drought_amd import _lib
-    lib = _lib.load()
-    ws = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    ops = _lib.load()
     res = {}
     for name, M, N, K, batch, akc, bnc in SHAPES:
         if only and name not in only.split(","):
@@ -72,18 +70,12 @@ def child(iters, only=None):
         A = torch.randn(batch, M, K, device="cuda") if akc else torch.randn(batch, K, M, device="cuda")
         B = torch.randn(batch, K, N, device="cuda") if bnc else torch.randn(batch, N, K, device="cuda")
         C = torch.empty(batch, M, N, device="cuda")
-        d = _lib.GemmDesc()
-        d.M, d.N, d.K, d.batch = M, N, K, batch
-        d.A, d.B, d.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
-        d.a_m, d.a_k = (_lib.idx(0, K), _lib.idx(0, 1)) if akc else (_lib.idx(0, 1), _lib.idx(0, M))
-        d.b_k, d.b_n = (_lib.idx(0, N), _lib.idx(0, 1)) if bnc else (_lib.idx(0, 1), _lib.idx(0, K))
-        d.a_z, d.b_z, d.c_z = _lib.idx(0, M * K), _lib.idx(0, K * N), _lib.idx(0, M * N)
-        d.c_m, d.c_n = _lib.idx(0, N), _lib.idx(0, 1)
-        d.alpha, d.beta, d.bias, d.bias_stride, d.relu = 1.0, 0.0, None, 1, 0
-        st = _lib.stream_handle()
+        am, ak = ((0, K), (0, 1)) if akc else ((0, 1), (0, M))
+        bk, bn = ((0, N), (0, 1)) if bnc else ((0, 1), (0, K))
+        maps = _lib.gemm_maps(am, ak, (0, M * K), bk, bn, (0, K * N), (0, N), (0, 1), (0, M * N))
 
         def run():
-            _lib.check(lib.dstagnn_gemm_f32(ctypes.byref(d), _lib.ptr(ws), ws.numel(), st), name)
+            ops.gemm_f32(A, B, C, [M, N, K, batch], maps, [0, 0, 0], 1.0, 0.0, None, 1, False)
         for _ in range(3):
             run()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -22,10 +22,11 @@ STEPS=${STEPS:-pytest,smoke,bench,prof}
 IFS=',' read -ra S <<< "$STEPS"
 for s in "${S[@]}"; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 180 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    dp2)    DSTAGNN_DIST_BACKEND=gloo DSTAGNN_DEVICE_MOD=1 run dp2 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-extras ;;
     sweep)  run gemm_sweep 600 python tools/gemm_sweep.py ;;
     *) echo "unknown step $s" ;;
   esac
