@@ -17,7 +17,11 @@ EXT_FLAGS := -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBC
 EXT_LIBS := -L$(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip \
 	-Ldstagnn_drought_amd -ldstagnn -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
 
-all: $(LIB) $(EXT) $(EMD_HOST)
+all: $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib
+
+# FETCH_SIZE / WRITE_SIZE width calibration (tools/pmc_step.sh)
+tools/fetch_calib: tools/fetch_calib.hip
+	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@
 
 $(EXT): dstagnn_drought_amd/csrc/torch_ops.cpp include/dstagnn.h $(LIB)
 	@mkdir -p build
@@ -35,6 +39,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 clean:
-	rm -rf build $(LIB) $(EXT) $(EMD_HOST)
+	rm -rf build $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib
 
 .PHONY: all clean

@@ -8,11 +8,14 @@ make_model-style init, synthetic x ~ N(0,1), seeded d_out / d_re_At.
 A step = forward + backward of one batch through the HIP library (+ the RCCL
 all-reduce of the parameter gradients when --gpus > 1: data parallel, weak scaling).
 
-Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel
-(gemm_f32_hot_kernel = the pre_conv forward GEMM, M=B*N, N=d_model, K=F*T), timed
-live with HIP events on the stream it runs on; `cpu_baseline` is the CPU oracle
-(a literal restatement of the reference's loops, oracle/dstagnn_ref.py) timed on
-this host's cores on a bounded sample.
+Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel family, the GEMMs
+(every dense contraction of the step: 27 gemm_f32 calls with their split-K folds): summed
+algorithmic FLOP over summed durations, each call bracketed by HIP events on the stream it
+runs on (dstagnn::prof_start/stop, serialised steps); `hot_kernel` keeps round 1's single
+pre_conv forward GEMM figure; `hbm_roofline` is the metric's "%HBM roofline" (memory-side
+bytes per step from the committed rocprofv3 PMC summary over this run's step time) with
+the MFMA-busy fraction; `cpu_baseline` is the CPU oracle (a literal restatement of the
+reference's loops, oracle/dstagnn_ref.py) timed on this host's cores on a bounded sample.
 """
 import argparse
 import json
@@ -120,6 +123,18 @@ def extras(dev, steps, warmup):
                             "workload": "PEMS08 first DSTAGNN_block (F=1, res_att 0) fwd+bwd, B=32"},
             "model_step": {"samples_per_s": round(B / t_model, 1), "ms_per_step": round(t_model * 1e3, 4),
                            "workload": "make_model nb_block=4 PEMS08: fwd + SmoothL1 + bwd + Adam, B=32"}}
+
+
+PMC_FILE = "profiles/block_pmc.json"
+
+
+def load_pmc():
+    """Counter summary of the same step (tools/pmc_step.sh -> tools/pmc_step_summary.py), or None."""
+    try:
+        with open(os.path.join(ROOT, PMC_FILE)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def algorithmic_flops_per_sample(c=CFG):
@@ -245,6 +260,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hot-iters", type=int, default=50)
+    ap.add_argument("--prof-steps", type=int, default=5, help="serialised steps for the GEMM-family event timing")
     ap.add_argument("--no-extras", action="store_true", help="skip the first-block / full-model lines")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -306,7 +322,6 @@ def main():
     log(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step (host issue {t_issue / args.steps * 1e3:.3f} ms/step)")
     value = world * B * args.steps / elapsed
 
-    # ---- dominant kernel: the pre_conv fwd GEMM (gemm_f32_hot_kernel), HIP events on its stream
     ops = _lib.load()
     names, ps, slots = blk._param_list()
     graph = blk._graph()
@@ -315,20 +330,44 @@ def main():
              bf.flags_of(True, sparse, False))
     ops.block_time_stage(*targs, 10, 3)
     hot_ms = ops.block_time_stage(*targs, 10, args.hot_iters)
+
+    # ---- dominant kernel family: the GEMMs (27 calls per step, the largest share of the step's
+    # kernel time).  HIP event pairs around every GEMM call (kernel + split-K fold) over
+    # --prof-steps steps run on ONE stream (dstagnn::prof_start serialises the block)
+    fam = None
+    if args.prof_steps > 0:
+        ops.prof_start(4096)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.prof_steps):
+            step()
+        torch.cuda.synchronize()
+        t_ser = (time.perf_counter() - t0) / args.prof_steps
+        launches, flops, gbytes, gms, gmax, dropped = ops.prof_stop()
+        P = args.prof_steps
+        fam = dict(launches=launches / P, flops=flops / P, bytes=gbytes / P, ms=gms / P, max_ms=gmax,
+                   serial_step_ms=t_ser * 1e3, dropped=dropped)
+    pmc = load_pmc()
+    if fam is not None:
+        achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                "traffic": pmc["gemm_family"]["bytes_corrected"] if pmc else None,
+                "kernel": "gemm_f32 family: every GEMM call of one step (kernel + split-K fold), summed",
+                "launches_per_step": round(fam["launches"], 1), "gflop_per_step": round(fam["flops"] / 1e9, 4),
+                "ms_per_step": round(fam["ms"], 4), "avg_launch_us": round(fam["ms"] / fam["launches"] * 1e3, 3),
+                "share_of_serial_step": round(fam["ms"] / fam["serial_step_ms"], 3),
+                "min_bytes_per_step": int(fam["bytes"]),
+                "timing": f"HIP events around each call, {args.prof_steps} serialised steps"}
+    else:
+        roof = None
+    # the single longest-running GEMM call site of round 1, kept for continuity: the pre_conv
+    # forward GEMM (gemm_f32_hot_kernel), back-to-back launches timed with HIP events
     M, Nn, Kk = B * c["N"], c["d_model"], c["C"] * c["T"]
-    hot_flops = 2.0 * M * Nn * Kk
-    achieved = hot_flops / (hot_ms * 1e-3) / 1e12
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "hot_kernel_traffic.json")
-    if os.path.exists(tfile):
-        try:
-            traffic = json.load(open(tfile)).get("bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
-    roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-            "kernel": "gemm_f32_hot_kernel (pre_conv fwd GEMM %dx%dx%d)" % (M, Nn, Kk),
-            "avg_launch_us": round(hot_ms * 1e3, 3)}
+    hot_achieved = 2.0 * M * Nn * Kk / (hot_ms * 1e-3) / 1e12
+    hot = {"kernel": "gemm_f32_hot_kernel (pre_conv fwd GEMM %dx%dx%d)" % (M, Nn, Kk),
+           "avg_launch_us": round(hot_ms * 1e3, 3), "achieved": round(hot_achieved, 3), "unit": "TFLOP/s",
+           "frac": round(hot_achieved / PEAK_FP32_TFLOPS, 4)}
 
     log(f"hot kernel {hot_ms * 1e3:.2f} us/launch")
     cpu = None
@@ -341,6 +380,15 @@ def main():
         ext = extras(dev, max(5, args.steps // 2), 3)
     # whole-block roofline: 758.8 MFLOP per sample fwd+bwd, compute-bound
     # (arithmetic intensity ~460 flop/B vs the fp32 ridge ~20): peak samples/s = 157.3 TF / F_alg
+    # the metric's "%HBM roofline": memory-side bytes of one step (rocprofv3 FETCH_SIZE /
+    # WRITE_SIZE passes, width-corrected: profiles/block_pmc.json) over this run's step time
+    hbm_roof = None
+    if pmc:
+        bps = pmc["step"]["bytes_corrected"]
+        gbs = bps / (ms_per_step * 1e-3) / 1e9
+        hbm_roof = {"bytes_per_step": bps, "achieved_GBs": round(gbs, 1), "peak_GBs": PEAK_HBM_GBS,
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "mfma_busy_frac": pmc["step"]["mfma_busy_frac"],
+                    "gemm_mfma_busy_frac": pmc["gemm_family"]["mfma_busy_frac"], "source": PMC_FILE}
     f_alg = algorithmic_flops_per_sample()
     peak_sps = PEAK_FP32_TFLOPS * 1e12 / f_alg
     block_roof = {"bound": "mfma", "alg_flop_per_sample": round(f_alg / 1e6, 1), "unit_flop": "MFLOP",
@@ -359,7 +407,9 @@ def main():
                        "parallelism": f"dp{world}"},
             "algorithmic_tflops": round(algorithmic_flops_per_sample() * value / 1e12, 3),
             "roofline": roof,
+            "hot_kernel": hot,
             "block_roofline": block_roof,
+            "hbm_roofline": hbm_roof,
             "cpu_baseline": cpu,
         }
         if ext is not None:

@@ -406,7 +406,7 @@ struct Streams {
   SideStream* ss = nullptr;
   void init(hipStream_t main) {
     st = main;
-    ss = side_stream_for_device();
+    ss = gemm_prof_on() ? nullptr : side_stream_for_device();
     sd = ss ? ss->side : st;
   }
   int event_pair(hipStream_t from, hipStream_t to) {
@@ -1012,6 +1012,8 @@ void* align256(void* p) { return (void*)(((uintptr_t)p + 255) & ~uintptr_t(255))
 extern "C" {
 
 const char* dstagnn_last_error(void) { return g_last_error.c_str(); }
+int dstagnn_prof_start(int capacity) { return gemm_prof_start(capacity); }
+int dstagnn_prof_stop(dstagnn_prof_stats* stats) { return gemm_prof_stop(stats); }
 int dstagnn_version(void) { return 1; }
 
 int dstagnn_block_sizes(const dstagnn_block_dims* d, size_t* save_bytes, size_t* scratch_bytes) {

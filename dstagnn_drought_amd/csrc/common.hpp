@@ -229,3 +229,8 @@ struct Gemm {
 };
 // ws: split-K partial slab scratch (may be null -> no split)
 int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st);
+// GEMM-family profiling (gemm.hip): while on, the block runs on ONE stream (no side-stream
+// overlap) so every recorded GEMM duration is its own
+bool gemm_prof_on();
+int gemm_prof_start(int capacity);
+int gemm_prof_stop(dstagnn_prof_stats* out);

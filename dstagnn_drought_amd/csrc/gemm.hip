@@ -596,10 +596,82 @@ void launch_cfg(const GemmK& k, bool akc, bool bnc, bool hot, hipStream_t st) {
 #undef DS_GEMM_LAUNCH
 }
 
+// ---------------------------------------------------------------------------------
+// GEMM-family profiling (dstagnn_prof_start / _stop): a timing event pair around every
+// run_gemm call (kernel + split-K fold) on the stream it is issued on, with its algorithmic
+// FLOP and minimum bytes, so the benchmark reports the family's achieved rate from HIP
+// events of the same run.  Off by default (one branch per call).
+// ---------------------------------------------------------------------------------
+struct ProfRec {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  double flops = 0, bytes = 0;
+};
+struct Prof {
+  bool on = false;
+  int n = 0, cap = 0, dropped = 0;
+  ProfRec* rec = nullptr;
+};
+Prof g_prof;
+
 }  // namespace
+
+bool gemm_prof_on() { return g_prof.on; }
+
+int gemm_prof_start(int capacity) {
+  if (capacity <= 0) return DSTAGNN_E_ARG;
+  if (capacity > g_prof.cap) {
+    ProfRec* r = new ProfRec[capacity];
+    for (int i = 0; i < g_prof.cap; ++i) r[i] = g_prof.rec[i];
+    for (int i = g_prof.cap; i < capacity; ++i) {
+      if (hipEventCreate(&r[i].e0) != hipSuccess || hipEventCreate(&r[i].e1) != hipSuccess) {
+        set_last_error("prof: hipEventCreate failed");
+        delete[] r;
+        return DSTAGNN_E_ARG;
+      }
+    }
+    delete[] g_prof.rec;
+    g_prof.rec = r;
+    g_prof.cap = capacity;
+  }
+  g_prof.n = 0;
+  g_prof.dropped = 0;
+  g_prof.on = true;
+  return 0;
+}
+
+int gemm_prof_stop(dstagnn_prof_stats* out) {
+  g_prof.on = false;
+  dstagnn_prof_stats s{};
+  for (int i = 0; i < g_prof.n; ++i) {
+    ProfRec& r = g_prof.rec[i];
+    if (hipEventSynchronize(r.e1) != hipSuccess) { set_last_error("prof: event sync failed"); return DSTAGNN_E_ARG; }
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.e0, r.e1) != hipSuccess) { set_last_error("prof: elapsed failed"); return DSTAGNN_E_ARG; }
+    s.launches += 1;
+    s.flops += r.flops;
+    s.bytes += r.bytes;
+    s.ms += ms;
+    s.max_ms = std::max(s.max_ms, (double)ms);
+  }
+  s.dropped = g_prof.dropped;
+  g_prof.n = 0;
+  if (out) *out = s;
+  return 0;
+}
 
 int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return 0;
+  ProfRec* prec = nullptr;
+  if (g_prof.on) {
+    if (g_prof.n < g_prof.cap) {
+      prec = &g_prof.rec[g_prof.n++];
+      prec->flops = 2.0 * g.M * g.N * (double)g.K * g.batch;
+      prec->bytes = 4.0 * g.batch * ((double)g.M * g.K + (double)g.K * g.N + (double)g.M * g.N * (g.beta != 0.f ? 2 : 1));
+      (void)hipEventRecord(prec->e0, st);
+    } else {
+      ++g_prof.dropped;
+    }
+  }
   if (!g.A || !g.B || !g.C) { set_last_error("gemm: null operand"); return DSTAGNN_E_ARG; }
   GemmK k;
   k.M = g.M; k.N = g.N; k.K = g.K; k.batch = g.batch;
@@ -692,6 +764,7 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv64(total, 256 / G)), dim3(256), 0, st, k, G);
     DS_CHECK_LAUNCH();
   }
+  if (prec) (void)hipEventRecord(prec->e1, st);
   return 0;
 }
 

@@ -622,6 +622,15 @@ std::tuple<Tensor, Tensor, Tensor> graph_topk(const Tensor& sta, int64_t k, int6
 
 int64_t library_version() { return dstagnn_version(); }
 
+// GEMM-family profiling: prof_start(capacity); ...; prof_stop() ->
+// [launches, flops, bytes, ms, max_ms, dropped]
+void prof_start(int64_t capacity) { check_rc(dstagnn_prof_start((int)capacity), "dstagnn_prof_start"); }
+std::vector<double> prof_stop() {
+  dstagnn_prof_stats s{};
+  check_rc(dstagnn_prof_stop(&s), "dstagnn_prof_stop");
+  return {s.launches, s.flops, s.bytes, s.ms, s.max_ms, s.dropped};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dstagnn, m) {
@@ -649,6 +658,8 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("fast_stag_distances(Tensor coords, Tensor feats, float max_distance) -> Tensor");
   m.def("graph_topk(Tensor sta, int k, int mode) -> (Tensor, Tensor, Tensor)");
   m.def("version() -> int", library_version);
+  m.def("prof_start(int capacity) -> ()", prof_start);
+  m.def("prof_stop() -> float[]", prof_stop);
 }
 
 // PyTorch-ROCm dispatches HIP device tensors under the CUDA key

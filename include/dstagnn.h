@@ -258,6 +258,23 @@ int dstagnn_fast_stag_distances(const double* coords, int N, int Dc, const doubl
 int dstagnn_graph_topk(const double* sta, int N, int k, int mode, double* A, double* R, int32_t* nbr,
                        dstagnn_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * GEMM-family profiling (benchmark support).  dstagnn_prof_start(capacity) arms a timing
+ * event pair around each of the next `capacity` GEMM calls (kernel + split-K fold, on the
+ * stream they are issued on) and makes the block run on ONE stream (no side-stream overlap,
+ * so each duration is that GEMM's own); dstagnn_prof_stop() synchronises and sums.
+ * ------------------------------------------------------------------------------------- */
+typedef struct dstagnn_prof_stats {
+  double launches;  /* GEMM calls recorded                                      */
+  double flops;     /* sum of 2*M*N*K*batch                                     */
+  double bytes;     /* sum of minimum operand bytes 4*(MK + KN + MN (x2 if beta)) */
+  double ms;        /* sum of event-measured durations                          */
+  double max_ms;    /* longest single call                                      */
+  double dropped;   /* calls beyond capacity (not recorded)                     */
+} dstagnn_prof_stats;
+int dstagnn_prof_start(int capacity);
+int dstagnn_prof_stop(dstagnn_prof_stats* stats);
+
 const char* dstagnn_last_error(void);
 int dstagnn_version(void);
 

@@ -27,6 +27,7 @@ for s in "${S[@]}"; do
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     dp2)    DSTAGNN_DIST_BACKEND=gloo DSTAGNN_DEVICE_MOD=1 run dp2 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-extras ;;
+    pmcs)   echo "== pmcs ($(date +%T))"; bash tools/pmc_step.sh || exit $? ;;
     sweep)  run gemm_sweep 600 python tools/gemm_sweep.py ;;
     *) echo "unknown step $s" ;;
   esac
