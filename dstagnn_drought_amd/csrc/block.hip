@@ -1013,6 +1013,7 @@ extern "C" {
 
 const char* dstagnn_last_error(void) { return g_last_error.c_str(); }
 int dstagnn_prof_start(int capacity) { return gemm_prof_start(capacity); }
+int dstagnn_set_splitk_target(int target) { return gemm_set_splitk_target(target); }
 int dstagnn_prof_stop(dstagnn_prof_stats* stats) { return gemm_prof_stop(stats); }
 int dstagnn_version(void) { return 1; }
 
@@ -1020,6 +1021,17 @@ int dstagnn_block_sizes(const dstagnn_block_dims* d, size_t* save_bytes, size_t*
   DS_TRY(check_dims(d));
   if (!save_bytes || !scratch_bytes) return DSTAGNN_E_ARG;
   plan_sizes(mkdims(*d), save_bytes, scratch_bytes);
+  return 0;
+}
+
+int dstagnn_block_save_offset(const dstagnn_block_dims* d, int which, size_t* offset_bytes, size_t* count) {
+  DS_TRY(check_dims(d));
+  if (!offset_bytes || !count || which != 0) return DSTAGNN_E_ARG;
+  const Dims m = mkdims(*d);
+  Arena a((void*)(uintptr_t)256);  // the forward carves the 256-aligned save buffer the same way
+  SaveBufs s = plan_save(m, a);
+  *offset_bytes = (size_t)((char*)s.X - (char*)(uintptr_t)256);
+  *count = (size_t)(m.BN * m.CT);
   return 0;
 }
 

@@ -234,3 +234,4 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st);
 bool gemm_prof_on();
 int gemm_prof_start(int capacity);
 int gemm_prof_stop(dstagnn_prof_stats* out);
+int gemm_set_splitk_target(int target);

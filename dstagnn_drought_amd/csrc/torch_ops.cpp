@@ -328,6 +328,18 @@ std::tuple<Tensor, Tensor, Tensor> block_bwd(const Tensor& x, const c10::optiona
   return {r.dx, r.dres.defined() ? r.dres : at::empty({0}, f32(x)), r.flat};
 }
 
+// the Chebyshev output X (B,N,T,C) the forward keeps in `save` (parity tests: its sign
+// pattern is the ReLU decision of model/DSTAGNN_my.py:133)
+Tensor block_cheb_out(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params, at::IntArrayRef slots,
+                      at::TensorList graph, at::IntArrayRef cfg, double drop_p, int64_t seed, int64_t flags) {
+  BlockCall c = make_call(x, res, params, slots, graph, cfg, drop_p, seed, flags);
+  auto [out, re_at, save] = run_forward(c, x, res);
+  size_t off = 0, n = 0;
+  check_rc(dstagnn_block_save_offset(&c.d, 0, &off, &n), "dstagnn_block_save_offset");
+  const int64_t base = (int64_t)((256 - ((uintptr_t)save.data_ptr() & 255)) & 255);  // the library's align256
+  return save.narrow(0, base + (int64_t)off, (int64_t)n * 4).view(at::kFloat).view({c.d.B, c.d.N, c.d.T, c.d.C}).clone();
+}
+
 // HIP-event timing of one block stage (dstagnn_block_time_stage) after one forward:
 // mean milliseconds per launch on the current stream
 double block_time_stage(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params,
@@ -622,6 +634,8 @@ std::tuple<Tensor, Tensor, Tensor> graph_topk(const Tensor& sta, int64_t k, int6
 
 int64_t library_version() { return dstagnn_version(); }
 
+int64_t set_splitk_target(int64_t target) { return dstagnn_set_splitk_target((int)target); }
+
 // GEMM-family profiling: prof_start(capacity); ...; prof_stop() ->
 // [launches, flops, bytes, ms, max_ms, dropped]
 void prof_start(int64_t capacity) { check_rc(dstagnn_prof_start((int)capacity), "dstagnn_prof_start"); }
@@ -641,6 +655,7 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("block_bwd(Tensor x, Tensor? res_att, Tensor d_out, Tensor? d_re_at, Tensor save, Tensor[] params, "
         "int[] slots, Tensor[] graph, int[] cfg, float drop_p, int seed, int flags) -> (Tensor, Tensor, Tensor)");
   m.def("block_time_stage(" DSTAGNN_BLK_ARGS ", int stage, int iters) -> float");
+  m.def("block_cheb_out(" DSTAGNN_BLK_ARGS ") -> Tensor");
 #undef DSTAGNN_BLK_ARGS
   m.def("dropout_masks(Tensor like, int[] shape, int[] cfg, float drop_p, int seed) -> (Tensor, Tensor)");
   m.def("cheb_sat_fwd(Tensor x, Tensor sat, Tensor theta_cat, Tensor mask_cat, Tensor[] graph, int C, bool sparse) "
@@ -659,6 +674,7 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("graph_topk(Tensor sta, int k, int mode) -> (Tensor, Tensor, Tensor)");
   m.def("version() -> int", library_version);
   m.def("prof_start(int capacity) -> ()", prof_start);
+  m.def("set_splitk_target(int target) -> int", set_splitk_target);
   m.def("prof_stop() -> float[]", prof_stop);
 }
 
@@ -669,6 +685,7 @@ TORCH_LIBRARY_IMPL(dstagnn, CUDA, m) {
   m.impl("block_bwd", block_bwd);
   m.impl("block_time_stage", block_time_stage);
   m.impl("dropout_masks", dropout_masks);
+  m.impl("block_cheb_out", block_cheb_out);
   m.impl("cheb_sat_fwd", cheb_sat_fwd);
   m.impl("cheb_sat_bwd", cheb_sat_bwd);
   m.impl("gemm_f32", gemm_f32);

@@ -136,6 +136,13 @@ int dstagnn_block_forward(const dstagnn_block_dims* d, const dstagnn_block_param
                           void* save, size_t save_bytes, void* scratch, size_t scratch_bytes,
                           dstagnn_stream_t stream);
 
+/* Introspection for parity tests: byte offset (from the 256-aligned start of `save`) and
+ * element count of a tensor the forward keeps in `save`.  which = 0: the Chebyshev output
+ * X = ReLU(cheb_conv_withSAt pre-activation), layout (B,N,T,C) — its sign pattern is the
+ * ReLU decision of :133, which an fp64 oracle can adopt where the pre-activation is within
+ * rounding of 0. */
+int dstagnn_block_save_offset(const dstagnn_block_dims* d, int which, size_t* offset_bytes, size_t* count);
+
 /* Autograd backward of the block (replaces torch autograd over :225-253).
  *   d_out (B,N,C,T); d_re_at (B,F,h,T,T) or NULL (no gradient flows into re_At)
  *   d_x (B,N,F,T) written; d_res_att written per res_mode (NULL for mode 0)
@@ -274,6 +281,12 @@ typedef struct dstagnn_prof_stats {
 } dstagnn_prof_stats;
 int dstagnn_prof_start(int capacity);
 int dstagnn_prof_stop(dstagnn_prof_stats* stats);
+
+/* Split-K policy of the GEMMs: a GEMM with a grid below 128 workgroups splits its K range
+ * over about `target` workgroups (default 512).  target = 1 never splits, so every reduction
+ * runs in one fixed order and a sample's results are bit-identical at any batch size (parity
+ * tests).  Returns the previous target; target <= 0 only queries. */
+int dstagnn_set_splitk_target(int target);
 
 const char* dstagnn_last_error(void);
 int dstagnn_version(void);

@@ -98,10 +98,14 @@ def spatial_attention_scores(p, Z, K, dk):
     return torch.matmul(Q, Kt.transpose(-1, -2)) / np.sqrt(dk)
 
 
-def cheb_conv_sat(x, sat, adj_pa, thetas, masks, cheb, hoist=False):
+def cheb_conv_sat(x, sat, adj_pa, thetas, masks, cheb, hoist=False, relu_mask=None, pre_out=None):
     """cheb_conv_withSAt.forward (:117-133).  Softmax over dim=1 (source node i, quirk 2).
     hoist=False reproduces the reference's T x K loop literally (the softmax is recomputed
-    for every timestep); hoist=True computes it once per k (exact, quirk 3)."""
+    for every timestep); hoist=True computes it once per k (exact, quirk 3).
+    relu_mask (B,N,C,T), optional: the ReLU of :133 takes these decisions instead of z > 0
+    (out = z * mask, gradient mask) — a parity test hands in the decisions of the
+    implementation under test, valid where they agree with sign(z) or |z| is within
+    rounding of 0.  pre_out (dict, optional) receives the pre-activation z under "z"."""
     B, N, Fin, T = x.shape
     Kc = len(thetas)
     C = thetas[0].shape[1]
@@ -119,7 +123,12 @@ def cheb_conv_sat(x, sat, adj_pa, thetas, masks, cheb, hoist=False):
             rhs = Wk.permute(0, 2, 1).matmul(g)
             o = o + rhs.matmul(thetas[k])
         outs.append(o.unsqueeze(-1))
-    return F.relu(torch.cat(outs, dim=-1))
+    z = torch.cat(outs, dim=-1)
+    if pre_out is not None:
+        pre_out["z"] = z.detach()
+    if relu_mask is not None:
+        return z * relu_mask.to(z.dtype)
+    return F.relu(z)
 
 
 def gtu(p, name, X, k):
@@ -129,7 +138,8 @@ def gtu(p, name, X, k):
     return torch.tanh(c[:, :C]) * torch.sigmoid(c[:, -C:])
 
 
-def block_forward(p, x, res_att, cheb, adj_pa, dims, train=False, drop_masks=None, hoist=False):
+def block_forward(p, x, res_att, cheb, adj_pa, dims, train=False, drop_masks=None, hoist=False, relu_mask=None,
+                  pre_out=None):
     """DSTAGNN_block.forward (:225-253).  Returns (x_out (B,N,C,T), re_At (B,F,h,T,T)).
 
     dims: dict(n_heads, d_k, d_v, K).  train=True applies the two Dropout(0.05)
@@ -149,7 +159,8 @@ def block_forward(p, x, res_att, cheb, adj_pa, dims, train=False, drop_masks=Non
     STAt = spatial_attention_scores(p, SEmx, K, dk)                     # :235
     thetas = [p[f"cheb_conv_SAt.Theta.{k}"] for k in range(K)]
     masks = [p[f"cheb_conv_SAt.mask.{k}"] for k in range(K)]
-    spatial_gcn = cheb_conv_sat(x, STAt, adj_pa, thetas, masks, cheb, hoist=hoist)  # :236
+    spatial_gcn = cheb_conv_sat(x, STAt, adj_pa, thetas, masks, cheb, hoist=hoist, relu_mask=relu_mask,
+                                pre_out=pre_out)                        # :236
     X = spatial_gcn.permute(0, 2, 1, 3)                                 # :237
     tc = torch.cat([gtu(p, "gtu3", X, 3), gtu(p, "gtu5", X, 5), gtu(p, "gtu7", X, 7)], dim=-1)  # :238-242
     tc = tc @ p["fcmy.0.weight"].t() + p["fcmy.0.bias"]                 # :243
@@ -195,13 +206,14 @@ def split_state_dict(sd, nb_block):
     return blocks, final
 
 
-def block_forward_backward(p, x, res_att, cheb, adj_pa, dims, g_out, g_re, hoist=True):
+def block_forward_backward(p, x, res_att, cheb, adj_pa, dims, g_out, g_re, hoist=True, relu_mask=None, pre_out=None):
     """Forward + autograd backward of one block with upstream grads (g_out, g_re).
-    Returns (out, re_at, grad_x, grad_res_att or None, {param_name: grad or None})."""
+    Returns (out, re_at, grad_x, grad_res_att or None, {param_name: grad or None}).
+    relu_mask / pre_out: see cheb_conv_sat."""
     pp = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
     xx = x.detach().clone().requires_grad_(True)
     ra = res_att.detach().clone().requires_grad_(True) if torch.is_tensor(res_att) else res_att
-    out, re_at = block_forward(pp, xx, ra, cheb, adj_pa, dims, hoist=hoist)
+    out, re_at = block_forward(pp, xx, ra, cheb, adj_pa, dims, hoist=hoist, relu_mask=relu_mask, pre_out=pre_out)
     loss = (out * g_out).sum()
     if g_re is not None:
         loss = loss + (re_at * g_re).sum()

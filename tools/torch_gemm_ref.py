@@ -1,20 +1,26 @@
-"""rocBLAS/hipBLASLt (torch.mm, fp32) timing at the block's GEMM shapes, for comparison."""
+"""rocBLAS/hipBLASLt (torch.mm / bmm, fp32, no TF32) timing at the block's GEMM shapes
+(tools/gemm_sweep.py SHAPES), as a library reference point for the hand-written GEMM."""
+import os
+import sys
+
 import torch
-shapes = [("preconv", 5440, 512, 384), ("qkv", 12288, 288, 170), ("gtu7", 32640, 64, 224), ("dX7", 65280, 32, 448),
-          ("dWp", 512, 384, 5440), ("sat_dW", 192, 512, 5440), ("big", 4096, 4096, 2048)]
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gemm_sweep import SHAPES  # noqa: E402
+
 torch.backends.cuda.matmul.allow_tf32 = False
-for name, M, N, K in shapes:
-    a = torch.randn(M, K, device="cuda")
-    b = torch.randn(K, N, device="cuda")
+for name, M, N, K, batch, akc, bnc in SHAPES:
+    a = torch.randn(batch, M, K, device="cuda") if akc else torch.randn(batch, K, M, device="cuda").transpose(1, 2)
+    b = torch.randn(batch, K, N, device="cuda") if bnc else torch.randn(batch, N, K, device="cuda").transpose(1, 2)
     for _ in range(5):
-        torch.mm(a, b)
+        torch.bmm(a, b)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
     n = 50
+    e0.record()
     for _ in range(n):
-        torch.mm(a, b)
+        torch.bmm(a, b)
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / n * 1e3
-    print(f"{name:8s} {M}x{N}x{K}: {us:8.1f} us  {2 * M * N * K / us / 1e6:7.1f} TF/s")
+    print(f"{name:12s} {M}x{N}x{K}x{batch}: {us:8.1f} us  {2 * M * N * K * batch / us / 1e6:7.1f} TF/s", flush=True)
