@@ -9,13 +9,11 @@
 // peak; gfx950 has no xf32).  A workgroup is 4 waves arranged WGM x WGN; each wave
 // owns WM x WN 32x32 accumulators, so the block tile is (32*WM*WGM) x (32*WN*WGN) x 16
 // (64x64, 128x64, 128x128, 128x32, 256x32 are instantiated; a cost model picks one).
-// Global loads of full k-tiles are issued UNCONDITIONALLY (out-of-range rows/columns are
-// clamped to a valid address; their products land only in unstored C entries): a
-// predicated load makes hipcc branch and wait vmcnt(0) per element, serialising the
-// k-tile prefetch.  The next k-tile is
-// prefetched into registers while the MFMAs consume the current LDS buffer (2 LDS
-// buffers, one barrier per k-tile).  Long reductions are split over workgroups into
-// fp32 partial slabs summed by a deterministic second pass (no float atomics).
+// Operands are staged global -> LDS by LDS-DMA (global_load_lds_dword) in a 2- or 3-stage
+// pipeline (see gemm_glds_body); out-of-range rows/columns are clamped to a valid address
+// (their products land only in unstored C entries), so full k-tiles issue with no
+// per-element predicate.  Long reductions are split over workgroups into fp32 partial
+// slabs summed by a deterministic second pass (no float atomics).
 #include <cstdio>
 #include <cstdlib>
 
@@ -24,9 +22,6 @@
 namespace {
 
 constexpr int BKMAX = 32;  // k-tile depth (16 or 32, template parameter)
-#ifndef DSTAGNN_GEMM_NS4
-#define DSTAGNN_GEMM_NS4 0  // 1: 4-stage LDS-DMA pipeline where the vmcnt budget allows (measured slower: occupancy)
-#endif
 
 #ifdef DSTAGNN_ABLATE_STAMP
 // timeline probe build: thread 0 of each of the first 4096 workgroups records s_memtime
@@ -368,14 +363,15 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int NSTAGE>
 __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
   constexpr int BK = 32;
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // DMA instructions per thread per tile
   // pipeline depth: NS-1 tiles in flight; the counted wait holds (NS-2) tiles' DMAs, which
   // must fit the 6-bit vmcnt (63)
-  constexpr int NS = (DSTAGNN_GEMM_NS4 && 2 * (LA + LB) <= 63) ? 4 : 3;
+  constexpr int NS = NSTAGE;
+  static_assert(NS == 2 || NS == 3 || (NS == 4 && 2 * (LA + LB) <= 63), "pipeline depth");
   __shared__ __attribute__((aligned(16))) float As[NS][BM * BK];
   __shared__ __attribute__((aligned(16))) float Bs[NS][BN * BK];
 
@@ -529,109 +525,17 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
 #endif
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool GLDS, bool KTWO>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool GLDS, bool KTWO, int NS>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmK g) {
-  if constexpr (GLDS) gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO>(g);
-  else gemm_f32_body<WGM, WGN, WM, WN, A_KC, B_NC, 32, KTWO>(g);
+  static_assert(GLDS, "the LDS-DMA pipeline is the only GEMM body");
+  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, NS>(g);
 }
 // identical body under its own symbol: the call site the benchmark reports as the
 // dominant kernel (rocprofv3 then lists exactly that call site's launches)
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool GLDS, bool KTWO>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool GLDS, bool KTWO, int NS>
 __global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmK g) {
-  if constexpr (GLDS) gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO>(g);
-  else gemm_f32_body<WGM, WGN, WM, WN, A_KC, B_NC, 32, KTWO>(g);
-}
-
-// ---------------------------------------------------------------------------------
-// Direct (LDS-free) path for the block's many small-K contractions: every wave owns a
-// 32 x (32 WN) output tile and streams its A rows / B columns straight from global memory
-// into the MFMA operand registers (no LDS image, no barrier, waves fully independent), so
-// latency is hidden by wave occupancy instead of a per-workgroup DMA pipeline.  Chunks of
-// 8 k: lane half h supplies k = kb + 4h + s at MFMA step s (A and B agree).  Operands that
-// are contiguous along k load V floats per instruction (V = 4, 2 or 1 by alignment);
-// V = 0 walks the general index map one element at a time.
-// ---------------------------------------------------------------------------------
-template <int V>
-__device__ __forceinline__ void load_k4(const float* base, int32_t row, const KIdx& km, int k0, int kend,
-                                        float (&v)[4]) {
-  if (k0 + 4 <= kend) {
-    if constexpr (V == 4) {
-      const float4 q = *reinterpret_cast<const float4*>(base + row + k0);
-      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-    } else if constexpr (V == 2) {
-      const float2 q0 = *reinterpret_cast<const float2*>(base + row + k0);
-      const float2 q1 = *reinterpret_cast<const float2*>(base + row + k0 + 2);
-      v[0] = q0.x; v[1] = q0.y; v[2] = q1.x; v[3] = q1.y;
-    } else if constexpr (V == 1) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) v[s] = base[row + k0 + s];
-    } else {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) v[s] = base[row + koff(km, k0 + s)];
-    }
-  } else {
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      v[s] = (k0 + s < kend) ? base[row + (V > 0 ? k0 + s : koff(km, k0 + s))] : 0.f;
-  }
-}
-
-template <int WN, int VA, int VB>
-__global__ __launch_bounds__(256) void gemm_direct_kernel(GemmK gin) {
-  const GemmK g = load_args(gin);
-  const int lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t t = blockIdx.x * 4u + wid;  // wave tile, n fastest (waves of a workgroup share A rows)
-  const uint32_t tn = g.tiles_n, tm = g.tiles_m;
-  const uint32_t per_z = tn * tm;
-  if (t >= per_z * (uint32_t)g.batch * (uint32_t)g.splitk) return;  // whole wave: no barriers below
-  const uint32_t zz = t / per_z, tr = t - zz * per_z;
-  TileCoord c;
-  c.m0 = (int)(tr / tn) * 32;
-  c.n0 = (int)(tr % tn) * (32 * WN);
-  c.zb = (int)zz / g.splitk;
-  c.sp = (int)zz % g.splitk;
-  const int kbeg = c.sp * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
-  const float* A = g.A + zoff(g.az, c.zb) + g.abias;
-  const float* Bp = g.B + zoff(g.bz, c.zb) + g.bbias;
-  const int lr = lane & 31, h = lane >> 5;
-  const int32_t arow = koff(g.am, min(c.m0 + lr, g.M - 1));
-  int32_t bcol[WN];
-#pragma unroll
-  for (int j = 0; j < WN; ++j) bcol[j] = koff(g.bn, min(c.n0 + j * 32 + lr, g.N - 1));
-
-  floatx16 acc[WN];
-#pragma unroll
-  for (int j = 0; j < WN; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-
-  float a[2][4], b[2][WN][4];
-  auto load = [&](int kb, int buf) {
-    const int k0 = kb + 4 * h;
-    load_k4<VA>(A, arow, g.ak, k0, kend, a[buf]);
-#pragma unroll
-    for (int j = 0; j < WN; ++j) load_k4<VB>(Bp, bcol[j], g.bk, k0, kend, b[buf][j]);
-  };
-  const int nch = kend > kbeg ? (kend - kbeg + 7) / 8 : 0;
-  if (nch > 0) load(kbeg, 0);
-  for (int ch = 0; ch < nch; ch += 2) {
-    if (ch + 1 < nch) load(kbeg + (ch + 1) * 8, 1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < WN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][s], b[0][j][s], acc[j], 0, 0, 0);
-    if (ch + 1 >= nch) break;
-    if (ch + 2 < nch) load(kbeg + (ch + 2) * 8, 0);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < WN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][s], b[1][j][s], acc[j], 0, 0, 0);
-  }
-  floatx16 accm[1][WN];
-#pragma unroll
-  for (int j = 0; j < WN; ++j) accm[0][j] = acc[j];
-  gemm_epilogue<1, WN>(g, c, 0, 0, lane, accm);
+  static_assert(GLDS, "the LDS-DMA pipeline is the only GEMM body");
+  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, NS>(g);
 }
 
 // out[zb][m][n] = epilogue( sum_s ws[zb][s][m][n] ).  A workgroup takes 256/G outputs and
@@ -671,7 +575,7 @@ struct Cfg {
 };
 constexpr Cfg kCfgs[] = {{2, 2, 1, 1}, {2, 2, 2, 1}, {2, 2, 2, 2}, {4, 1, 1, 1}, {4, 1, 2, 1}};
 
-template <int WGM, int WGN, int WM, int WN, bool KTWO, bool GLDS>
+template <int WGM, int WGN, int WM, int WN, bool KTWO, bool GLDS, int NS>
 void launch_cfg(const GemmK& k, bool akc, bool bnc, bool hot, hipStream_t st) {
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   GemmK kk = k;
@@ -680,10 +584,10 @@ void launch_cfg(const GemmK& k, bool akc, bool bnc, bool hot, hipStream_t st) {
   kk.n_fast = (int64_t)k.M >= (int64_t)k.N ? 1u : 0u;  // A (M x K) is the bigger operand
   const dim3 grid((unsigned)((int64_t)kk.tiles_m * kk.tiles_n * k.batch * k.splitk));
 #define DS_GEMM_LAUNCH(KER)                                                                                  \
-  if (akc && bnc) hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, true, GLDS, KTWO>), grid, dim3(256), 0, st, kk);       \
-  else if (akc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, false, GLDS, KTWO>), grid, dim3(256), 0, st, kk);      \
-  else if (bnc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, true, GLDS, KTWO>), grid, dim3(256), 0, st, kk);      \
-  else            hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, false, GLDS, KTWO>), grid, dim3(256), 0, st, kk);
+  if (akc && bnc) hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, true, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);   \
+  else if (akc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, false, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);  \
+  else if (bnc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, true, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);  \
+  else            hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, false, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);
   if (hot) { DS_GEMM_LAUNCH(gemm_f32_hot_kernel) } else { DS_GEMM_LAUNCH(gemm_f32_kernel) }
 #undef DS_GEMM_LAUNCH
 }
@@ -708,42 +612,6 @@ Prof g_prof;
 // range to about this many (1 = never split: every reduction in one fixed order, so a
 // per-sample result is bit-identical at any batch size); DSTAGNN_SPLITK_TARGET overrides
 int g_splitk_target = getenv("DSTAGNN_SPLITK_TARGET") ? atoi(getenv("DSTAGNN_SPLITK_TARGET")) : 512;
-
-// widest V in {4, 2, 1} such that every k-run start of a k-contiguous operand is
-// V-float aligned (base, row map and batch map); 0 when the operand is not k-contiguous
-int vec_width(const float* base, const Idx2& rowmap, const Idx2& kmap, const Idx2& zmap) {
-  if (kmap.two || kmap.s0 != 1) return 0;
-  for (int v : {4, 2}) {
-    const bool ok = ((uintptr_t)base % (4 * v)) == 0 && rowmap.s0 % v == 0 && (!rowmap.two || rowmap.s1 % v == 0) &&
-                    zmap.s0 % v == 0 && (!zmap.two || zmap.s1 % v == 0);
-    if (ok) return v;
-  }
-  return 1;
-}
-
-template <int WN, int VA>
-void launch_direct_vb(const GemmK& k, int vb, dim3 grid, hipStream_t st) {
-  switch (vb) {
-    case 4: hipLaunchKernelGGL((gemm_direct_kernel<WN, VA, 4>), grid, dim3(256), 0, st, k); break;
-    case 2: hipLaunchKernelGGL((gemm_direct_kernel<WN, VA, 2>), grid, dim3(256), 0, st, k); break;
-    case 1: hipLaunchKernelGGL((gemm_direct_kernel<WN, VA, 1>), grid, dim3(256), 0, st, k); break;
-    default: hipLaunchKernelGGL((gemm_direct_kernel<WN, VA, 0>), grid, dim3(256), 0, st, k); break;
-  }
-}
-template <int WN>
-void launch_direct(const GemmK& k, int va, int vb, hipStream_t st) {
-  GemmK kk = k;
-  kk.tiles_m = (uint32_t)cdiv64(k.M, 32);
-  kk.tiles_n = (uint32_t)cdiv64(k.N, 32 * WN);
-  const int64_t waves = (int64_t)kk.tiles_m * kk.tiles_n * k.batch * k.splitk;
-  const dim3 grid((unsigned)cdiv64(waves, 4));
-  switch (va) {
-    case 4: launch_direct_vb<WN, 4>(kk, vb, grid, st); break;
-    case 2: launch_direct_vb<WN, 2>(kk, vb, grid, st); break;
-    case 1: launch_direct_vb<WN, 1>(kk, vb, grid, st); break;
-    default: launch_direct_vb<WN, 0>(kk, vb, grid, st); break;
-  }
-}
 
 }  // namespace
 
@@ -873,33 +741,30 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   const bool akc = !g.ak.two && g.ak.s0 == 1;
   const bool bnc = !g.bn.two && g.bn.s0 == 1;
   const bool hot = g.hot != 0;
-#define DS_CFG_SWITCH(KT, GL)                                              \
-  switch (best) {                                                          \
-    case 0: launch_cfg<2, 2, 1, 1, KT, GL>(k, akc, bnc, hot, st); break;   \
-    case 1: launch_cfg<2, 2, 2, 1, KT, GL>(k, akc, bnc, hot, st); break;   \
-    case 2: launch_cfg<2, 2, 2, 2, KT, GL>(k, akc, bnc, hot, st); break;   \
-    case 3: launch_cfg<4, 1, 1, 1, KT, GL>(k, akc, bnc, hot, st); break;   \
-    default: launch_cfg<4, 1, 2, 1, KT, GL>(k, akc, bnc, hot, st); break;  \
+  // LDS pipeline depth: 3 stages keep two k-tiles in flight per workgroup (needed when a CU
+  // holds about one workgroup: long split-K reductions); 2 stages cut the workgroup's LDS by a
+  // third, so more workgroups are resident per CU and latency is hidden across workgroups
+  // (measured on the bench step: -1.5 % with 2 stages wherever the grid exceeds the CUs)
+  int ns = blocks * splitk > 256 ? 2 : 3;
+  static const int env_ns = getenv("DSTAGNN_GEMM_NS") ? atoi(getenv("DSTAGNN_GEMM_NS")) : 0;
+  if (env_ns == 2 || env_ns == 3) ns = env_ns;
+#define DS_CFG_SWITCH(KT, NS)                                                \
+  switch (best) {                                                            \
+    case 0: launch_cfg<2, 2, 1, 1, KT, true, NS>(k, akc, bnc, hot, st); break;   \
+    case 1: launch_cfg<2, 2, 2, 1, KT, true, NS>(k, akc, bnc, hot, st); break;   \
+    case 2: launch_cfg<2, 2, 2, 2, KT, true, NS>(k, akc, bnc, hot, st); break;   \
+    case 3: launch_cfg<4, 1, 1, 1, KT, true, NS>(k, akc, bnc, hot, st); break;   \
+    default: launch_cfg<4, 1, 2, 1, KT, true, NS>(k, akc, bnc, hot, st); break;  \
   }
   const bool ktwo = g.ak.two || g.bk.two;
-  // implementation: 1 = LDS-DMA 3-stage pipeline (default), 0 = register-staged
-  static const int impl = getenv("DSTAGNN_GEMM_IMPL") ? atoi(getenv("DSTAGNN_GEMM_IMPL")) : 1;
   static const bool glog = getenv("DSTAGNN_GEMM_LOG") != nullptr;
   if (glog)
-    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld\n", g.M, g.N,
-            g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk);
-  if (impl == 2) {  // direct (LDS-free) wave-tile path
-    const int va = vec_width(g.A + g.a_off, g.am, g.ak, g.az);
-    const int vb = vec_width(g.B + g.b_off, g.bn, g.bk, g.bz);
-    static const int env_wn = getenv("DSTAGNN_GEMM_WN") ? atoi(getenv("DSTAGNN_GEMM_WN")) : 0;
-    const int wn = env_wn ? env_wn : (g.N > 32 ? 2 : 1);
-    if (glog) fprintf(stderr, "[gemm] direct va=%d vb=%d wn=%d\n", va, vb, wn);
-    if (wn == 2) launch_direct<2>(k, va, vb, st);
-    else launch_direct<1>(k, va, vb, st);
-  } else if (impl) {
-    if (ktwo) { DS_CFG_SWITCH(true, true) } else { DS_CFG_SWITCH(false, true) }
+    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d\n", g.M,
+            g.N, g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk, ns);
+  if (ns == 2) {
+    if (ktwo) { DS_CFG_SWITCH(true, 2) } else { DS_CFG_SWITCH(false, 2) }
   } else {
-    if (ktwo) { DS_CFG_SWITCH(true, false) } else { DS_CFG_SWITCH(false, false) }
+    if (ktwo) { DS_CFG_SWITCH(true, 3) } else { DS_CFG_SWITCH(false, 3) }
   }
 #undef DS_CFG_SWITCH
   DS_CHECK_LAUNCH();

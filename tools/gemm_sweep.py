@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Tuning sweep for the strided f32-MFMA GEMM (dstagnn_gemm_f32) on the DSTAGNN block's
 GEMM shapes (PEMS08, B=32).  Each (tile config, implementation) runs in its own subprocess
-because the overrides (DSTAGNN_GEMM_CFG / DSTAGNN_GEMM_IMPL) are read once per process;
+because the overrides (DSTAGNN_GEMM_CFG / DSTAGNN_GEMM_NS) are read once per process;
 every run is checked against torch.bmm.
 
     python tools/gemm_sweep.py            # full sweep, prints a table
@@ -97,8 +97,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
-    # spec = <tile config | auto>:<impl: 1 LDS-DMA pipeline, 0 register-staged>
-    ap.add_argument("--configs", default="auto:1,auto:0,0:1,0:0,1:1,1:0,2:1,3:1,3:0,4:1")
+    # spec = <tile config | auto>:<LDS pipeline stages: 2, 3, or auto>
+    ap.add_argument("--configs", default="auto:auto,auto:2,auto:3,0:2,0:3,1:3,2:3,3:2,3:3,4:3")
     ap.add_argument("--only", default=None)
     ap.add_argument("--big", action="store_true", help="add large square steady-state probes")
     ap.add_argument("--large", action="store_true", help="add the GAMBIA / SYN large-M shapes")
@@ -115,8 +115,10 @@ def main():
         return
     table = {}
     for spec in args.configs.split(","):
-        cfg, impl = spec.split(":")
-        env = dict(os.environ, DSTAGNN_GEMM_IMPL=impl)
+        cfg, ns = spec.split(":")
+        env = dict(os.environ)
+        if ns != "auto":
+            env["DSTAGNN_GEMM_NS"] = ns
         if cfg != "auto":
             env["DSTAGNN_GEMM_CFG"] = cfg
         env["DSTAGNN_GEMM_CHECK"] = "" if os.environ.get("DSTAGNN_NOCHECK") else "1"
