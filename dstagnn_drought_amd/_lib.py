@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(_HERE, "libdstagnn.so")
 
 RES_NONE, RES_BCAST, RES_FULL = 0, 1, 2
 # dstagnn::block flags
-F_TRAIN, F_SPARSE, F_DIRECT, F_POISON = 1, 2, 4, 8
+F_TRAIN, F_SPARSE, F_DIRECT, F_POISON, F_FLASH = 1, 2, 4, 8, 16
 
 _ops = None
 

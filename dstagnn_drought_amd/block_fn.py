@@ -52,11 +52,17 @@ def res_arg(res_att, F):
     return res_att.float().contiguous()
 
 
-def graph_list(graph, sparse):
-    """[cheb (K,N,N), adj_pa (N,N)] + the int32 CSC/CSR union support for the sparse path."""
+FLASH_KEYS = ("csr2csc", "apa_bits", "apa_bits_t", "apa_ptr", "apa_row", "tsupp")
+
+
+def graph_list(graph, sparse, flash=False):
+    """[cheb (K,N,N), adj_pa (N,N)] + the int32 CSC/CSR union support for the sparse path
+    + the flash-attention index data (model.flash_support) for the fused path."""
     g = [graph["cheb"], graph["adj_pa"]]
     if sparse:
         g += [graph["csc_ptr"], graph["csc_row"], graph["csr_ptr"], graph["csr_col"]]
+        if flash:
+            g += [graph[k] for k in FLASH_KEYS]
     return g
 
 
@@ -69,22 +75,37 @@ def use_sparse(graph, meta, T):
     return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= (1 << 20)
 
 
+def use_flash(graph, meta, T, force=None):
+    """Fused (flash-style) Chebyshev attention (cheb_flash.hip): the (B,K,N,N) scores, softmax
+    and score gradient are never written; on the sparse path with d_k == 32 (the MFMA tile),
+    automatically from N >= 1024 (DSTAGNN_FLASH=0/1 overrides), or when forced."""
+    if not use_sparse(graph, meta, T) or meta["d_k"] != 32:
+        return False
+    if force is not None:
+        return bool(force)
+    env = os.environ.get("DSTAGNN_FLASH")
+    if env is not None:
+        return env == "1"
+    return graph["adj_pa"].shape[0] >= 1024
+
+
 def cfg_of(meta):
     return [meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"], meta["C"]]
 
 
-def flags_of(train, sparse, direct):
+def flags_of(train, sparse, direct, flash=False):
     return ((_lib.F_TRAIN if train else 0) | (_lib.F_SPARSE if sparse else 0) | (_lib.F_DIRECT if direct else 0)
-            | (_lib.F_POISON if _POISON else 0))
+            | (_lib.F_POISON if _POISON else 0) | (_lib.F_FLASH if flash else 0))
 
 
-def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False):
+def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False, flash=None):
     """(out, re_at) = dstagnn::block(...) — autograd-tracked."""
     ops = _lib.load()
     x = x.float().contiguous()
     sparse = use_sparse(graph, meta, x.shape[3])
-    return ops.block(x, res_arg(res_att, x.shape[2]), list(params), slots, graph_list(graph, sparse), cfg_of(meta),
-                     float(meta.get("drop_p", 0.05)), int(seed), flags_of(train, sparse, direct))
+    fl = use_flash(graph, meta, x.shape[3], flash)
+    return ops.block(x, res_arg(res_att, x.shape[2]), list(params), slots, graph_list(graph, sparse, fl),
+                     cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed), flags_of(train, sparse, direct, fl))
 
 
 def dropout_masks(meta, x_shape, seed):

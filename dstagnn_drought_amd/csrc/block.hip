@@ -45,7 +45,8 @@ struct Dims {
   int B, N, F, T, h, dk, dv, D, K, C;
   int64_t FT, BFT, BN, NN, HQ, HV, QW, KD, KC, CT, KCT, S;
   int Tg[3], Lp[3], ks[3];
-  bool first, sparse;
+  bool first, sparse, flash;
+  int64_t nnz;  // flash: union-support entries
 };
 
 Dims mkdims(const dstagnn_block_dims& d) {
@@ -58,6 +59,8 @@ Dims mkdims(const dstagnn_block_dims& d) {
   for (int g = 0; g < 3; ++g) { m.ks[g] = 3 + 2 * g; m.Tg[g] = m.T - m.ks[g] + 1; m.Lp[g] = m.T + m.ks[g] - 1; }
   m.first = (m.F == 1);
   m.sparse = d.cheb_sparse != 0;
+  m.flash = m.sparse && d.cheb_flash != 0;
+  m.nnz = m.flash ? d.cheb_nnz : 0;
   return m;
 }
 
@@ -67,6 +70,7 @@ struct SaveBufs {
   // (D, F*T), Theta_cat (F, K*C), GTU conv weights (o, j, c) fwd and (j', o, c) flipped bwd
   float *Wqkv, *Wqk, *Wp, *thcat, *Wgf[3], *Wgb[3];
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
+  float *lse, *psupp, *wsupp;  // flash path: column log-sum-exp (B,K,N), P and T o P on the support (B,K,nnz)
   float* conv[3];
   float *G, *tco, *r, *mu_c, *rs_c, *u_et, *mu_et, *rs_et;
 };
@@ -92,8 +96,11 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   s.rs_s = a.take(m.BN);
   s.Zd = a.take(m.BN * m.D);
   s.qk = a.take(m.BN * 2 * m.KD);
-  s.P = a.take((int64_t)m.B * m.K * m.NN);
+  s.P = m.flash ? nullptr : a.take((int64_t)m.B * m.K * m.NN);
   s.W = m.sparse ? nullptr : a.take((int64_t)m.B * m.K * m.NN);
+  s.lse = m.flash ? a.take((int64_t)m.B * m.K * m.N) : nullptr;
+  s.psupp = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
+  s.wsupp = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.xth = a.take(m.BN * m.KCT);
   s.X = a.take(m.BN * m.CT);
   for (int g = 0; g < 3; ++g) s.conv[g] = a.take(m.BN * 2 * m.C * std::max(m.Tg[g], 0));
@@ -122,6 +129,7 @@ struct Scratch {
   float *gemm_ws_side, *part_side, *dWqkv, *dWqk;
   float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dconv[3], *dW, *dxth,
       *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dE, *dctx, *dqkv, *dscore, *du_et, *dGt;
+  float *dws, *dzs, *cc;  // flash path: dW and P o dP on the support (B,K,nnz), c (B,K,N)
 };
 
 Scratch plan_scratch(const Dims& m, Arena& a) {
@@ -143,7 +151,10 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.gcon_a = a.take(m.BFT * m.N);
   s.gcon_e = m.first ? a.take((int64_t)m.B * m.T * m.N) : nullptr;
   for (int g = 0; g < 3; ++g) s.dconv[g] = a.take(m.BN * 2 * m.C * m.Lp[g]);
-  s.dW = a.take((int64_t)m.B * m.K * m.NN);
+  s.dW = m.flash ? nullptr : a.take((int64_t)m.B * m.K * m.NN);
+  s.dws = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
+  s.dzs = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
+  s.cc = m.flash ? a.take((int64_t)m.B * m.K * m.N) : nullptr;
   s.dxth = a.take(m.BN * m.KCT);
   s.dthcat = a.take((int64_t)m.F * m.KC);
   s.dqk = a.take(m.BN * 2 * m.KD);
@@ -183,6 +194,10 @@ int check_dims(const dstagnn_block_dims* d) {
     set_last_error("cheb_sparse requires 0 < C*T <= 2^20");
     return DSTAGNN_E_SHAPE;
   }
+  if (d->cheb_flash && (!d->cheb_sparse || d->d_k != 32 || d->cheb_nnz <= 0)) {
+    set_last_error("cheb_flash requires cheb_sparse, d_k == 32 and cheb_nnz > 0");
+    return DSTAGNN_E_SHAPE;
+  }
   if (d->F != 1 && d->F != d->C) {
     // the reference fails at model/DSTAGNN_my.py:252 (x.permute + time_conv_output)
     set_last_error("The size of tensor a (" + std::to_string(d->F) + ") must match the size of tensor b (" +
@@ -204,6 +219,7 @@ struct ChebIO {
   bool sparse;
   const float* thcat;      // (F, K*C)
   float *P, *W, *xth, *X;  // W unused (null) on the sparse path; xth (B,N,T,K,C), X (B,N,T,C)
+  const ChebFl* fl = nullptr;  // fused (flash) attention: softmax statistics + support P, no dense P
 };
 
 ChebSp make_sp(int B, int N, int K, int C, int T, const dstagnn_graph* g) {
@@ -215,6 +231,7 @@ ChebSp make_sp(int B, int N, int K, int C, int T, const dstagnn_graph* g) {
 }
 
 int cheb_softmax(const ChebIO& c, hipStream_t st) {
+  if (c.fl) return op_flash_forward(*c.fl, st);
   ChebSm sm;
   sm.B = c.B; sm.K = c.K; sm.N = c.N; sm.S = c.S; sm.apa = c.g->adj_pa; sm.cheb = c.g->cheb; sm.P = c.P;
   sm.W = c.sparse ? nullptr : c.W;
@@ -239,6 +256,7 @@ int cheb_aggregate(const ChebIO& c, float* ws, hipStream_t st) {
   if (c.sparse) {
     ChebSp sp = make_sp(c.B, c.N, c.K, c.C, c.T, c.g);
     sp.P = c.P; sp.xth = c.xth; sp.out = c.X;
+    if (c.fl) { sp.wsupp = c.fl->wsupp; sp.nnz = c.fl->nnz; }
     return op_cheb_spmm_fwd(sp, st);
   }
   Gemm g;
@@ -336,6 +354,21 @@ int unpack_theta(const float* thcat, int K, int F, int C, float* const* dtheta, 
   a.K = K; a.F = F; a.C = C; a.unpack = 1; a.cat_in = thcat;
   for (int k = 0; k < K; ++k) a.dst[k] = dtheta[k];
   return op_pack_theta(a, st);
+}
+
+// the fused (flash) Chebyshev attention's arguments (cheb_flash.hip)
+ChebFl make_fl(const Dims& m, const dstagnn_block_params& p, const dstagnn_graph& g, const SaveBufs& s) {
+  ChebFl f;
+  f.B = m.B; f.N = m.N; f.K = m.K; f.nnz = (int)m.nnz; f.nw = (m.N + 31) / 32;
+  f.scale = 1.f / sqrtf((float)m.dk);
+  f.qk = s.qk; f.ld = 2 * m.KD; f.kd = (int)m.KD;
+  f.apa = g.adj_pa;
+  for (int k = 0; k < m.K; ++k) f.mask[k] = p.mask[k];
+  f.bits = g.apa_bits; f.bits_t = g.apa_bits_t;
+  f.csc_ptr = g.csc_ptr; f.csc_row = g.csc_row; f.csr_ptr = g.csr_ptr; f.csr_col = g.csr_col; f.csr2csc = g.csr2csc;
+  f.apa_ptr = g.apa_ptr; f.apa_row = g.apa_row; f.tsupp = g.tsupp;
+  f.lse = s.lse; f.psupp = s.psupp; f.wsupp = s.wsupp;
+  return f;
 }
 
 // host-side issue timing per stage (DSTAGNN_HOST_PROFILE=1): accumulates and prints
@@ -439,6 +472,7 @@ struct Fwd {
   hipStream_t st;
   Streams ks;
   bool params_forked = false;
+  ChebFl fl;
 
   int stage_tat() {
     const int64_t N = m.N;
@@ -555,7 +589,7 @@ struct Fwd {
       g.C = s.qk; g.cm = idx1(2 * m.KD); g.cn = idx1(1);
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
-    {  // S'[b,k] = Q'_k K'_k^T / sqrt(dk)  (:19) -> written into P (softmaxed in place)
+    if (!m.flash) {  // S'[b,k] = Q'_k K'_k^T / sqrt(dk)  (:19) -> written into P (softmaxed in place)
       Gemm g;
       g.M = m.N; g.N = m.N; g.K = m.dk; g.batch = m.B * m.K;
       g.A = s.qk; g.am = idx1(2 * m.KD); g.ak = idx1(1); g.az = idx2(m.K, m.dk, m.N * 2 * m.KD);
@@ -572,6 +606,10 @@ struct Fwd {
     c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
     c.x = x; c.S = s.P; c.mask = p.mask; c.g = &gr; c.sparse = m.sparse; c.thcat = s.thcat;
     c.P = s.P; c.W = s.W; c.xth = s.xth; c.X = s.X;
+    if (m.flash) {
+      fl = make_fl(m, p, gr, s);
+      c.fl = &fl;
+    }
     return c;
   }
   int stage_cheb() { return cheb_forward(cheb_io(), w.gemm_ws, st); }
@@ -661,6 +699,13 @@ struct Bwd {
   hipStream_t st;
   Streams ks;
   hipStream_t sd = nullptr;  // side stream (== st when disabled)
+  ChebFl fl;
+  ChebFl flash_args() {
+    ChebFl f = make_fl(m, p, gr, s);
+    f.dws = w.dws; f.dzs = w.dzs; f.cc = w.cc; f.dqk = w.dqk;
+    for (int k = 0; k < m.K; ++k) f.dmask[k] = gd.mask[k];
+    return f;
+  }
   int fork() { return ks.fork(); }
   int join() { return ks.join(); }
 
@@ -742,6 +787,9 @@ struct Bwd {
       // T_k != 0 (no memset)
       ChebSp sp = make_sp(B, N, K, C, m.T, &gr);
       sp.P = s.P; sp.xth = s.xth; sp.g = w.gpre; sp.dW = w.dW; sp.dxth = w.dxth;
+      if (m.flash) {  // T o P and dW compact on the support
+        sp.nnz = (int)m.nnz; sp.wsupp = s.wsupp; sp.dws = w.dws; sp.csr2csc = gr.csr2csc;
+      }
       DS_TRY(op_cheb_sddmm_bwd(sp, st));
       DS_TRY(op_cheb_spmm_t_bwd(sp, st));
     } else {
@@ -762,15 +810,23 @@ struct Bwd {
         DS_TRY(gemm(g));
       }
     }
-    // softmax backward in place: dz = P * (T o dW - colsum(P T o dW))
+    // softmax backward: dz = P * (T o dW - colsum(P T o dW)).  Unfused: in place, dense.
+    // Fused (flash): only c_j and P dP on the support; dz is recomputed by the dQ'/dK' and
+    // mask-gradient kernels
     ChebSm sm;
     sm.B = B; sm.K = K; sm.N = N; sm.apa = gr.adj_pa; sm.cheb = gr.cheb; sm.P = s.P;
     sm.dW = w.dW; sm.dz = w.dW;
     for (int k = 0; k < K; ++k) sm.dmask[k] = gd.mask[k];
-    DS_TRY(op_cheb_softmax_bwd(sm, st));
+    if (m.flash) {
+      fl = flash_args();
+      DS_TRY(op_flash_colc(fl, st));
+    } else {
+      DS_TRY(op_cheb_softmax_bwd(sm, st));
+    }
     // --- side: mask and Theta gradients
     DS_TRY(fork());
-    DS_TRY(op_cheb_mask_grad(sm, sd));
+    if (m.flash) DS_TRY(op_flash_mask_grad(fl, sd));
+    else DS_TRY(op_cheb_mask_grad(sm, sd));
     {
       Gemm g;  // dTheta_cat[f,(k,c)] = sum_{b,i,t} x[b,i,f,t] dxth[b,i,t,k,c]
       g.M = F; g.N = (int)KC; g.K = B * N * m.T;
@@ -803,7 +859,8 @@ struct Bwd {
   int stage_sat() {
     const float sc = 1.f / sqrtf((float)m.dk);
     const int64_t ld = 2 * m.KD;
-    {  // dQ'[b,i,k,:] = sum_j dz[b,k,i,j] K'[b,j,k,:] / sqrt(dk)
+    if (m.flash) DS_TRY(op_flash_dqk(fl, st));  // dQ' | dK' with P tiles recomputed, no dense dz
+    if (!m.flash) {  // dQ'[b,i,k,:] = sum_j dz[b,k,i,j] K'[b,j,k,:] / sqrt(dk)
       Gemm g;
       g.M = m.N; g.N = m.dk; g.K = m.N; g.batch = m.B * m.K;
       g.A = w.dW; g.am = idx1(m.N); g.ak = idx1(1); g.az = idx1(m.NN);
@@ -812,7 +869,7 @@ struct Bwd {
       g.alpha = sc;
       DS_TRY(gemm(g));
     }
-    {  // dK'[b,j,k,:] = sum_i dz[b,k,i,j] Q'[b,i,k,:] / sqrt(dk)
+    if (!m.flash) {  // dK'[b,j,k,:] = sum_i dz[b,k,i,j] Q'[b,i,k,:] / sqrt(dk)
       Gemm g;
       g.M = m.N; g.N = m.dk; g.K = m.N; g.batch = m.B * m.K;
       g.A = w.dW; g.am = idx1(1); g.ak = idx1(m.N); g.az = idx1(m.NN);
@@ -997,6 +1054,11 @@ int check_graph(const Dims& m, const dstagnn_graph* g) {
   if (!g->cheb || !g->adj_pa) { set_last_error("graph: null cheb / adj_pa"); return DSTAGNN_E_ARG; }
   if (m.sparse && (g->nnz <= 0 || !g->csc_ptr || !g->csc_row || !g->csr_ptr || !g->csr_col)) {
     set_last_error("cheb_sparse set but the graph carries no CSC/CSR support");
+    return DSTAGNN_E_ARG;
+  }
+  if (m.flash && (g->nnz != m.nnz || !g->csr2csc || !g->apa_bits || !g->apa_bits_t || !g->apa_ptr || !g->apa_row ||
+                  !g->tsupp)) {
+    set_last_error("cheb_flash set but the graph lacks the flash data (or its nnz differs from cheb_nnz)");
     return DSTAGNN_E_ARG;
   }
   return 0;

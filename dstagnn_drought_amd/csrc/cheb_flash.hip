@@ -1,0 +1,358 @@
+// cheb_flash.hip — fused (flash-style) Chebyshev spatial attention for large graphs (gfx950).
+//
+// cheb_conv_withSAt (model/DSTAGNN_my.py:117-133) normalises, for every destination node j,
+//   z_ij = Q'_i . K'_j / sqrt(dk) + A_pa[i,j] M_k[i,j]        (SAt scores :19 + the mask term :122)
+//   P_ij = softmax over the source node i of z_ij             (dim=1, quirk 2)
+// and aggregates only over the T_k support (cheb_sparse.hip).  The unfused path writes the
+// (B,K,N,N) scores, reads them twice for the softmax and writes P, then writes the dense
+// score gradient dz for the dQ'/dK' GEMMs — 4 x 10.7 GB per step at N = 4096, B = 32.  Here
+// none of those is written:
+//
+//   forward   stats   per (b,k, 32 columns j): S tiles from Q', K' on the f32 matrix cores
+//                     (dk = 32: 16 MFMAs per 32x32 tile), the A_pa o M_k term added where
+//                     the A_pa bit row says so, online column max / exp-sum -> lse_j
+//             psupp   P and W = T o P on the T_k support only (CSC order, compact)
+//   backward  colc    dP = T o dW on the support (dW from the sparse SDDMM, compact):
+//                     c_j = sum_i P_ij dP_ij, dzs_ij = P_ij dP_ij          (dz = dzs - P c)
+//             dq      dQ'_i = s (sum_{j in supp} dzs_ij K'_j - sum_j P_ij c_j K'_j): the dense
+//                     term recomputes P tiles (S^T tile: the P fragment lands in the MFMA
+//                     A-operand layout for P . (c K'), no transpose)
+//             dk      dK'_j = s (sum_{i in supp} dzs_ij Q'_i - c_j sum_i P_ij Q'_i)
+//             mask    dM_k = A_pa o sum_b dz, on the A_pa support only
+// The MFMA is v_mfma_f32_32x32x2_f32 (exact fp32): lane l supplies A[m = l&31][k = l>>5] and
+// B[k = l>>5][n = l&31]; at step s the lane half h carries element d = 16h + s of the 32-long
+// Q'/K' rows; the accumulator holds D[m = (r&3) + 8(r>>2) + 4h][n = l&31] in register r.
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace {
+
+__device__ __forceinline__ void load16(const float* p, float (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+  }
+}
+
+__device__ __forceinline__ int frag_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ floatx16 zero16() {
+  floatx16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// the A_pa o M_k term of z_ij (A_pa is a weight matrix; read only where its bit is set)
+__device__ __forceinline__ float apa_term(const ChebFl& a, const float* Mk, int i, int j) {
+  const int64_t o = (int64_t)i * a.N + j;
+  return a.apa[o] * Mk[o];
+}
+
+// ---------------------------------------------------------------------------------------
+// forward: column statistics.  One wave per (b, k, 32 columns); waves independent.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void flash_stats_kernel(ChebFl a) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int nt = (a.N + 31) >> 5;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= (int64_t)a.B * a.K * nt) return;
+  const int jt = (int)(wid % nt), bk = (int)(wid / nt), k = bk % a.K, b = bk / a.K;
+  const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+  const float* Kp = Q + a.kd;
+  const int j = jt * 32 + l32, jc = min(j, a.N - 1);
+  float bkv[16];
+  load16(Kp + (int64_t)jc * a.ld + h * 16, bkv);
+  const int32_t* bt = a.bits_t + (int64_t)jc * a.nw;
+  const float* Mk = a.mask[k];
+  float m = -INFINITY, l = 0.f;
+  float aq[16];
+  load16(Q + (int64_t)min(l32, a.N - 1) * a.ld + h * 16, aq);
+  for (int it = 0; it < nt; ++it) {
+    floatx16 acc = zero16();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[s], bkv[s], acc, 0, 0, 0);
+    if (it + 1 < nt) load16(Q + (int64_t)min((it + 1) * 32 + l32, a.N - 1) * a.ld + h * 16, aq);
+    const uint32_t bits = (uint32_t)bt[it];
+    const int i0 = it * 32;
+    float z[16], tmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int il = frag_row(r, h), i = i0 + il;
+      float v = acc[r] * a.scale;
+      if ((bits >> il) & 1u) v += apa_term(a, Mk, i, jc);
+      v = i < a.N ? v : -INFINITY;
+      z[r] = v;
+      tmax = fmaxf(tmax, v);
+    }
+    if (tmax > -INFINITY) {
+      const float mn = fmaxf(m, tmax);
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s4[r & 3] += __expf(z[r] - mn);
+      l = l * __expf(m - mn) + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
+      m = mn;
+    }
+  }
+  const float m2 = __shfl_xor(m, 32, 64), l2 = __shfl_xor(l, 32, 64);
+  const float M = fmaxf(m, m2);
+  const float L = (m == -INFINITY ? 0.f : l * __expf(m - M)) + (m2 == -INFINITY ? 0.f : l2 * __expf(m2 - M));
+  if (h == 0 && j < a.N) a.lse[(int64_t)bk * a.N + j] = M + __logf(L);
+}
+
+__device__ __forceinline__ float dot32(const float* x, const float (&y)[32]) {
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 t = *reinterpret_cast<const float4*>(x + 4 * q);
+    s4[0] = fmaf(t.x, y[4 * q], s4[0]);
+    s4[1] = fmaf(t.y, y[4 * q + 1], s4[1]);
+    s4[2] = fmaf(t.z, y[4 * q + 2], s4[2]);
+    s4[3] = fmaf(t.w, y[4 * q + 3], s4[3]);
+  }
+  return (s4[0] + s4[1]) + (s4[2] + s4[3]);
+}
+
+// forward: P and W = T o P on the support of column j (CSC order).  One thread per (b,k,j).
+__global__ __launch_bounds__(256) void flash_psupp_kernel(ChebFl a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)a.B * a.K * a.N) return;
+  const int j = (int)(t % a.N), bk = (int)(t / a.N), k = bk % a.K, b = bk / a.K;
+  const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+  float kv[32];
+  const float* kr = Q + a.kd + (int64_t)j * a.ld;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(kr + 4 * q);
+    kv[4 * q] = v.x; kv[4 * q + 1] = v.y; kv[4 * q + 2] = v.z; kv[4 * q + 3] = v.w;
+  }
+  const float lse = a.lse[t];
+  const float* Mk = a.mask[k];
+  const int64_t base = (int64_t)bk * a.nnz;
+  for (int p = a.csc_ptr[j]; p < a.csc_ptr[j + 1]; ++p) {
+    const int i = a.csc_row[p];
+    const int64_t o = (int64_t)i * a.N + j;
+    const float w = a.apa[o];
+    const float z = dot32(Q + (int64_t)i * a.ld, kv) * a.scale + (w != 0.f ? w * Mk[o] : 0.f);
+    const float P = __expf(z - lse);
+    a.psupp[base + p] = P;
+    a.wsupp[base + p] = a.tsupp[(int64_t)k * a.nnz + p] * P;
+  }
+}
+
+// backward: c_j = sum_i P_ij T_ij dW_ij and dzs_ij = P_ij T_ij dW_ij on the support
+__global__ __launch_bounds__(256) void flash_colc_kernel(ChebFl a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)a.B * a.K * a.N) return;
+  const int j = (int)(t % a.N), bk = (int)(t / a.N), k = bk % a.K;
+  const int64_t base = (int64_t)bk * a.nnz;
+  float c = 0.f;
+  for (int p = a.csc_ptr[j]; p < a.csc_ptr[j + 1]; ++p) {
+    const float d = a.psupp[base + p] * (a.tsupp[(int64_t)k * a.nnz + p] * a.dws[base + p]);
+    a.dzs[base + p] = d;
+    c += d;
+  }
+  a.cc[t] = c;
+}
+
+// backward: dQ'.  One wave per (b, k, 32 rows i); the four waves of a workgroup run the same
+// trip count (tail waves compute a clamped tile and store nothing) and share the barriers.
+__global__ __launch_bounds__(256) void flash_dq_kernel(ChebFl a) {
+  __shared__ float Kt[4][32][33];
+  __shared__ float lse_t[4][32], c_t[4][32];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int nt = (a.N + 31) >> 5;
+  const int64_t total = (int64_t)a.B * a.K * nt;
+  int64_t wid = (int64_t)blockIdx.x * 4 + w;
+  const bool live = wid < total;
+  if (!live) wid = total - 1;
+  const int itl = (int)(wid % nt), bk = (int)(wid / nt), k = bk % a.K, b = bk / a.K;
+  const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+  const float* Kp = Q + a.kd;
+  const int ic = min(itl * 32 + l32, a.N - 1);
+  float bq[16];
+  load16(Q + (int64_t)ic * a.ld + h * 16, bq);
+  const int32_t* br = a.bits + (int64_t)ic * a.nw;
+  const float* Mk = a.mask[k];
+  const float* lseb = a.lse + (int64_t)bk * a.N;
+  const float* cb = a.cc + (int64_t)bk * a.N;
+  floatx16 O = zero16();
+  float ak[16];
+  load16(Kp + (int64_t)min(l32, a.N - 1) * a.ld + h * 16, ak);
+  for (int jt = 0; jt < nt; ++jt) {
+    const int j0 = jt * 32;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) Kt[w][l32][h * 16 + s] = ak[s];
+    if (h == 0) {
+      const int jj = j0 + l32;
+      lse_t[w][l32] = jj < a.N ? lseb[jj] : INFINITY;
+      c_t[w][l32] = jj < a.N ? cb[jj] : 0.f;
+    }
+    floatx16 S = zero16();  // S^T tile: D[m = j][n = i]
+#pragma unroll
+    for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(ak[s], bq[s], S, 0, 0, 0);
+    if (jt + 1 < nt) load16(Kp + (int64_t)min(j0 + 32 + l32, a.N - 1) * a.ld + h * 16, ak);
+    const uint32_t bits = (uint32_t)br[jt];
+    __syncthreads();
+    float pa[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jl = frag_row(r, h);
+      float v = S[r] * a.scale;
+      if ((bits >> jl) & 1u) v += apa_term(a, Mk, ic, j0 + jl);
+      pa[r] = __expf(v - lse_t[w][jl]) * c_t[w][jl];  // P_ij c_j (0 past N: lse = +inf)
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      O = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], Kt[w][frag_row(s, h)][l32], O, 0, 0, 0);
+    __syncthreads();
+  }
+  if (!live) return;
+  const int64_t zb = (int64_t)bk * a.nnz;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = itl * 32 + frag_row(r, h);
+    if (i >= a.N) continue;
+    float sp = 0.f;
+    for (int q = a.csr_ptr[i]; q < a.csr_ptr[i + 1]; ++q)
+      sp = fmaf(a.dzs[zb + a.csr2csc[q]], Kp[(int64_t)a.csr_col[q] * a.ld + l32], sp);
+    a.dqk[((int64_t)b * a.N + i) * a.ld + k * 32 + l32] = (sp - O[r]) * a.scale;
+  }
+}
+
+// backward: dK'.  One wave per (b, k, 32 columns j), same structure as flash_dq_kernel with
+// the S tile (D[m = i][n = j]) whose P fragment is the A operand of P^T . Q'.
+__global__ __launch_bounds__(256) void flash_dk_kernel(ChebFl a) {
+  __shared__ float Qt[4][32][33];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int nt = (a.N + 31) >> 5;
+  const int64_t total = (int64_t)a.B * a.K * nt;
+  int64_t wid = (int64_t)blockIdx.x * 4 + w;
+  const bool live = wid < total;
+  if (!live) wid = total - 1;
+  const int jtl = (int)(wid % nt), bk = (int)(wid / nt), k = bk % a.K, b = bk / a.K;
+  const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+  const float* Kp = Q + a.kd;
+  const int jc = min(jtl * 32 + l32, a.N - 1);
+  float bkv[16];
+  load16(Kp + (int64_t)jc * a.ld + h * 16, bkv);
+  const float lse = a.lse[(int64_t)bk * a.N + jc];
+  const int32_t* bt = a.bits_t + (int64_t)jc * a.nw;
+  const float* Mk = a.mask[k];
+  floatx16 U = zero16();
+  float aq[16];
+  load16(Q + (int64_t)min(l32, a.N - 1) * a.ld + h * 16, aq);
+  for (int it = 0; it < nt; ++it) {
+    const int i0 = it * 32;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) Qt[w][l32][h * 16 + s] = aq[s];
+    floatx16 S = zero16();  // D[m = i][n = j]
+#pragma unroll
+    for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[s], bkv[s], S, 0, 0, 0);
+    if (it + 1 < nt) load16(Q + (int64_t)min(i0 + 32 + l32, a.N - 1) * a.ld + h * 16, aq);
+    const uint32_t bits = (uint32_t)bt[it];
+    __syncthreads();
+    float pr[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int il = frag_row(r, h), i = i0 + il;
+      float v = S[r] * a.scale;
+      if ((bits >> il) & 1u) v += apa_term(a, Mk, i, jc);
+      pr[r] = i < a.N ? __expf(v - lse) : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      U = __builtin_amdgcn_mfma_f32_32x32x2f32(pr[s], Qt[w][frag_row(s, h)][l32], U, 0, 0, 0);
+    __syncthreads();
+  }
+  if (!live) return;
+  const int64_t zb = (int64_t)bk * a.nnz;
+  const float* cb = a.cc + (int64_t)bk * a.N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int j = jtl * 32 + frag_row(r, h);
+    if (j >= a.N) continue;
+    float sp = 0.f;
+    for (int p = a.csc_ptr[j]; p < a.csc_ptr[j + 1]; ++p)
+      sp = fmaf(a.dzs[zb + p], Q[(int64_t)a.csc_row[p] * a.ld + l32], sp);
+    a.dqk[((int64_t)b * a.N + j) * a.ld + a.kd + k * 32 + l32] = (sp - cb[j] * U[r]) * a.scale;
+  }
+}
+
+// backward: dM_k[i,j] = A_pa[i,j] sum_b dz_b[i,j] on the A_pa support.  One wave per (k, j),
+// lanes over the batch; P recomputed by a 32-long dot product per (b, i, j).
+__global__ __launch_bounds__(256) void flash_mask_grad_kernel(ChebFl a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= (int64_t)a.K * a.N) return;
+  const int j = (int)(wid % a.N), k = (int)(wid / a.N);
+  const float* Mk = a.mask[k];
+  float* dM = a.dmask[k];
+  if (!dM) return;
+  for (int q = a.apa_ptr[j]; q < a.apa_ptr[j + 1]; ++q) {
+    const int i = a.apa_row[q];
+    const int64_t o = (int64_t)i * a.N + j;
+    const float w = a.apa[o];
+    int pt = -1;  // the T-support entry (i, j), if any
+    for (int p = a.csc_ptr[j]; p < a.csc_ptr[j + 1]; ++p)
+      if (a.csc_row[p] == i) pt = p;
+    float s = 0.f;
+    for (int b = lane; b < a.B; b += 64) {
+      const int bk = b * a.K + k;
+      const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+      float kv[32];
+      const float* kr = Q + a.kd + (int64_t)j * a.ld;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(kr + 4 * u);
+        kv[4 * u] = v.x; kv[4 * u + 1] = v.y; kv[4 * u + 2] = v.z; kv[4 * u + 3] = v.w;
+      }
+      const float z = dot32(Q + (int64_t)i * a.ld, kv) * a.scale + w * Mk[o];
+      const float P = __expf(z - a.lse[(int64_t)bk * a.N + j]);
+      const float dzs = pt >= 0 ? a.dzs[(int64_t)bk * a.nnz + pt] : 0.f;
+      s += dzs - P * a.cc[(int64_t)bk * a.N + j];
+    }
+    s = wave_sum(s);
+    if (lane == 0) dM[o] = w * s;
+  }
+}
+
+unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
+
+}  // namespace
+
+int op_flash_forward(const ChebFl& a, hipStream_t st) {
+  const int nt = (a.N + 31) >> 5;
+  hipLaunchKernelGGL(flash_stats_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(flash_psupp_kernel, dim3((unsigned)cdiv64((int64_t)a.B * a.K * a.N, 256)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_flash_colc(const ChebFl& a, hipStream_t st) {
+  hipLaunchKernelGGL(flash_colc_kernel, dim3((unsigned)cdiv64((int64_t)a.B * a.K * a.N, 256)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_flash_dqk(const ChebFl& a, hipStream_t st) {
+  const int nt = (a.N + 31) >> 5;
+  hipLaunchKernelGGL(flash_dq_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(flash_dk_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
+int op_flash_mask_grad(const ChebFl& a, hipStream_t st) {
+  for (int k = 0; k < a.K; ++k) {
+    if (!a.dmask[k]) continue;
+    hipError_t e = hipMemsetAsync(a.dmask[k], 0, sizeof(float) * (size_t)a.N * a.N, st);
+    if (e != hipSuccess) { set_last_error(std::string("memset: ") + hipGetErrorString(e)); return (int)e; }
+  }
+  hipLaunchKernelGGL(flash_mask_grad_kernel, dim3(grid_waves((int64_t)a.K * a.N)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
+  return 0;
+}

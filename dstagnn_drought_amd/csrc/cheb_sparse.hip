@@ -13,6 +13,8 @@
 //   spmm_fwd    out[b,j,:]   = ReLU( sum_k sum_{i in supp(j)} T_k[i,j] P[b,k,i,j] xth[b,i,:,k,:] )
 //   sddmm_bwd   dW[b,k,i,j]  = <xth[b,i,:,k,:], g[b,j,:]>          for (i,j) in supp
 //   spmm_t_bwd  dxth[b,i,:,k,:] = sum_{j in supp_row(i)} T_k[i,j] P[b,k,i,j] g[b,j,:]
+// On the fused (flash) path T o P and dW are compact (B,K,nnz) arrays in CSC order
+// (ChebSp::wsupp / dws; the CSR walk maps through csr2csc) and P is never dense.
 // Layouts: xth (B,N,T,K,C) (the Theta GEMM's plain row-major output), out / g (B,N,T,C).
 // Element e = t*C + c of a node's C*T vector sits at e + t*(K-1)*C inside the node's
 // xth block, plus k*C.
@@ -59,10 +61,11 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   for (int k = 0; k < a.K; ++k) {
     const float* Pk = a.P + ((int64_t)b * a.K + k) * NN;
     const float* Tk = a.cheb + (int64_t)k * NN;
+    const float* Wk = a.wsupp ? a.wsupp + ((int64_t)b * a.K + k) * a.nnz : nullptr;
     for (int p = p0; p < p1; ++p) {
       const int i = a.csc_row[p];
       const int64_t o = (int64_t)i * a.N + j;
-      const float w = Tk[o] * Pk[o];
+      const float w = Wk ? Wk[p] : Tk[o] * Pk[o];
       const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
 #pragma unroll
       for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, xr[xo[q]], acc[q]);
@@ -97,6 +100,7 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
     xth_offsets<kNQ>(a, 0, lane, xo);
     for (int k = 0; k < a.K; ++k) {
       float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
+      float* dSk = a.dws ? a.dws + ((int64_t)b * a.K + k) * a.nnz : nullptr;
       for (int p = p0; p < p1; ++p) {
         const int i = a.csc_row[p];
         const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
@@ -104,13 +108,17 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
 #pragma unroll
         for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], xr[xo[q]], s);
         s = wave_sum(s);
-        if (lane == 0) dWk[(int64_t)i * a.N + j] = s;
+        if (lane == 0) {
+          if (dSk) dSk[p] = s;
+          else dWk[(int64_t)i * a.N + j] = s;
+        }
       }
     }
     return;
   }
   for (int k = 0; k < a.K; ++k) {  // long rows: the dot product walks the chunks
     float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
+    float* dSk = a.dws ? a.dws + ((int64_t)b * a.K + k) * a.nnz : nullptr;
     for (int p = p0; p < p1; ++p) {
       const int i = a.csc_row[p];
       const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
@@ -125,7 +133,10 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
         }
       }
       s = wave_sum(s);
-      if (lane == 0) dWk[(int64_t)i * a.N + j] = s;
+      if (lane == 0) {
+        if (dSk) dSk[p] = s;
+        else dWk[(int64_t)i * a.N + j] = s;
+      }
     }
   }
 }
@@ -145,13 +156,14 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
   for (int k = 0; k < a.K; ++k) {
     const float* Pk = a.P + ((int64_t)b * a.K + k) * NN;
     const float* Tk = a.cheb + (int64_t)k * NN;
+    const float* Wk = a.wsupp ? a.wsupp + ((int64_t)b * a.K + k) * a.nnz : nullptr;
     float acc[kNQ];
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) acc[q] = 0.f;
     for (int p = p0; p < p1; ++p) {
       const int j = a.csr_col[p];
       const int64_t o = (int64_t)i * a.N + j;
-      const float w = Tk[o] * Pk[o];
+      const float w = Wk ? Wk[a.csr2csc[p]] : Tk[o] * Pk[o];
       const float* gr = a.g + ((int64_t)b * a.N + j) * a.CT;
 #pragma unroll
       for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, gr[min(e0 + lane + 64 * q, a.CT - 1)], acc[q]);

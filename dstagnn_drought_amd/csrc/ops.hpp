@@ -130,8 +130,36 @@ struct ChebSp {
   const float* g = nullptr;      // (B,N,T,C)  bwd: d(pre-ReLU out)
   float* dW = nullptr;           // (B,K,N,N) bwd: written on the support only
   float* dxth = nullptr;         // (B,N,T,K,C) bwd
+  // fused (flash) path: W = T o P and dW kept compact on the support, (B,K,nnz) in CSC order
+  int nnz = 0;
+  const float* wsupp = nullptr;  // fwd / spmm_t: replaces T_k[i,j] P[b,k,i,j]
+  float* dws = nullptr;          // sddmm: written instead of dW
+  const int* csr2csc = nullptr;  // CSR position -> CSC position
 };
 bool cheb_sparse_ok(int CT);
+
+// fused (flash-style) Chebyshev attention (cheb_flash.hip); dk == 32
+struct ChebFl {
+  int B = 0, N = 0, K = 0, nnz = 0, nw = 0;  // nw = 32-bit words per A_pa bit row
+  float scale = 1.f;                       // 1/sqrt(dk)
+  const float* qk = nullptr; int64_t ld = 0; int kd = 0;  // (B*N, ld) rows [Q'_0..Q'_{K-1} | K'_0..]
+  const float* apa = nullptr;              // (N,N)
+  const float* mask[DSTAGNN_MAX_K] = {};   // (N,N) each
+  const int32_t* bits = nullptr;           // (N, nw): bit j of row i = A_pa[i,j] != 0
+  const int32_t* bits_t = nullptr;         // (N, nw): bit i of row j
+  const int *csc_ptr = nullptr, *csc_row = nullptr, *csr_ptr = nullptr, *csr_col = nullptr, *csr2csc = nullptr;
+  const int *apa_ptr = nullptr, *apa_row = nullptr;  // CSC of the A_pa support
+  const float* tsupp = nullptr;            // (K, nnz) T_k on the union support, CSC order
+  float* lse = nullptr;                    // (B,K,N) column log-sum-exp
+  float* psupp = nullptr; float* wsupp = nullptr;  // (B,K,nnz)
+  const float* dws = nullptr; float* dzs = nullptr; float* cc = nullptr;  // (B,K,nnz) x2, (B,K,N)
+  float* dqk = nullptr;                    // (B*N, ld) dQ' | dK'
+  float* dmask[DSTAGNN_MAX_K] = {};        // (N,N) each, fully written
+};
+int op_flash_forward(const ChebFl& a, hipStream_t st);   // lse, psupp, wsupp
+int op_flash_colc(const ChebFl& a, hipStream_t st);      // cc, dzs
+int op_flash_dqk(const ChebFl& a, hipStream_t st);       // dqk
+int op_flash_mask_grad(const ChebFl& a, hipStream_t st); // dmask
 int op_cheb_spmm_fwd(const ChebSp& a, hipStream_t st);
 int op_cheb_sddmm_bwd(const ChebSp& a, hipStream_t st);
 int op_cheb_spmm_t_bwd(const ChebSp& a, hipStream_t st);

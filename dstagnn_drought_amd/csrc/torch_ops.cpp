@@ -69,8 +69,9 @@ static_assert(sizeof(dstagnn_block_grads) == kSlots * sizeof(void*), "grads stru
 // quirk 11, their .grad stays None)
 bool unused_inner(int64_t slot) { return slot == 2 || slot == 3 || slot == 4 || slot == 38 || slot == 39; }
 
-// cfg = [n_heads, d_k, d_v, d_model, K, C]; flags: 1 train, 2 sparse, 4 direct grads, 8 poison
-enum { kTrain = 1, kSparse = 2, kDirect = 4, kPoison = 8 };
+// cfg = [n_heads, d_k, d_v, d_model, K, C]; flags: 1 train, 2 sparse, 4 direct grads, 8 poison,
+// 16 fused (flash) Chebyshev attention
+enum { kTrain = 1, kSparse = 2, kDirect = 4, kPoison = 8, kFlash = 16 };
 
 int res_mode_of(const c10::optional<Tensor>& res, int64_t F) {
   if (!res.has_value() || !res->defined()) return DSTAGNN_RES_NONE;
@@ -91,13 +92,17 @@ struct BlockCall {
   int64_t flags = 0;
 };
 
+dstagnn_graph graph_of(at::TensorList graph, bool sparse);
+
 BlockCall make_call(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params, at::IntArrayRef slots,
                     at::TensorList graph, at::IntArrayRef cfg, double drop_p, int64_t seed, int64_t flags) {
   check_dev(x, at::kFloat, "x");
   TORCH_CHECK(x.dim() == 4, "x must be (B,N,F,T), got ", x.sizes());
   TORCH_CHECK(cfg.size() == 6, "cfg must be [n_heads, d_k, d_v, d_model, K, C]");
   TORCH_CHECK(params.size() == slots.size(), "params / slots length mismatch");
-  TORCH_CHECK(graph.size() == 2 || graph.size() == 6, "graph = [cheb, adj_pa] or + [csc_ptr, csc_row, csr_ptr, csr_col]");
+  TORCH_CHECK(graph.size() == 2 || graph.size() == 6 || graph.size() == 12,
+              "graph = [cheb, adj_pa] (+ csc_ptr, csc_row, csr_ptr, csr_col (+ csr2csc, apa_bits, apa_bits_t, "
+              "apa_ptr, apa_row, tsupp))");
   BlockCall c;
   c.flags = flags;
   c.mode = res_mode_of(res, x.size(2));
@@ -118,19 +123,10 @@ BlockCall make_call(const Tensor& x, const c10::optional<Tensor>& res, at::Tenso
     check_dev(params[i], at::kFloat, "parameter");
     arr[slots[i]] = params[i].data_ptr<float>();
   }
-  check_dev(graph[0], at::kFloat, "cheb");
-  check_dev(graph[1], at::kFloat, "adj_pa");
-  c.g.cheb = graph[0].data_ptr<float>();
-  c.g.adj_pa = graph[1].data_ptr<float>();
-  if (graph.size() == 6) {
-    for (int i = 2; i < 6; ++i) check_dev(graph[i], at::kInt, "graph support");
-    c.g.nnz = (int)graph[3].numel();
-    c.g.csc_ptr = graph[2].data_ptr<int>();
-    c.g.csc_row = graph[3].data_ptr<int>();
-    c.g.csr_ptr = graph[4].data_ptr<int>();
-    c.g.csr_col = graph[5].data_ptr<int>();
-  }
-  TORCH_CHECK(!d.cheb_sparse || c.g.nnz > 0, "sparse Chebyshev path requested without a CSC/CSR support");
+  c.g = graph_of(graph, d.cheb_sparse != 0);
+  d.cheb_flash = (flags & kFlash) ? 1 : 0;
+  TORCH_CHECK(!d.cheb_flash || graph.size() == 12, "flash Chebyshev path requested without its graph data");
+  d.cheb_nnz = d.cheb_flash ? c.g.nnz : 0;
   return c;
 }
 
@@ -387,17 +383,29 @@ std::tuple<Tensor, Tensor> dropout_masks(const Tensor& like, at::IntArrayRef sha
 constexpr int64_t kGemmWsBytes = int64_t(8) << 22;  // the library's split-K slab (8M floats)
 
 dstagnn_graph graph_of(at::TensorList graph, bool sparse) {
-  TORCH_CHECK(graph.size() == 2 || graph.size() == 6, "graph = [cheb, adj_pa] or + CSC/CSR support");
+  TORCH_CHECK(graph.size() == 2 || graph.size() == 6 || graph.size() == 12, "graph: 2, 6 or 12 tensors");
   dstagnn_graph g{};
   check_dev(graph[0], at::kFloat, "cheb");
   check_dev(graph[1], at::kFloat, "adj_pa");
   g.cheb = graph[0].data_ptr<float>();
   g.adj_pa = graph[1].data_ptr<float>();
-  if (graph.size() == 6) {
+  if (graph.size() >= 6) {
     for (int i = 2; i < 6; ++i) check_dev(graph[i], at::kInt, "graph support");
     g.nnz = (int)graph[3].numel();
     g.csc_ptr = graph[2].data_ptr<int>(); g.csc_row = graph[3].data_ptr<int>();
     g.csr_ptr = graph[4].data_ptr<int>(); g.csr_col = graph[5].data_ptr<int>();
+  }
+  if (graph.size() == 12) {  // csr2csc, apa_bits, apa_bits_t, apa_ptr, apa_row, tsupp
+    for (int i = 6; i < 11; ++i) check_dev(graph[i], at::kInt, "flash graph data");
+    check_dev(graph[11], at::kFloat, "tsupp");
+    TORCH_CHECK(graph[6].numel() == g.nnz && graph[11].numel() % std::max(1, g.nnz) == 0, "flash graph data: sizes");
+    g.csr2csc = graph[6].data_ptr<int>();
+    g.apa_bits = graph[7].data_ptr<int32_t>();
+    g.apa_bits_t = graph[8].data_ptr<int32_t>();
+    g.apa_ptr = graph[9].data_ptr<int>();
+    g.apa_row = graph[10].data_ptr<int>();
+    g.apa_nnz = (int)graph[10].numel();
+    g.tsupp = graph[11].data_ptr<float>();
   }
   TORCH_CHECK(!sparse || g.nnz > 0, "sparse path requested without a CSC/CSR support");
   return g;

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .block_fn import block_call, slots_of
+from .block_fn import block_call, slots_of, use_flash
 from .head_fn import DSTAGNNHeadFunction
 from .graph import cheb_polynomial, scaled_Laplacian
 
@@ -101,18 +101,47 @@ def support_index(cheb_stack):
     of the union support of the stacked Chebyshev polynomials (K,N,N)."""
     nz = (cheb_stack != 0).any(dim=0)
     N = nz.shape[0]
-    cols = [torch.nonzero(nz[:, j], as_tuple=False).reshape(-1) for j in range(N)]
-    rows = [torch.nonzero(nz[i, :], as_tuple=False).reshape(-1) for i in range(N)]
 
-    def pack(lists):
+    def pack(m):  # rows of m in order -> (ptr, column indices)
+        r, c = torch.nonzero(m, as_tuple=True)
         ptr = torch.zeros(N + 1, dtype=torch.int32)
-        ptr[1:] = torch.cumsum(torch.tensor([len(v) for v in lists], dtype=torch.int64), 0).to(torch.int32)
-        idx = torch.cat(lists).to(torch.int32) if lists else torch.zeros(0, dtype=torch.int32)
-        return ptr, idx
+        ptr[1:] = torch.cumsum(torch.bincount(r, minlength=N), 0).to(torch.int32)
+        return ptr, c.to(torch.int32)
 
-    csc_ptr, csc_row = pack(cols)
-    csr_ptr, csr_col = pack(rows)
+    csc_ptr, csc_row = pack(nz.t())
+    csr_ptr, csr_col = pack(nz)
     return csc_ptr, csc_row, csr_ptr, csr_col
+
+
+def _bits(m):
+    """(N, ceil(N/32)) int32 words: bit (c % 32) of word [r][c // 32] = m[r][c]."""
+    R, C = m.shape
+    nw = (C + 31) // 32
+    pad = torch.zeros(R, nw * 32, dtype=torch.int64, device=m.device)
+    pad[:, :C] = m.to(torch.int64)
+    w = (pad.view(R, nw, 32) << torch.arange(32, device=m.device, dtype=torch.int64)).sum(-1)
+    return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32).contiguous()
+
+
+def flash_support(cheb_stack, csc_ptr, csc_row, csr_ptr, csr_col, adj_pa):
+    """Index data of the fused (flash-style) Chebyshev attention (cheb_flash.hip): csr2csc
+    (the CSC position of every CSR entry of the T_k union support), tsupp (K, nnz) = T_k on
+    that support in CSC order, the A_pa support as bit rows (apa_bits: row i, bit j) and bit
+    columns (apa_bits_t: column j, bit i), and its CSC (apa_ptr, apa_row).  Built on
+    adj_pa's device."""
+    dev = adj_pa.device
+    N = adj_pa.shape[0]
+    cp, cr = csc_ptr.to(dev).long(), csc_row.to(dev).long()
+    rp, rc = csr_ptr.to(dev).long(), csr_col.to(dev).long()
+    ccol = torch.repeat_interleave(torch.arange(N, device=dev), cp[1:] - cp[:-1])
+    rrow = torch.repeat_interleave(torch.arange(N, device=dev), rp[1:] - rp[:-1])
+    csc_key = ccol * N + cr                      # sorted (column-major order)
+    csr2csc = torch.searchsorted(csc_key, rc * N + rrow).to(torch.int32)
+    tsupp = cheb_stack.to(dev)[:, cr, ccol].contiguous()
+    nz = adj_pa != 0
+    apa_ptr, apa_row, _, _ = support_index(nz.unsqueeze(0).cpu())
+    return {"csr2csc": csr2csc, "tsupp": tsupp, "apa_bits": _bits(nz), "apa_bits_t": _bits(nz.t()),
+            "apa_ptr": apa_ptr.to(dev), "apa_row": apa_row.to(dev)}
 
 
 class cheb_conv(nn.Module):
@@ -190,6 +219,9 @@ class DSTAGNN_block(nn.Module):
         self.num_of_d = num_of_d
         self.nb_time_filter = nb_time_filter
         self.sparse_cheb = True  # use the CSC/CSR support path when the support is sparse
+        # fused (flash-style) Chebyshev attention for large graphs: None = automatic (sparse
+        # path, d_k == 32, N >= 1024), True / False force it (block_fn.use_flash)
+        self.flash_cheb = None
         self.direct_grads = False  # see set_direct_grads
         self.grads_ready = None    # DP hook: called with the block once its gradients are final
 
@@ -209,8 +241,11 @@ class DSTAGNN_block(nn.Module):
         drop = self.training and meta.get("drop_p", 0.0) > 0.0
         meta["seed"] = _rank_seed(int(torch.randint(0, 2 ** 62, (1,)).item())) if drop else 0
         names, params, slots = self._param_list()
-        out, re_at = block_call(x, res_att, params, slots, self._graph(), meta, meta["train"], meta["seed"],
-                                self.direct_grads)
+        graph = self._graph()
+        if use_flash(graph, meta, T, self.flash_cheb):
+            graph = self._flash_graph(graph)
+        out, re_at = block_call(x, res_att, params, slots, graph, meta, meta["train"], meta["seed"],
+                                self.direct_grads, flash=self.flash_cheb)
         if self.grads_ready is not None and out.requires_grad:
             # DP overlap (dp.GradAllReducer.attach): once this block's backward node has run,
             # its parameter gradients are final — hand them over from a post-hook on the node
@@ -249,6 +284,14 @@ class DSTAGNN_block(nn.Module):
             c = (key, graph)
             self.__dict__["_gcache"] = c
         return c[1]
+
+    def _flash_graph(self, graph):
+        """graph + the flash-attention index data (built once per graph, on its device)."""
+        if "csr2csc" not in graph:
+            cc = self.cheb_conv_SAt
+            graph.update(flash_support(cc.cheb_stack, graph["csc_ptr"], graph["csc_row"], graph["csr_ptr"],
+                                       graph["csr_col"], graph["adj_pa"]))
+        return graph
 
 
 class DSTAGNN_submodule(nn.Module):

@@ -63,6 +63,11 @@ typedef struct dstagnn_block_dims {
                               (T_k elementwise recurrence => ~3 nnz/column, quirk 4);
                               0: dense (N,N) T_k.  Rows of any length C*T <= 2^20
                               (walked in 1024-element chunks).                      */
+  int cheb_flash;          /* 1 (requires cheb_sparse, d_k == 32 and the flash fields of
+                              dstagnn_graph): fused Chebyshev attention — the (B,K,N,N)
+                              scores / softmax / score gradient are never materialised;
+                              S tiles are recomputed from Q', K' on the matrix cores    */
+  int cheb_nnz;            /* flash path: entries of the union support (== graph nnz)   */
 } dstagnn_block_dims;
 
 /* Parameter pointers in state_dict order.  For the first block
@@ -123,6 +128,14 @@ typedef struct dstagnn_graph {
   const int* csc_row;    /* (nnz) */
   const int* csr_ptr;    /* (N+1) */
   const int* csr_col;    /* (nnz) */
+  /* fused (flash) path only (cheb_flash = 1), else NULL / 0: */
+  const int* csr2csc;          /* (nnz)  CSC position of every CSR entry                      */
+  const int32_t* apa_bits;     /* (N, ceil(N/32)) bit j%32 of word [i][j/32] = adj_pa[i,j] != 0 */
+  const int32_t* apa_bits_t;   /* (N, ceil(N/32)) bit i%32 of word [j][i/32] = adj_pa[i,j] != 0 */
+  int apa_nnz;                 /* entries of the adj_pa support                                */
+  const int* apa_ptr;          /* (N+1)  CSC of the adj_pa support: per column j ...            */
+  const int* apa_row;          /* (apa_nnz) ... the rows i                                     */
+  const float* tsupp;          /* (K, nnz) T_k on the union support, CSC order                  */
 } dstagnn_graph;
 
 /* Bytes needed for the forward->backward `save` buffer and the per-call scratch. */

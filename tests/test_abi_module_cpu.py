@@ -22,7 +22,8 @@ def header_functions():
 class BlockDims(ctypes.Structure):  # struct dstagnn_block_dims (include/dstagnn.h)
     _fields_ = [(n, ctypes.c_int) for n in ("B", "N", "F", "T", "n_heads", "d_k", "d_v", "d_model", "K", "C",
                                             "res_mode", "train")] + \
-        [("drop_p", ctypes.c_float), ("seed", ctypes.c_uint64), ("cheb_sparse", ctypes.c_int)]
+        [("drop_p", ctypes.c_float), ("seed", ctypes.c_uint64), ("cheb_sparse", ctypes.c_int),
+         ("cheb_flash", ctypes.c_int), ("cheb_nnz", ctypes.c_int)]
 
 
 def c_abi():
