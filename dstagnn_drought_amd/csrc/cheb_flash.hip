@@ -37,6 +37,16 @@ __device__ __forceinline__ void load16(const float* p, float (&v)[16]) {
 
 __device__ __forceinline__ int frag_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// Each wave stages its tile in its own LDS slice and only its own lanes read it back, so the
+// hand-off needs no workgroup barrier: a wavefront-scope release/acquire orders the LDS
+// accesses (the compiler may not move a read of another lane's element above this lane's
+// writes) and waves run independently.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ floatx16 zero16() {
   floatx16 z;
 #pragma unroll
@@ -156,17 +166,14 @@ __global__ __launch_bounds__(256) void flash_colc_kernel(ChebFl a) {
   a.cc[t] = c;
 }
 
-// backward: dQ'.  One wave per (b, k, 32 rows i); the four waves of a workgroup run the same
-// trip count (tail waves compute a clamped tile and store nothing) and share the barriers.
+// backward: dQ'.  One wave per (b, k, 32 rows i), independent (own LDS slice).
 __global__ __launch_bounds__(256) void flash_dq_kernel(ChebFl a) {
   __shared__ float Kt[4][32][33];
   __shared__ float lse_t[4][32], c_t[4][32];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const int nt = (a.N + 31) >> 5;
-  const int64_t total = (int64_t)a.B * a.K * nt;
-  int64_t wid = (int64_t)blockIdx.x * 4 + w;
-  const bool live = wid < total;
-  if (!live) wid = total - 1;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + w;
+  if (wid >= (int64_t)a.B * a.K * nt) return;
   const int itl = (int)(wid % nt), bk = (int)(wid / nt), k = bk % a.K, b = bk / a.K;
   const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
   const float* Kp = Q + a.kd;
@@ -194,7 +201,7 @@ __global__ __launch_bounds__(256) void flash_dq_kernel(ChebFl a) {
     for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(ak[s], bq[s], S, 0, 0, 0);
     if (jt + 1 < nt) load16(Kp + (int64_t)min(j0 + 32 + l32, a.N - 1) * a.ld + h * 16, ak);
     const uint32_t bits = (uint32_t)br[jt];
-    __syncthreads();
+    wave_lds_sync();
     float pa[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -206,9 +213,8 @@ __global__ __launch_bounds__(256) void flash_dq_kernel(ChebFl a) {
 #pragma unroll
     for (int s = 0; s < 16; ++s)
       O = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], Kt[w][frag_row(s, h)][l32], O, 0, 0, 0);
-    __syncthreads();
+    wave_lds_sync();
   }
-  if (!live) return;
   const int64_t zb = (int64_t)bk * a.nnz;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -227,10 +233,8 @@ __global__ __launch_bounds__(256) void flash_dk_kernel(ChebFl a) {
   __shared__ float Qt[4][32][33];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const int nt = (a.N + 31) >> 5;
-  const int64_t total = (int64_t)a.B * a.K * nt;
-  int64_t wid = (int64_t)blockIdx.x * 4 + w;
-  const bool live = wid < total;
-  if (!live) wid = total - 1;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + w;
+  if (wid >= (int64_t)a.B * a.K * nt) return;
   const int jtl = (int)(wid % nt), bk = (int)(wid / nt), k = bk % a.K, b = bk / a.K;
   const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
   const float* Kp = Q + a.kd;
@@ -252,7 +256,7 @@ __global__ __launch_bounds__(256) void flash_dk_kernel(ChebFl a) {
     for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[s], bkv[s], S, 0, 0, 0);
     if (it + 1 < nt) load16(Q + (int64_t)min(i0 + 32 + l32, a.N - 1) * a.ld + h * 16, aq);
     const uint32_t bits = (uint32_t)bt[it];
-    __syncthreads();
+    wave_lds_sync();
     float pr[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -264,9 +268,8 @@ __global__ __launch_bounds__(256) void flash_dk_kernel(ChebFl a) {
 #pragma unroll
     for (int s = 0; s < 16; ++s)
       U = __builtin_amdgcn_mfma_f32_32x32x2f32(pr[s], Qt[w][frag_row(s, h)][l32], U, 0, 0, 0);
-    __syncthreads();
+    wave_lds_sync();
   }
-  if (!live) return;
   const int64_t zb = (int64_t)bk * a.nnz;
   const float* cb = a.cc + (int64_t)bk * a.N;
 #pragma unroll
@@ -318,6 +321,16 @@ __global__ __launch_bounds__(256) void flash_mask_grad_kernel(ChebFl a) {
   }
 }
 
+// dM_k = 0 off the A_pa support: every (N,N) mask gradient in one launch (hipMemsetAsync ran at
+// ~0.2 TB/s here, 0.4 ms per 67 MB mask at N = 4096)
+__global__ __launch_bounds__(256) void flash_zero_kernel(ChebFl a) {
+  const int64_t NN = (int64_t)a.N * a.N, tot = NN * a.K;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (int64_t)gridDim.x * 256) {
+    const int k = (int)(e / NN);
+    if (a.dmask[k]) a.dmask[k][e - (int64_t)k * NN] = 0.f;
+  }
+}
+
 unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
 
 }  // namespace
@@ -347,11 +360,9 @@ int op_flash_dqk(const ChebFl& a, hipStream_t st) {
 }
 
 int op_flash_mask_grad(const ChebFl& a, hipStream_t st) {
-  for (int k = 0; k < a.K; ++k) {
-    if (!a.dmask[k]) continue;
-    hipError_t e = hipMemsetAsync(a.dmask[k], 0, sizeof(float) * (size_t)a.N * a.N, st);
-    if (e != hipSuccess) { set_last_error(std::string("memset: ") + hipGetErrorString(e)); return (int)e; }
-  }
+  const int64_t tot = (int64_t)a.K * a.N * a.N;
+  hipLaunchKernelGGL(flash_zero_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(tot, 256), 8192)), dim3(256), 0, st, a);
+  DS_CHECK_LAUNCH();
   hipLaunchKernelGGL(flash_mask_grad_kernel, dim3(grid_waves((int64_t)a.K * a.N)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   return 0;

@@ -363,73 +363,150 @@ __global__ __launch_bounds__(256) void tat_bwd_kernel(TatArgs a) {
   }
 }
 
-// Long-series variant (GAMBIA T=144: A and dA together exceed the 160 KB of LDS): only A
-// stays resident.  dV first (needs A), then per column j one thread forms
-// c_j = sum_i A_ij dA_ij and overwrites column j of A with dS (dA recomputed from
-// dctx . V, dv FMAs per element), then dQ / dK from dS.
-__global__ __launch_bounds__(256) void tat_bwd_lowmem_kernel(TatArgs a) {
+// Long-series variants (GAMBIA T = 144: one workgroup per (b,f,head) problem would hold
+// 140-160 KB of LDS and leave most of its threads idle in the column phases).  The query-axis
+// softmax normalises each COLUMN j over the rows i, so a problem splits into column chunks of
+// kTatCW columns, one workgroup each (B*F*h*ceil(T/kTatCW) workgroups):
+//   fwd  S[:, chunk] -> re_At, softmax -> att; then ctx = att . V as one batched GEMM
+//   bwd  dA[:, chunk] = dctx . V_chunk^T, dV_chunk = A_chunk^T dctx, dS[:, chunk] (-> d score),
+//        dK_chunk = s dS_chunk^T Q; then dQ = s dS . K as one batched GEMM
+constexpr int kTatCW = 16;
+
+__host__ __device__ inline int tat_cols_fwd_floats(int T, int dk) {
+  return T * (dk + 1) + kTatCW * (dk + 1) + T * kTatCW + 2 * 16 * 16;
+}
+__host__ __device__ inline int tat_cols_bwd_floats(int T, int dk, int dv) {
+  return T * (dk + 1) + T * (dv + 1) + kTatCW * (dv + 1) + 2 * T * kTatCW + 16 * 16;
+}
+
+// column reduction helper: 256 threads = 16 columns x 16 row groups (tid = g * 16 + jj)
+__device__ __forceinline__ float col_reduce16(float v, float* red, bool is_max) {
+  const int jj = threadIdx.x & 15, g = threadIdx.x >> 4;
+  red[g * 16 + jj] = v;
+  __syncthreads();
+  float r = red[jj];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) r = is_max ? fmaxf(r, red[q * 16 + jj]) : r + red[q * 16 + jj];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void tat_fwd_cols_kernel(TatArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int T = a.T, dk = a.dk, dv = a.dv;
-  const int dkp = dk + 1, dvp = dv + 1;
+  const int T = a.T, dk = a.dk, dkp = dk + 1;
+  const int nch = (T + kTatCW - 1) / kTatCW;
+  const int id = blockIdx.x / nch, j0 = (blockIdx.x % nch) * kTatCW, cw = min(kTatCW, T - j0);
   float* Qs = sm;
   float* Ks = Qs + T * dkp;
-  float* Vs = Ks + T * dkp;
-  float* dCs = Vs + T * dvp;    // T*dvp
-  float* As = dCs + T * dvp;    // T*T  (A, then dS column by column)
-  const int id = blockIdx.x;
-  const int hd = id % a.h;
-  const int bf = id / a.h;
-  const int ld = 2 * a.h * dk + a.h * dv;
-  const int ldc = a.h * dv;
+  float* Ss = Ks + kTatCW * dkp;   // [i][jj]
+  float* red = Ss + T * kTatCW;
+  const int hd = id % a.h, bf = id / a.h, b = bf / a.F;
+  const int ld = 2 * a.h * dk + a.h * a.dv;
+  const float* base = a.qkv + (int64_t)bf * T * ld;
+  for (int e = threadIdx.x; e < T * dk; e += 256) {
+    const int i = e / dk, d = e - i * dk;
+    Qs[i * dkp + d] = base[(int64_t)i * ld + hd * dk + d];
+  }
+  for (int e = threadIdx.x; e < cw * dk; e += 256) {
+    const int jj = e / dk, d = e - jj * dk;
+    Ks[jj * dkp + d] = base[(int64_t)(j0 + jj) * ld + a.h * dk + hd * dk + d];
+  }
+  __syncthreads();
+  const int64_t sbase = (int64_t)id * T * T;
+  const float* rp = nullptr;
+  if (a.res_mode == DSTAGNN_RES_BCAST) rp = a.res + ((int64_t)b * a.h + hd) * T * T;
+  else if (a.res_mode == DSTAGNN_RES_FULL) rp = a.res + sbase;
+  for (int e = threadIdx.x; e < T * kTatCW; e += 256) {
+    const int i = e / kTatCW, jj = e - i * kTatCW;
+    float sc = 0.f;
+    if (jj < cw) {
+      for (int d = 0; d < dk; ++d) sc = fmaf(Qs[i * dkp + d], Ks[jj * dkp + d], sc);
+      sc *= a.scale;
+      if (rp) sc += rp[(int64_t)i * T + j0 + jj];
+      a.re_at[sbase + (int64_t)i * T + j0 + jj] = sc;
+    }
+    Ss[e] = sc;
+  }
+  __syncthreads();
+  const int jj = threadIdx.x & 15, g = threadIdx.x >> 4;
+  float m = -INFINITY;
+  for (int i = g; i < T; i += 16) m = fmaxf(m, Ss[i * kTatCW + jj]);
+  m = col_reduce16(m, red, true);
+  float l = 0.f;
+  for (int i = g; i < T; i += 16) l += __expf(Ss[i * kTatCW + jj] - m);
+  l = col_reduce16(l, red, false);
+  const float inv = 1.f / l;
+  if (jj < cw)
+    for (int i = g; i < T; i += 16) a.att[sbase + (int64_t)i * T + j0 + jj] = __expf(Ss[i * kTatCW + jj] - m) * inv;
+}
+
+__global__ __launch_bounds__(256) void tat_bwd_cols_kernel(TatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int T = a.T, dk = a.dk, dv = a.dv, dkp = dk + 1, dvp = dv + 1;
+  const int nch = (T + kTatCW - 1) / kTatCW;
+  const int id = blockIdx.x / nch, j0 = (blockIdx.x % nch) * kTatCW, cw = min(kTatCW, T - j0);
+  float* Qs = sm;                       // T x dkp
+  float* dCs = Qs + T * dkp;            // T x dvp
+  float* Vs = dCs + T * dvp;            // kTatCW x dvp
+  float* As = Vs + kTatCW * dvp;        // [i][jj]
+  float* dAs = As + T * kTatCW;         // [i][jj] -> dS
+  float* red = dAs + T * kTatCW;
+  const int hd = id % a.h, bf = id / a.h;
+  const int ld = 2 * a.h * dk + a.h * dv, ldc = a.h * dv;
   const float* base = a.qkv + (int64_t)bf * T * ld;
   const float* cb = a.dctx + (int64_t)bf * T * ldc;
   const int64_t sbase = (int64_t)id * T * T;
-  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
-    int i = e / dk, d = e % dk;
+  for (int e = threadIdx.x; e < T * dk; e += 256) {
+    const int i = e / dk, d = e - i * dk;
     Qs[i * dkp + d] = base[(int64_t)i * ld + hd * dk + d];
-    Ks[i * dkp + d] = base[(int64_t)i * ld + a.h * dk + hd * dk + d];
   }
-  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {
-    int i = e / dv, d = e % dv;
-    Vs[i * dvp + d] = base[(int64_t)i * ld + 2 * a.h * dk + hd * dv + d];
+  for (int e = threadIdx.x; e < T * dv; e += 256) {
+    const int i = e / dv, d = e - i * dv;
     dCs[i * dvp + d] = cb[(int64_t)i * ldc + hd * dv + d];
   }
-  for (int e = threadIdx.x; e < T * T; e += blockDim.x) As[e] = a.att[sbase + e];
+  for (int e = threadIdx.x; e < cw * dv; e += 256) {
+    const int jj = e / dv, d = e - jj * dv;
+    Vs[jj * dvp + d] = base[(int64_t)(j0 + jj) * ld + 2 * a.h * dk + hd * dv + d];
+  }
+  for (int e = threadIdx.x; e < T * kTatCW; e += 256) {
+    const int i = e / kTatCW, jj = e - i * kTatCW;
+    As[e] = jj < cw ? a.att[sbase + (int64_t)i * T + j0 + jj] : 0.f;
+  }
   __syncthreads();
   float* dbase = a.dqkv + (int64_t)bf * T * ld;
-  for (int e = threadIdx.x; e < T * dv; e += blockDim.x) {  // dV[j][d] = sum_i A[i][j] dctx[i][d]
-    int j = e / dv, d = e % dv;
-    float s = 0.f;
-    for (int i = 0; i < T; ++i) s = fmaf(As[i * T + j], dCs[i * dvp + d], s);
-    dbase[(int64_t)j * ld + 2 * a.h * dk + hd * dv + d] = s;
+  for (int e = threadIdx.x; e < T * kTatCW; e += 256) {  // dA[i][j] = sum_d dctx[i][d] V[j][d]
+    const int i = e / kTatCW, jj = e - i * kTatCW;
+    float acc = 0.f;
+    if (jj < cw)
+      for (int d = 0; d < dv; ++d) acc = fmaf(dCs[i * dvp + d], Vs[jj * dvp + d], acc);
+    dAs[e] = acc;
+  }
+  for (int e = threadIdx.x; e < cw * dv; e += 256) {  // dV[j][d] = sum_i A[i][j] dctx[i][d]
+    const int jj = e / dv, d = e - jj * dv;
+    float acc = 0.f;
+    for (int i = 0; i < T; ++i) acc = fmaf(As[i * kTatCW + jj], dCs[i * dvp + d], acc);
+    dbase[(int64_t)(j0 + jj) * ld + 2 * a.h * dk + hd * dv + d] = acc;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < T; j += blockDim.x) {
-    float c = 0.f;
-    for (int i = 0; i < T; ++i) {
-      float da = 0.f;
-      for (int d = 0; d < dv; ++d) da = fmaf(dCs[i * dvp + d], Vs[j * dvp + d], da);
-      c = fmaf(As[i * T + j], da, c);
+  // column softmax backward: dS = A (dA - sum_i A dA) + d re_At
+  const int jj = threadIdx.x & 15, g = threadIdx.x >> 4;
+  float c = 0.f;
+  for (int i = g; i < T; i += 16) c = fmaf(As[i * kTatCW + jj], dAs[i * kTatCW + jj], c);
+  c = col_reduce16(c, red, false);
+  for (int i = g; i < T; i += 16) {
+    float v = As[i * kTatCW + jj] * (dAs[i * kTatCW + jj] - c);
+    if (jj < cw) {
+      if (a.dre) v += a.dre[sbase + (int64_t)i * T + j0 + jj];
+      a.dscore[sbase + (int64_t)i * T + j0 + jj] = v;
     }
-    for (int i = 0; i < T; ++i) {
-      float da = 0.f;
-      for (int d = 0; d < dv; ++d) da = fmaf(dCs[i * dvp + d], Vs[j * dvp + d], da);
-      float v = As[i * T + j] * (da - c);
-      if (a.dre) v += a.dre[sbase + i * T + j];
-      As[i * T + j] = v;
-    }
+    dAs[i * kTatCW + jj] = v;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < T * T; e += blockDim.x) a.dscore[sbase + e] = As[e];
-  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
-    int i = e / dk, d = e % dk;
-    float sq = 0.f, sk = 0.f;
-    for (int j = 0; j < T; ++j) {
-      sq = fmaf(As[i * T + j], Ks[j * dkp + d], sq);
-      sk = fmaf(As[j * T + i], Qs[j * dkp + d], sk);
-    }
-    dbase[(int64_t)i * ld + hd * dk + d] = sq * a.scale;
-    dbase[(int64_t)i * ld + a.h * dk + hd * dk + d] = sk * a.scale;
+  for (int e = threadIdx.x; e < cw * dk; e += 256) {  // dK[j][d] = s sum_i dS[i][j] Q[i][d]
+    const int jj2 = e / dk, d = e - jj2 * dk;
+    float acc = 0.f;
+    for (int i = 0; i < T; ++i) acc = fmaf(dAs[i * kTatCW + jj2], Qs[i * dkp + d], acc);
+    dbase[(int64_t)(j0 + jj2) * ld + a.h * dk + hd * dk + d] = acc * a.scale;
   }
 }
 
@@ -1063,9 +1140,6 @@ static size_t tat_fwd_lds(int T, int dk, int dv) {
 static size_t tat_bwd_lds(int T, int dk, int dv) {
   return sizeof(float) * (size_t)(2 * T * (dk + 1) + 2 * T * (dv + 1) + 2 * T * T);
 }
-static size_t tat_bwd_lowmem_lds(int T, int dk, int dv) {
-  return sizeof(float) * (size_t)(2 * T * (dk + 1) + 2 * T * (dv + 1) + T * T);
-}
 
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st) {
@@ -1081,8 +1155,21 @@ int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
     return 0;
   }
   size_t lds = tat_fwd_lds(T, dk, dv);
-  if (lds > 160 * 1024) { set_last_error("tat_fwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
-  if (lds > 64 * 1024) DS_TRY(allow_lds((const void*)tat_fwd_kernel, lds));
+  if (lds > 64 * 1024) {  // long series: column chunks, then ctx = att . V as one batched GEMM
+    const size_t lc = sizeof(float) * (size_t)tat_cols_fwd_floats(T, dk);
+    if (lc > 160 * 1024) { set_last_error("tat_fwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
+    if (lc > 64 * 1024) DS_TRY(allow_lds((const void*)tat_fwd_cols_kernel, lc));
+    const int nch = (T + kTatCW - 1) / kTatCW;
+    hipLaunchKernelGGL(tat_fwd_cols_kernel, dim3((unsigned)(P * nch)), dim3(256), lc, st, a);
+    DS_CHECK_LAUNCH();
+    const int64_t ld = 2 * (int64_t)h * dk + (int64_t)h * dv, ldc = (int64_t)h * dv;
+    Gemm g;  // ctx[bf,i,hd,:] = sum_j att[bf,hd,i,j] V[bf,j,hd,:]
+    g.M = T; g.N = dv; g.K = T; g.batch = P;
+    g.A = att; g.am = idx1(T); g.ak = idx1(1); g.az = idx1((int64_t)T * T);
+    g.B = qkv; g.b_off = 2 * (int64_t)h * dk; g.bk = idx1(ld); g.bn = idx1(1); g.bz = idx2(h, dv, (int64_t)T * ld);
+    g.C = ctx; g.cm = idx1(ldc); g.cn = idx1(1); g.cz = idx2(h, dv, (int64_t)T * ldc);
+    return run_gemm(g, nullptr, 0, st);
+  }
   hipLaunchKernelGGL(tat_fwd_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
@@ -1102,15 +1189,22 @@ int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
     return 0;
   }
   size_t lds = tat_bwd_lds(T, dk, dv);
-  if (lds > 160 * 1024) {  // long series: A-only LDS variant
-    lds = tat_bwd_lowmem_lds(T, dk, dv);
-    if (lds > 160 * 1024) { set_last_error("tat_bwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
-    DS_TRY(allow_lds((const void*)tat_bwd_lowmem_kernel, lds));
-    hipLaunchKernelGGL(tat_bwd_lowmem_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
+  if (lds > 64 * 1024) {  // long series: column chunks, then dQ = s dS . K as one batched GEMM
+    const size_t lc = sizeof(float) * (size_t)tat_cols_bwd_floats(T, dk, dv);
+    if (lc > 160 * 1024) { set_last_error("tat_bwd: T too large for LDS"); return DSTAGNN_E_SHAPE; }
+    if (lc > 64 * 1024) DS_TRY(allow_lds((const void*)tat_bwd_cols_kernel, lc));
+    const int nch = (T + kTatCW - 1) / kTatCW;
+    hipLaunchKernelGGL(tat_bwd_cols_kernel, dim3((unsigned)(P * nch)), dim3(256), lc, st, a);
     DS_CHECK_LAUNCH();
-    return 0;
+    const int64_t ld = 2 * (int64_t)h * dk + (int64_t)h * dv;
+    Gemm g;  // dQ[bf,i,hd,:] = s sum_j dS[bf,hd,i,j] K[bf,j,hd,:]
+    g.M = T; g.N = dk; g.K = T; g.batch = P;
+    g.A = dscore; g.am = idx1(T); g.ak = idx1(1); g.az = idx1((int64_t)T * T);
+    g.B = qkv; g.b_off = (int64_t)h * dk; g.bk = idx1(ld); g.bn = idx1(1); g.bz = idx2(h, dk, (int64_t)T * ld);
+    g.C = dqkv; g.cm = idx1(ld); g.cn = idx1(1); g.cz = idx2(h, dk, (int64_t)T * ld);
+    g.alpha = a.scale;
+    return run_gemm(g, nullptr, 0, st);
   }
-  if (lds > 64 * 1024) DS_TRY(allow_lds((const void*)tat_bwd_kernel, lds));
   hipLaunchKernelGGL(tat_bwd_kernel, dim3((unsigned)(B * F * h)), dim3(256), lds, st, a);
   DS_CHECK_LAUNCH();
   return 0;
