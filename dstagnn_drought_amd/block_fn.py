@@ -75,11 +75,12 @@ def use_sparse(graph, meta, T):
     return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= (1 << 20)
 
 
-def use_flash(graph, meta, T, force=None):
+def use_flash(graph, meta, T, force=None, B=0):
     """Fused (flash-style) Chebyshev attention (cheb_flash.hip): the (B,K,N,N) scores, softmax
     and score gradient are never written; on the sparse path with d_k == 32 (the MFMA tile),
-    automatically from N >= 1024 (DSTAGNN_FLASH=0/1 overrides), or when forced."""
-    if not use_sparse(graph, meta, T) or meta["d_k"] != 32:
+    automatically from N >= 1024 (DSTAGNN_FLASH=0/1 overrides), or when forced; batches up to
+    128 per call (the mask-gradient kernel's lanes)."""
+    if not use_sparse(graph, meta, T) or meta["d_k"] != 32 or B > 128:
         return False
     if force is not None:
         return bool(force)
@@ -103,7 +104,7 @@ def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False
     ops = _lib.load()
     x = x.float().contiguous()
     sparse = use_sparse(graph, meta, x.shape[3])
-    fl = use_flash(graph, meta, x.shape[3], flash)
+    fl = use_flash(graph, meta, x.shape[3], flash, x.shape[0])
     return ops.block(x, res_arg(res_att, x.shape[2]), list(params), slots, graph_list(graph, sparse, fl),
                      cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed), flags_of(train, sparse, direct, fl))
 

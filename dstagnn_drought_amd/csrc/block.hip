@@ -194,8 +194,8 @@ int check_dims(const dstagnn_block_dims* d) {
     set_last_error("cheb_sparse requires 0 < C*T <= 2^20");
     return DSTAGNN_E_SHAPE;
   }
-  if (d->cheb_flash && (!d->cheb_sparse || d->d_k != 32 || d->cheb_nnz <= 0)) {
-    set_last_error("cheb_flash requires cheb_sparse, d_k == 32 and cheb_nnz > 0");
+  if (d->cheb_flash && (!d->cheb_sparse || d->d_k != 32 || d->cheb_nnz <= 0 || d->B > 128)) {
+    set_last_error("cheb_flash requires cheb_sparse, d_k == 32, cheb_nnz > 0 and B <= 128");
     return DSTAGNN_E_SHAPE;
   }
   if (d->F != 1 && d->F != d->C) {

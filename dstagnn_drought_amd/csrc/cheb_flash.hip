@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void flash_dk_kernel(ChebFl a) {
 }
 
 // backward: dM_k[i,j] = A_pa[i,j] sum_b dz_b[i,j] on the A_pa support.  One wave per (k, j),
-// lanes over the batch; P recomputed by a 32-long dot product per (b, i, j).
+// lanes over the batch (B <= 128); P recomputed by a 32-long dot product per (b, i, j).
 __global__ __launch_bounds__(256) void flash_mask_grad_kernel(ChebFl a) {
   const int lane = threadIdx.x & 63;
   const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -293,6 +293,23 @@ __global__ __launch_bounds__(256) void flash_mask_grad_kernel(ChebFl a) {
   const float* Mk = a.mask[k];
   float* dM = a.dmask[k];
   if (!dM) return;
+  // per lane: K'_j, lse_j and c_j of its batch elements b = lane + 64 bb (loaded once per column)
+  constexpr int kMaxBB = 2;
+  const int nb = min(kMaxBB, (a.B + 63) / 64);
+  float kv[kMaxBB][32], lse[kMaxBB], cj[kMaxBB];
+#pragma unroll
+  for (int bb = 0; bb < kMaxBB; ++bb) {
+    const int b = min(lane + 64 * bb, a.B - 1);
+    const int bk = b * a.K + k;
+    const float* kr = a.qk + (int64_t)b * a.N * a.ld + k * 32 + a.kd + (int64_t)j * a.ld;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float4 v = *reinterpret_cast<const float4*>(kr + 4 * u);
+      kv[bb][4 * u] = v.x; kv[bb][4 * u + 1] = v.y; kv[bb][4 * u + 2] = v.z; kv[bb][4 * u + 3] = v.w;
+    }
+    lse[bb] = a.lse[(int64_t)bk * a.N + j];
+    cj[bb] = a.cc[(int64_t)bk * a.N + j];
+  }
   for (int q = a.apa_ptr[j]; q < a.apa_ptr[j + 1]; ++q) {
     const int i = a.apa_row[q];
     const int64_t o = (int64_t)i * a.N + j;
@@ -301,20 +318,15 @@ __global__ __launch_bounds__(256) void flash_mask_grad_kernel(ChebFl a) {
     for (int p = a.csc_ptr[j]; p < a.csc_ptr[j + 1]; ++p)
       if (a.csc_row[p] == i) pt = p;
     float s = 0.f;
-    for (int b = lane; b < a.B; b += 64) {
+    for (int bb = 0; bb < nb; ++bb) {
+      const int b = lane + 64 * bb;
+      if (b >= a.B) break;
       const int bk = b * a.K + k;
       const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
-      float kv[32];
-      const float* kr = Q + a.kd + (int64_t)j * a.ld;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float4 v = *reinterpret_cast<const float4*>(kr + 4 * u);
-        kv[4 * u] = v.x; kv[4 * u + 1] = v.y; kv[4 * u + 2] = v.z; kv[4 * u + 3] = v.w;
-      }
-      const float z = dot32(Q + (int64_t)i * a.ld, kv) * a.scale + w * Mk[o];
-      const float P = __expf(z - a.lse[(int64_t)bk * a.N + j]);
+      const float z = dot32(Q + (int64_t)i * a.ld, kv[bb]) * a.scale + w * Mk[o];
+      const float P = __expf(z - lse[bb]);
       const float dzs = pt >= 0 ? a.dzs[(int64_t)bk * a.nnz + pt] : 0.f;
-      s += dzs - P * a.cc[(int64_t)bk * a.N + j];
+      s += dzs - P * cj[bb];
     }
     s = wave_sum(s);
     if (lane == 0) dM[o] = w * s;
@@ -324,11 +336,10 @@ __global__ __launch_bounds__(256) void flash_mask_grad_kernel(ChebFl a) {
 // dM_k = 0 off the A_pa support: every (N,N) mask gradient in one launch (hipMemsetAsync ran at
 // ~0.2 TB/s here, 0.4 ms per 67 MB mask at N = 4096)
 __global__ __launch_bounds__(256) void flash_zero_kernel(ChebFl a) {
-  const int64_t NN = (int64_t)a.N * a.N, tot = NN * a.K;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (int64_t)gridDim.x * 256) {
-    const int k = (int)(e / NN);
-    if (a.dmask[k]) a.dmask[k][e - (int64_t)k * NN] = 0.f;
-  }
+  float* d = a.dmask[blockIdx.y];
+  if (!d) return;
+  const int64_t NN = (int64_t)a.N * a.N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < NN; e += (int64_t)gridDim.x * 256) d[e] = 0.f;
 }
 
 unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
@@ -360,8 +371,9 @@ int op_flash_dqk(const ChebFl& a, hipStream_t st) {
 }
 
 int op_flash_mask_grad(const ChebFl& a, hipStream_t st) {
-  const int64_t tot = (int64_t)a.K * a.N * a.N;
-  hipLaunchKernelGGL(flash_zero_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(tot, 256), 8192)), dim3(256), 0, st, a);
+  const int64_t NN = (int64_t)a.N * a.N;
+  hipLaunchKernelGGL(flash_zero_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(NN, 256), 4096), (unsigned)a.K),
+                     dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   hipLaunchKernelGGL(flash_mask_grad_kernel, dim3(grid_waves((int64_t)a.K * a.N)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();

@@ -242,7 +242,7 @@ class DSTAGNN_block(nn.Module):
         meta["seed"] = _rank_seed(int(torch.randint(0, 2 ** 62, (1,)).item())) if drop else 0
         names, params, slots = self._param_list()
         graph = self._graph()
-        if use_flash(graph, meta, T, self.flash_cheb):
+        if use_flash(graph, meta, T, self.flash_cheb, B):
             graph = self._flash_graph(graph)
         out, re_at = block_call(x, res_att, params, slots, graph, meta, meta["train"], meta["seed"],
                                 self.direct_grads, flash=self.flash_cheb)

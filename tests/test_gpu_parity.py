@@ -317,7 +317,7 @@ def hip_cheb_relu_mask(blk, x, res):
     names, ps, slots = blk._param_list()
     graph = blk._graph()
     sparse = bf.use_sparse(graph, blk.meta, x.shape[3])
-    fl = bf.use_flash(graph, blk.meta, x.shape[3], blk.flash_cheb)
+    fl = bf.use_flash(graph, blk.meta, x.shape[3], blk.flash_cheb, x.shape[0])
     if fl:
         graph = blk._flash_graph(graph)
     X = _lib.load().block_cheb_out(x.detach().float().contiguous(), bf.res_arg(res, x.shape[2]), list(ps), slots,

@@ -8,9 +8,12 @@ Adam steps at lr 1e-3 every parameter tensor agrees to <= 1e-4 * max(1, |p|) (me
 ~1e-7 typical, 1.4e-6 worst) EXCEPT fcmy.0.bias: its gradient sums, over the C channels, the
 LayerNorm-over-C backward (model/DSTAGNN_my.py:252), which cancels exactly wherever the ReLUs
 pass (sum_c dLN/dx_c = 0); as training proceeds it becomes rounding-level and Adam's
-normalised step turns fp32 summation-order noise into O(lr) moves.  (Its gradient itself
-matches the oracle to 1e-6 relative — tools/dbg_train_grad.py, train mode, at init.)
-It is held to lr * steps / 4.
+normalised step turns fp32 summation-order noise into O(lr) moves, so in this trajectory it
+is held to lr * steps / 4.  Its GRADIENT is pinned tightly elsewhere: every parameter
+gradient of a 3-block make_model + SmoothL1 against the reference's own values
+(test_gpu_parity.py::test_model_golden, 1e-4 * scale), and train mode with both dropouts on
+against the oracle fed the exact masks the HIP path drew
+(test_gpu_parity.py::test_block_train_mode_dropout_vs_oracle).
 """
 import os
 
