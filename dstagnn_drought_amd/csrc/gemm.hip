@@ -8,8 +8,9 @@
 // Math: v_mfma_f32_32x32x2_f32 (exact fp32 FMA chain, 64 FLOP/clk/SIMD = the fp32
 // peak; gfx950 has no xf32).  A workgroup is 4 waves arranged WGM x WGN; each wave
 // owns WM x WN 32x32 accumulators, so the block tile is (32*WM*WGM) x (32*WN*WGN) x 16
-// (64x64, 128x64, 128x128, 128x32, 256x32 are instantiated; a cost model picks one).
-// Operands are staged global -> LDS by LDS-DMA (global_load_lds_dword) in a 2- or 3-stage
+// (64x64, 128x128, 128x32 are instantiated; a cost model picks one).
+// Operands are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4 where every quad is
+// contiguous and aligned, global_load_lds_dword otherwise) in a 2- or 3-stage
 // pipeline (see gemm_glds_body); out-of-range rows/columns are clamped to a valid address
 // (their products land only in unstored C entries), so full k-tiles issue with no
 // per-element predicate.  Long reductions are split over workgroups into fp32 partial
@@ -19,524 +20,12 @@
 
 #include "common.hpp"
 
+#include "gemm_kern.hpp"
+
+using namespace dsgemm;
+
 namespace {
 
-constexpr int BKMAX = 32;  // k-tile depth (16 or 32, template parameter)
-
-#ifdef DSTAGNN_ABLATE_STAMP
-// timeline probe build: thread 0 of each of the first 4096 workgroups records s_memtime
-__device__ unsigned long long g_stamps[4096 * 16];
-#define DS_STAMP(i)                                                              \
-  do {                                                                           \
-    if (threadIdx.x == 0 && blockIdx.x < 4096 && (i) < 16)                       \
-      g_stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();            \
-  } while (0)
-#else
-#define DS_STAMP(i) do {} while (0)
-#endif
-
-struct GemmK {
-  int M, N, K, batch, splitk, kchunk;
-  int32_t abias, bbias;  // added to every A / B element offset (see run_gemm)
-  uint32_t tiles_m, tiles_n, n_fast;
-  // every map is branch-free (single-level ones encoded with d = 2^31): no control flow
-  // between the kernel-argument loads, so they all issue in one round at entry
-  const float* A; KIdx am, ak; ZIdx az;
-  const float* B; KIdx bn, bk; ZIdx bz;
-  float* C; KIdx cm, cn; ZIdx cz;
-  float alpha, beta;
-  const float* bias; int32_t bias_stride;
-  int relu;
-  float* ws;  // split partials [batch][splitk][M][N]
-  const float* emask;  // optional: zero where emask <= 0 (same maps as C, offset c_off)
-  float* Cout;         // optional: destination instead of C (beta still reads C)
-};
-
-
-__device__ __forceinline__ void epilogue_store(const GemmK& g, int zb, int m, int n, float v) {
-  const int64_t zo = zoff(g.cz, zb);
-  const int32_t o = koff(g.cm, m) + koff(g.cn, n);
-  v *= g.alpha;
-  if (g.beta != 0.f) v += g.beta * g.C[zo + o];
-  if (g.bias) v += g.bias[n * g.bias_stride];
-  if (g.relu) v = fmaxf(v, 0.f);
-  if (g.emask) v = g.emask[zo + o] > 0.f ? v : 0.f;
-  (g.Cout ? g.Cout : g.C)[zo + o] = v;
-}
-
-struct TileCoord {
-  int m0, n0, zb, sp;
-};
-// XCD-aware tile order (1-D grid): the dispatcher deals consecutive workgroup ids
-// round-robin over the 8 XCDs, so id%8 labels the blocks sharing one L2.  Give each
-// such group a contiguous run of tiles, the small operand's index fastest, so the
-// blocks that re-read one panel of the big operand sit behind the same L2.
-// Bijective for any count.
-template <int BM, int BN>
-__device__ __forceinline__ TileCoord decode_tile(const GemmK& g) {
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
-  const uint32_t q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const uint32_t t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const uint32_t gn = g.tiles_n, gm = g.tiles_m;
-  const uint32_t tf = g.n_fast ? gn : gm, ts = g.n_fast ? gm : gn;
-  const uint32_t f = t % tf, tr = t / tf, sl = tr % ts;
-  TileCoord c;
-  c.n0 = (int)(g.n_fast ? f : sl) * BN;
-  c.m0 = (int)(g.n_fast ? sl : f) * BM;
-  const int zz = (int)(tr / ts);
-  c.zb = zz / g.splitk;
-  c.sp = zz % g.splitk;
-  return c;
-}
-
-// --- epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-template <int WM, int WN>
-__device__ __forceinline__ void gemm_epilogue(const GemmK& g, const TileCoord& c, int wrow0, int wcol0, int lane,
-                                              floatx16 (&acc)[WM][WN]) {
-  const int lr = lane & 31, lk = lane >> 5;
-  const bool reads = g.splitk == 1 && (g.beta != 0.f || g.emask);
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int n = c.n0 + wcol0 + j * 32 + lr;
-      if (n >= g.N) continue;
-      if (reads) {
-        // beta * C and the ReLU mask: all 16 loads issued before the first store (the
-        // stores may alias C, so element-wise load/store pairs would serialise 16 memory
-        // round trips per lane)
-        const int64_t zo = zoff(g.cz, c.zb);
-        const int32_t no = koff(g.cn, n);
-        float cin[16], em[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = min(c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk, g.M - 1);
-          const int64_t o = zo + koff(g.cm, m) + no;
-          cin[r] = g.beta != 0.f ? g.C[o] : 0.f;
-          em[r] = g.emask ? g.emask[o] : 1.f;
-        }
-        float* dst = g.Cout ? g.Cout : g.C;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          if (m >= g.M) continue;
-          float v = acc[i][j][r] * g.alpha + g.beta * cin[r];
-          if (g.bias) v += g.bias[n * g.bias_stride];
-          if (g.relu) v = fmaxf(v, 0.f);
-          if (em[r] <= 0.f) v = 0.f;
-          dst[zo + koff(g.cm, m) + no] = v;
-        }
-        continue;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (m >= g.M) continue;
-        if (g.splitk > 1) {
-          g.ws[(((int64_t)c.zb * g.splitk + c.sp) * g.M + m) * g.N + n] = acc[i][j][r];
-        } else {
-          epilogue_store(g, c.zb, m, n, acc[i][j][r]);
-        }
-      }
-    }
-}
-
-// A_KC: A is contiguous along k (16 lanes read one row's k-tile).  Otherwise lanes run
-// along m.  B_NC: B contiguous along n (lanes along n), otherwise lanes along k.
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, int BK, bool KTWO>
-__device__ __forceinline__ void gemm_f32_body(const GemmK& gin) {
-  constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
-  constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // elements per thread per k-tile
-  // LDS tiles are k-contiguous rows padded to BK+4 floats: a lane reads 4 consecutive k
-  // of its fragment row with one ds_read_b128 (row stride 36 dwords: the 16-lane groups
-  // of a b128 read hit 16 distinct 4-bank slots, conflict-free).
-  constexpr int LDK = BK + 4;
-  __shared__ __attribute__((aligned(16))) float As[2][BM][LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDK];
-
-  DS_STAMP(0);
-  const GemmK g = load_args(gin);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid / WGN, wc = wid % WGN;
-  const TileCoord tc = decode_tile<BM, BN>(g);
-  const int m0 = tc.m0, n0 = tc.n0, zb = tc.zb, sp = tc.sp;
-  DS_STAMP(11);
-  const int kbeg = sp * g.kchunk;
-  const int kend = min(g.K, kbeg + g.kchunk);
-
-  const float* A = g.A + zoff(g.az, zb);
-  const float* Bp = g.B + zoff(g.bz, zb);
-
-  // --- per-thread element coordinates inside a tile (fixed over the k loop)
-  int a_ml[LA], a_kl[LA], b_kl[LB], b_nl[LB];
-#pragma unroll
-  for (int j = 0; j < LA; ++j) {
-    int e = tid + 256 * j;
-    if (A_KC) { a_kl[j] = e % BK; a_ml[j] = e / BK; }
-    else      { a_ml[j] = e % BM; a_kl[j] = e / BM; }
-  }
-#pragma unroll
-  for (int j = 0; j < LB; ++j) {
-    int e = tid + 256 * j;
-    if (B_NC) { b_nl[j] = e % BN; b_kl[j] = e / BN; }
-    else      { b_kl[j] = e % BK; b_nl[j] = e / BK; }
-  }
-  // per-element row / column offsets as int32 from the (wave-uniform) operand bases:
-  // the host guarantees every offset fits (check_span), halving the pointer registers
-  // Per-element offsets are unsigned 32-bit element offsets from the wave-uniform operand
-  // bases (host-checked span < 2^30), so loads use the SGPR-base + 32-bit VGPR-offset form.
-  // Single-level k maps (KTWO = false): the k term is folded into a per-thread constant
-  // plus a wave-uniform k0*stride, i.e. ONE add per element per k-tile.  Two-level k
-  // maps (KTWO = true, the implicit-im2col convolutions) divide per element.
-  uint32_t ao[LA], bo[LB];
-#pragma unroll
-  for (int j = 0; j < LA; ++j) {
-    const int m = m0 + a_ml[j];
-    ao[j] = (uint32_t)g.abias + (m < g.M ? (uint32_t)koff(g.am, m) : 0u);  // clamped: row 0 is valid
-    if (!KTWO) ao[j] += (uint32_t)(a_kl[j] * g.ak.s0);
-  }
-#pragma unroll
-  for (int j = 0; j < LB; ++j) {
-    const int n = n0 + b_nl[j];
-    bo[j] = (uint32_t)g.bbias + (n < g.N ? (uint32_t)koff(g.bn, n) : 0u);
-    if (!KTWO) bo[j] += (uint32_t)(b_kl[j] * g.bk.s0);
-  }
-  DS_STAMP(12);
-  auto ld = [](const float* base, uint32_t off) -> float {
-    return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (size_t)(off << 2));
-  };
-  auto aoff = [&](int j, int k0) -> uint32_t {
-    return KTWO ? ao[j] + (uint32_t)koff(g.ak, k0 + a_kl[j]) : ao[j] + (uint32_t)(k0 * g.ak.s0);
-  };
-  auto boff = [&](int j, int k0) -> uint32_t {
-    return KTWO ? bo[j] + (uint32_t)koff(g.bk, k0 + b_kl[j]) : bo[j] + (uint32_t)(k0 * g.bk.s0);
-  };
-
-  float ra[LA], rb[LB];
-  // Rows m >= M / columns n >= N read row/column 0 (valid memory): they only feed C
-  // rows/columns the epilogue never stores, so they need no masking.  k >= kend must
-  // read as 0; that happens only in the last k-tile, handled by a uniform branch so the
-  // full tiles issue all their loads back to back with no per-element predicate (a
-  // predicated load is sunk into an exec-masked region and waited on alone).
-  auto load_tile = [&](int k0) {
-    if (k0 + BK <= kend) {
-#pragma unroll
-      for (int j = 0; j < LA; ++j) ra[j] = ld(A, aoff(j, k0));
-#pragma unroll
-      for (int j = 0; j < LB; ++j) rb[j] = ld(Bp, boff(j, k0));
-    } else {
-#pragma unroll
-      for (int j = 0; j < LA; ++j) ra[j] = (k0 + a_kl[j] < kend) ? ld(A, aoff(j, k0)) : 0.f;
-#pragma unroll
-      for (int j = 0; j < LB; ++j) rb[j] = (k0 + b_kl[j] < kend) ? ld(Bp, boff(j, k0)) : 0.f;
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < LA; ++j) As[buf][a_ml[j]][a_kl[j]] = ra[j];
-#pragma unroll
-    for (int j = 0; j < LB; ++j) Bs[buf][b_nl[j]][b_kl[j]] = rb[j];
-  };
-
-  floatx16 acc[WM][WN];
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  DS_STAMP(1);
-  if (ntiles > 0) {
-    load_tile(kbeg);
-    store_tile(0);
-    __syncthreads();
-  }
-  DS_STAMP(2);
-  // The MFMA's k order inside a tile is free as long as A and B agree: lane half h
-  // (lane >> 5) supplies k = h*BK/2 + s at step s, so each lane's k run is contiguous.
-  const int lr = lane & 31, lk = lane >> 5;
-  const int kh = lk * (BK / 2);
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-#ifndef DSTAGNN_ABLATE_LOADS
-    if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BK);
-#endif
-#pragma unroll
-    for (int q = 0; q < BK / 8; ++q) {
-      float4 a4[WM], b4[WN];
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-        a4[i] = *reinterpret_cast<const float4*>(&As[cur][wr * 32 * WM + i * 32 + lr][kh + 4 * q]);
-#pragma unroll
-      for (int j = 0; j < WN; ++j)
-        b4[j] = *reinterpret_cast<const float4*>(&Bs[cur][wc * 32 * WN + j * 32 + lr][kh + 4 * q]);
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int i = 0; i < WM; ++i)
-#pragma unroll
-          for (int j = 0; j < WN; ++j) {
-            const float av = s4 == 0 ? a4[i].x : s4 == 1 ? a4[i].y : s4 == 2 ? a4[i].z : a4[i].w;
-            const float bv = s4 == 0 ? b4[j].x : s4 == 1 ? b4[j].y : s4 == 2 ? b4[j].z : b4[j].w;
-#ifdef DSTAGNN_ABLATE_MFMA
-            acc[i][j][0] += av * bv;
-#else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-#endif
-          }
-    }
-    if (t + 1 < ntiles) store_tile(cur ^ 1);
-#ifndef DSTAGNN_ABLATE_SYNC
-    __syncthreads();
-#endif
-    if (t < 8) DS_STAMP(3 + t);
-  }
-
-  gemm_epilogue<WM, WN>(g, tc, wr * 32 * WM, wc * 32 * WN, lane, acc);
-#ifdef DSTAGNN_ABLATE_STAMP
-  __syncthreads();
-  DS_STAMP(15);
-#endif
-}
-
-// ---------------------------------------------------------------------------------
-// LDS-DMA pipeline (global_load_lds_dword): the operands go global -> LDS with no VGPR
-// staging and no ds_write pass, three LDS stages deep, so tile t+2 is in flight while
-// tile t is multiplied.  The DMA image is lane-linear per wave instruction (64 dwords),
-// so the layouts are chosen per operand orientation:
-//   m-contiguous operand (A not A_KC, B B_NC): image [BK][BM] (k rows of BM floats); a
-//     wave instruction reads 64 consecutive m at one k (coalesced); fragments are
-//     ds_read_b32 at (k, m = lane&31), conflict-free.
-//   k-contiguous operand: image [BM][BK] with the 4-float quads of row m XOR-swizzled by
-//     (m>>1)&7; the swizzle is applied on the SOURCE address (lane l of an instruction
-//     fetches the k that belongs in slot l), fragments are ds_read_b128, conflict-free.
-// Ordering: tile t's DMAs are retired by a counted vmcnt (tile t+1 stays in flight), then a
-// raw s_barrier makes them visible to every wave and proves every wave has finished
-// reading the stage that tile t+2 will overwrite.  No __syncthreads in the loop: its
-// fence would drain the in-flight DMAs (vmcnt(0)).
-// ---------------------------------------------------------------------------------
-__device__ float g_zero_page[64];  // k >= K lanes of the last tile fetch zeros from here
-
-// The DMA is issued from inline asm, not __builtin_amdgcn_global_load_lds: with the
-// builtin, hipcc's waitcnt pass cannot tell the fragment ds_reads of stage t from the DMA
-// in flight into stage t+2 and drains it (vmcnt(0)) before every read.  The asm saves and
-// restores M0 (compiler-owned); all ordering is by the explicit waits + barrier below.
-// four DMAs into consecutive 1 KiB LDS slots under one M0: the instruction offset moves
-// both the LDS destination and the global source (probed: tools/glds_probe.hip), so the
-// VGPR offsets carry -1024*i and the SGPR base is pre-lowered by 4 KiB to keep them >= 0.
-__device__ __forceinline__ void glds4_saddr(const float* base_m4k, uint32_t o0, uint32_t o1, uint32_t o2,
-                                            uint32_t o3, uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
-      "global_load_lds_dword %1, %5\n\t"
-      "global_load_lds_dword %2, %5 offset:1024\n\t"
-      "global_load_lds_dword %3, %5 offset:2048\n\t"
-      "global_load_lds_dword %4, %5 offset:3072\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"((o0 << 2) + 4096u), "v"((o1 << 2) + 3072u), "v"((o2 << 2) + 2048u), "v"((o3 << 2) + 1024u),
-        "s"(base_m4k), "s"(lds_addr)
-      : "memory");
-}
-__device__ __forceinline__ void glds_vaddr(const void* p, uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(p), "s"(lds_addr)
-      : "memory");
-}
-__device__ __forceinline__ uint32_t lds_addr_of(const float* p) {
-  return (uint32_t)reinterpret_cast<uintptr_t>(p);  // low 32 bits of a shared-aperture address
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm_barrier() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] | vmcnt[5:4] << 14
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (0 << 8) | ((N >> 4) << 14));
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int NSTAGE>
-__device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
-  constexpr int BK = 32;
-  constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
-  constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // DMA instructions per thread per tile
-  // pipeline depth: NS-1 tiles in flight; the counted wait holds (NS-2) tiles' DMAs, which
-  // must fit the 6-bit vmcnt (63)
-  constexpr int NS = NSTAGE;
-  static_assert(NS == 2 || NS == 3 || (NS == 4 && 2 * (LA + LB) <= 63), "pipeline depth");
-  __shared__ __attribute__((aligned(16))) float As[NS][BM * BK];
-  __shared__ __attribute__((aligned(16))) float Bs[NS][BN * BK];
-
-  DS_STAMP(0);
-  const GemmK g = load_args(gin);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid / WGN, wc = wid % WGN;
-  const TileCoord tc = decode_tile<BM, BN>(g);
-  DS_STAMP(11);
-  const int kbeg = tc.sp * g.kchunk;
-  const int kend = min(g.K, kbeg + g.kchunk);
-  const float* A = g.A + zoff(g.az, tc.zb);
-  const float* Bp = g.B + zoff(g.bz, tc.zb);
-
-  // element e = 256 j + tid of a tile image -> (row, k); lane l of the wave instruction j
-  // writes image slot 256 j + 64 wid + l
-  int a_ml[LA], a_kl[LA], b_nl[LB], b_kl[LB];
-  uint32_t ao[LA], bo[LB];
-#pragma unroll
-  for (int j = 0; j < LA; ++j) {
-    const int e = tid + 256 * j;
-    if (A_KC) {
-      const int m = e / BK, sl = e % BK;
-      a_ml[j] = m;
-      a_kl[j] = ((((sl >> 2) ^ ((m >> 1) & 7)) << 2) | (sl & 3));
-    } else {
-      a_kl[j] = e / BM;
-      a_ml[j] = e % BM;
-    }
-    const int m = tc.m0 + a_ml[j];
-    ao[j] = (uint32_t)g.abias + (m < g.M ? (uint32_t)koff(g.am, m) : 0u);  // clamped rows are never stored
-    if (!KTWO) ao[j] += (uint32_t)(a_kl[j] * g.ak.s0);
-  }
-#pragma unroll
-  for (int j = 0; j < LB; ++j) {
-    const int e = tid + 256 * j;
-    if (B_NC) {
-      b_kl[j] = e / BN;
-      b_nl[j] = e % BN;
-    } else {
-      const int n = e / BK, sl = e % BK;
-      b_nl[j] = n;
-      b_kl[j] = ((((sl >> 2) ^ ((n >> 1) & 7)) << 2) | (sl & 3));
-    }
-    const int n = tc.n0 + b_nl[j];
-    bo[j] = (uint32_t)g.bbias + (n < g.N ? (uint32_t)koff(g.bn, n) : 0u);
-    if (!KTWO) bo[j] += (uint32_t)(b_kl[j] * g.bk.s0);
-  }
-  DS_STAMP(12);
-  auto aoff = [&](int j, int k0) -> uint32_t {
-    return KTWO ? ao[j] + (uint32_t)koff(g.ak, k0 + a_kl[j]) : ao[j] + (uint32_t)(k0 * g.ak.s0);
-  };
-  auto boff = [&](int j, int k0) -> uint32_t {
-    return KTWO ? bo[j] + (uint32_t)koff(g.bk, k0 + b_kl[j]) : bo[j] + (uint32_t)(k0 * g.bk.s0);
-  };
-  auto gp = [](const float* base, uint32_t off) -> const void* {
-    return reinterpret_cast<const char*>(base) + (size_t)(off << 2);
-  };
-  auto issue = [&](int k0, int st) {
-    const uint32_t da = lds_addr_of(&As[st][64 * wid]);
-    const uint32_t db = lds_addr_of(&Bs[st][64 * wid]);
-    if (k0 + BK <= kend) {
-      static_assert(LA % 4 == 0 && LB % 4 == 0, "DMA batches of 4");
-#pragma unroll
-      for (int j = 0; j < LA; j += 4)
-        glds4_saddr(A - 1024, aoff(j, k0), aoff(j + 1, k0), aoff(j + 2, k0), aoff(j + 3, k0), da + 1024 * j);
-#pragma unroll
-      for (int j = 0; j < LB; j += 4)
-        glds4_saddr(Bp - 1024, boff(j, k0), boff(j + 1, k0), boff(j + 2, k0), boff(j + 3, k0), db + 1024 * j);
-    } else {
-#pragma unroll
-      for (int j = 0; j < LA; ++j)
-        glds_vaddr(k0 + a_kl[j] < kend ? gp(A, aoff(j, k0)) : (const void*)g_zero_page, da + 1024 * j);
-#pragma unroll
-      for (int j = 0; j < LB; ++j)
-        glds_vaddr(k0 + b_kl[j] < kend ? gp(Bp, boff(j, k0)) : (const void*)g_zero_page, db + 1024 * j);
-    }
-  };
-
-  floatx16 acc[WM][WN];
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-#pragma unroll
-  for (int s0 = 0; s0 < NS - 1; ++s0)
-    if (s0 < ntiles) issue(kbeg + s0 * BK, s0);
-  DS_STAMP(1);
-  // lane half h (lane >> 5) supplies k = 16 h + s at MFMA step s (A and B agree)
-  const int lr = lane & 31, lk = lane >> 5;
-  const int arow0 = wr * 32 * WM, bcol0 = wc * 32 * WN;
-  int st = 0;
-  for (int t = 0; t < ntiles; ++t) {
-    {  // retire tile t; the tiles issued after it stay in flight
-      const int ahead = min(ntiles - 1 - t, NS - 2);
-      if (NS == 4 && ahead >= 2) wait_vm_barrier<(NS == 4 ? 2 : 0) * (LA + LB)>();
-      else if (ahead >= 1) wait_vm_barrier<LA + LB>();
-      else wait_vm_barrier<0>();
-    }
-    if (t == 0) DS_STAMP(2);
-    if (t + NS - 1 < ntiles) issue(kbeg + (t + NS - 1) * BK, st == 0 ? NS - 1 : st - 1);
-    const float* as = As[st];
-    const float* bs = Bs[st];
-#pragma unroll
-    for (int q = 0; q < BK / 8; ++q) {
-      float av[WM][4], bv[WN][4];
-#pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const int m = arow0 + i * 32 + lr;
-        if (A_KC) {
-          const int pq = (lk * 4 + q) ^ ((m >> 1) & 7);
-          const float4 v = *reinterpret_cast<const float4*>(as + m * BK + pq * 4);
-          av[i][0] = v.x; av[i][1] = v.y; av[i][2] = v.z; av[i][3] = v.w;
-        } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) av[i][c] = as[(lk * 16 + q * 4 + c) * BM + m];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int n = bcol0 + j * 32 + lr;
-        if (!B_NC) {
-          const int pq = (lk * 4 + q) ^ ((n >> 1) & 7);
-          const float4 v = *reinterpret_cast<const float4*>(bs + n * BK + pq * 4);
-          bv[j][0] = v.x; bv[j][1] = v.y; bv[j][2] = v.z; bv[j][3] = v.w;
-        } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) bv[j][c] = bs[(lk * 16 + q * 4 + c) * BN + n];
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int i = 0; i < WM; ++i)
-#pragma unroll
-          for (int j = 0; j < WN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][c], bv[j][c], acc[i][j], 0, 0, 0);
-    }
-    if (t < 8) DS_STAMP(3 + t);
-    st = st == NS - 1 ? 0 : st + 1;
-  }
-  gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
-#ifdef DSTAGNN_ABLATE_STAMP
-  __syncthreads();
-  DS_STAMP(15);
-#endif
-}
-
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool GLDS, bool KTWO, int NS>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmK g) {
-  static_assert(GLDS, "the LDS-DMA pipeline is the only GEMM body");
-  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, NS>(g);
-}
-// identical body under its own symbol: the call site the benchmark reports as the
-// dominant kernel (rocprofv3 then lists exactly that call site's launches)
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool GLDS, bool KTWO, int NS>
-__global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmK g) {
-  static_assert(GLDS, "the LDS-DMA pipeline is the only GEMM body");
-  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, NS>(g);
-}
 
 // out[zb][m][n] = epilogue( sum_s ws[zb][s][m][n] ).  A workgroup takes 256/G outputs and
 // G split groups per output (G = power of two ~ splitk/8), combined by an LDS tree.
@@ -573,23 +62,20 @@ struct Cfg {
   int bm() const { return 32 * wm * wgm; }
   int bn() const { return 32 * wn * wgn; }
 };
-constexpr Cfg kCfgs[] = {{2, 2, 1, 1}, {2, 2, 2, 1}, {2, 2, 2, 2}, {4, 1, 1, 1}, {4, 1, 2, 1}};
+constexpr Cfg kCfgs[] = {{2, 2, 1, 1}, {2, 2, 2, 2}, {4, 1, 1, 1}};  // 64x64, 128x128, 128x32
 
-template <int WGM, int WGN, int WM, int WN, bool KTWO, bool GLDS, int NS>
-void launch_cfg(const GemmK& k, bool akc, bool bnc, bool hot, hipStream_t st) {
-  constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
-  GemmK kk = k;
-  kk.tiles_m = (uint32_t)cdiv64(k.M, BM);
-  kk.tiles_n = (uint32_t)cdiv64(k.N, BN);
-  kk.n_fast = (int64_t)k.M >= (int64_t)k.N ? 1u : 0u;  // A (M x K) is the bigger operand
-  const dim3 grid((unsigned)((int64_t)kk.tiles_m * kk.tiles_n * k.batch * k.splitk));
-#define DS_GEMM_LAUNCH(KER)                                                                                  \
-  if (akc && bnc) hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, true, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);   \
-  else if (akc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, true, false, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);  \
-  else if (bnc)   hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, true, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);  \
-  else            hipLaunchKernelGGL((KER<WGM, WGN, WM, WN, false, false, GLDS, KTWO, NS>), grid, dim3(256), 0, st, kk);
-  if (hot) { DS_GEMM_LAUNCH(gemm_f32_hot_kernel) } else { DS_GEMM_LAUNCH(gemm_f32_kernel) }
-#undef DS_GEMM_LAUNCH
+
+// 16-B DMA eligibility of one operand (see gemm_glds_body): every quad of elements one lane
+// moves must be 4 consecutive floats at a 16-B aligned address.  kmaj: the image is
+// [rows][BK] (quads along k, which needs a unit-stride single-level k map); otherwise
+// [BK][rows] (quads along rows: a unit-stride row map whose quads never straddle a level
+// and a row count that is a multiple of 4).  All remaining offsets must be multiples of 4.
+bool quad_ok(const Idx2& x) { return x.s0 % 4 == 0 && (!x.two || x.s1 % 4 == 0); }
+bool rows_quad(const Idx2& x) { return x.s0 == 1 && (!x.two || (x.f.d % 4 == 0 && x.s1 % 4 == 0)); }
+int dma_width(const float* base, const Idx2& rowmap, int rows, const Idx2& kmap, const Idx2& zmap, bool kmaj) {
+  if ((reinterpret_cast<uintptr_t>(base) & 15) != 0 || !quad_ok(zmap)) return 1;
+  if (kmaj) return (!kmap.two && kmap.s0 == 1 && quad_ok(rowmap)) ? 4 : 1;
+  return (rows_quad(rowmap) && rows % 4 == 0 && quad_ok(kmap)) ? 4 : 1;
 }
 
 // ---------------------------------------------------------------------------------
@@ -712,8 +198,8 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   int best = 0;
   {
     const int64_t b64 = cdiv64(g.M, 64) * cdiv64(g.N, 64) * g.batch;
-    if (g.N <= 32) best = 3;
-    else if (b64 >= 4096 && g.K >= 1024) best = 2;
+    if (g.N <= 32) best = 2;
+    else if (b64 >= 4096 && g.K >= 1024) best = 1;
     else best = 0;
   }
   if (env_cfg >= 0 && env_cfg < (int)(sizeof(kCfgs) / sizeof(kCfgs[0]))) best = env_cfg;
@@ -741,6 +227,9 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   const bool akc = !g.ak.two && g.ak.s0 == 1;
   const bool bnc = !g.bn.two && g.bn.s0 == 1;
   const bool hot = g.hot != 0;
+  static const int env_v = getenv("DSTAGNN_GEMM_DMA16") ? atoi(getenv("DSTAGNN_GEMM_DMA16")) : 1;
+  const int va = env_v ? dma_width(g.A + g.a_off, g.am, g.M, g.ak, g.az, akc) : 1;
+  const int vb = env_v ? dma_width(g.B + g.b_off, g.bn, g.N, g.bk, g.bz, !bnc) : 1;
   // LDS pipeline depth: 3 stages keep two k-tiles in flight per workgroup (needed when a CU
   // holds about one workgroup: long split-K reductions); 2 stages cut the workgroup's LDS by a
   // third, so more workgroups are resident per CU and latency is hidden across workgroups
@@ -748,25 +237,15 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   int ns = blocks * splitk > 256 ? 2 : 3;
   static const int env_ns = getenv("DSTAGNN_GEMM_NS") ? atoi(getenv("DSTAGNN_GEMM_NS")) : 0;
   if (env_ns == 2 || env_ns == 3) ns = env_ns;
-#define DS_CFG_SWITCH(KT, NS)                                                \
-  switch (best) {                                                            \
-    case 0: launch_cfg<2, 2, 1, 1, KT, true, NS>(k, akc, bnc, hot, st); break;   \
-    case 1: launch_cfg<2, 2, 2, 1, KT, true, NS>(k, akc, bnc, hot, st); break;   \
-    case 2: launch_cfg<2, 2, 2, 2, KT, true, NS>(k, akc, bnc, hot, st); break;   \
-    case 3: launch_cfg<4, 1, 1, 1, KT, true, NS>(k, akc, bnc, hot, st); break;   \
-    default: launch_cfg<4, 1, 2, 1, KT, true, NS>(k, akc, bnc, hot, st); break;  \
-  }
+  k.nstage = ns;
   const bool ktwo = g.ak.two || g.bk.two;
   static const bool glog = getenv("DSTAGNN_GEMM_LOG") != nullptr;
   if (glog)
-    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d\n", g.M,
-            g.N, g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk, ns);
-  if (ns == 2) {
-    if (ktwo) { DS_CFG_SWITCH(true, 2) } else { DS_CFG_SWITCH(false, 2) }
-  } else {
-    if (ktwo) { DS_CFG_SWITCH(true, 3) } else { DS_CFG_SWITCH(false, 3) }
-  }
-#undef DS_CFG_SWITCH
+    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d\n",
+            g.M, g.N, g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk, ns, va, vb);
+  using Unit = void (*)(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+  static const Unit units[3][2] = {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}};
+  units[best][ktwo ? 1 : 0](k, akc, bnc, va, vb, hot, st);
   DS_CHECK_LAUNCH();
   if (splitk > 1) {
     int64_t total = (int64_t)g.batch * g.M * g.N;
@@ -779,9 +258,3 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   return 0;
 }
 
-#ifdef DSTAGNN_ABLATE_STAMP
-extern "C" int dstagnn_debug_stamps(unsigned long long* host, int n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (size_t)n, 0,
-                                  hipMemcpyDeviceToHost);
-}
-#endif

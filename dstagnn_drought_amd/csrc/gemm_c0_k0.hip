@@ -1,0 +1,6 @@
+// GEMM instantiation unit: 64x64 tile, single-level k maps (see gemm_kern.hpp)
+#include "gemm_kern.hpp"
+
+namespace dsgemm {
+DS_GEMM_UNIT(gemm_c0_k0, 2, 2, 1, 1, false)
+}  // namespace dsgemm
