@@ -370,6 +370,27 @@ def main():
            "frac": round(hot_achieved / PEAK_FP32_TFLOPS, 4)}
 
     log(f"hot kernel {hot_ms * 1e3:.2f} us/launch")
+    # opt-in bf16-operand GEMM variant (dstagnn::set_gemm_bf16): the same step, timed the same
+    # way, reported beside the fp32 headline (never as `value`)
+    bf16 = None
+    if world == 1 and not args.no_extras:
+        prev = ops.set_gemm_bf16(1)
+        try:
+            for _ in range(args.warmup):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            t_bf = (time.perf_counter() - t0) / args.steps
+        finally:
+            ops.set_gemm_bf16(prev)
+        bf16 = {"ms_per_step": round(t_bf * 1e3, 4), "value": round(B / t_bf, 2), "unit": "samples/s",
+                "dtype": "bf16 GEMM operands, fp32 accumulate / softmax / LayerNorm / reductions",
+                "tolerance": "normwise ||err||/||ref|| <= 3e-2 per tensor vs the fp64 oracle "
+                             "(tests/test_gpu_parity.py::test_bf16_gemm_variant)"}
+        log(f"bf16 GEMM variant: {t_bf * 1e3:.3f} ms/step")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(f"cpu baseline on {host_cores()} threads")
@@ -412,6 +433,8 @@ def main():
             "hbm_roofline": hbm_roof,
             "cpu_baseline": cpu,
         }
+        if bf16 is not None:
+            line["variant_bf16_gemm"] = bf16
         if ext is not None:
             line["extras"] = ext
         print(json.dumps(line), flush=True)

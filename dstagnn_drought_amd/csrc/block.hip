@@ -1076,6 +1076,7 @@ extern "C" {
 const char* dstagnn_last_error(void) { return g_last_error.c_str(); }
 int dstagnn_prof_start(int capacity) { return gemm_prof_start(capacity); }
 int dstagnn_set_splitk_target(int target) { return gemm_set_splitk_target(target); }
+int dstagnn_set_gemm_bf16(int on) { return gemm_set_bf16(on); }
 int dstagnn_prof_stop(dstagnn_prof_stats* stats) { return gemm_prof_stop(stats); }
 int dstagnn_version(void) { return 1; }
 

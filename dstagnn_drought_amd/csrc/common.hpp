@@ -9,6 +9,7 @@
 #include "../../include/dstagnn.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------
@@ -235,3 +236,4 @@ bool gemm_prof_on();
 int gemm_prof_start(int capacity);
 int gemm_prof_stop(dstagnn_prof_stats* out);
 int gemm_set_splitk_target(int target);
+int gemm_set_bf16(int on);

@@ -98,6 +98,10 @@ Prof g_prof;
 // range to about this many (1 = never split: every reduction in one fixed order, so a
 // per-sample result is bit-identical at any batch size); DSTAGNN_SPLITK_TARGET overrides
 int g_splitk_target = getenv("DSTAGNN_SPLITK_TARGET") ? atoi(getenv("DSTAGNN_SPLITK_TARGET")) : 512;
+// operand precision of every GEMM: 0 = fp32 (v_mfma_f32_32x32x2_f32, the reference's
+// arithmetic), 1 = bf16 operands rounded to nearest even with fp32 accumulation
+// (v_mfma_f32_32x32x16_bf16) — an opt-in variant, see gemm_set_bf16
+int g_bf16 = 0;
 
 }  // namespace
 
@@ -106,6 +110,12 @@ bool gemm_prof_on() { return g_prof.on; }
 int gemm_set_splitk_target(int target) {
   const int prev = g_splitk_target;
   if (target > 0) g_splitk_target = target;
+  return prev;
+}
+
+int gemm_set_bf16(int on) {
+  const int prev = g_bf16;
+  if (on >= 0) g_bf16 = on ? 1 : 0;
   return prev;
 }
 
@@ -241,11 +251,13 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   const bool ktwo = g.ak.two || g.bk.two;
   static const bool glog = getenv("DSTAGNN_GEMM_LOG") != nullptr;
   if (glog)
-    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d\n",
-            g.M, g.N, g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk, ns, va, vb);
+    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d bf=%d\n",
+            g.M, g.N, g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk, ns, va, vb, g_bf16);
   using Unit = void (*)(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-  static const Unit units[3][2] = {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}};
-  units[best][ktwo ? 1 : 0](k, akc, bnc, va, vb, hot, st);
+  static const Unit units[2][3][2] = {
+      {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}},
+      {{gemm_c0_k0_bf, gemm_c0_k1_bf}, {gemm_c1_k0_bf, gemm_c1_k1_bf}, {gemm_c2_k0_bf, gemm_c2_k1_bf}}};
+  units[g_bf16 ? 1 : 0][best][ktwo ? 1 : 0](k, akc, bnc, va, vb, hot, st);
   DS_CHECK_LAUNCH();
   if (splitk > 1) {
     int64_t total = (int64_t)g.batch * g.M * g.N;

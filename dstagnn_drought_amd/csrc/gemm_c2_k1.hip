@@ -1,6 +1,6 @@
-// GEMM instantiation unit: 128x32 tile, two-level k maps (see gemm_kern.hpp)
+// GEMM instantiation unit: 128x32 tile, two-level k maps, fp32 (see gemm_kern.hpp)
 #include "gemm_kern.hpp"
 
 namespace dsgemm {
-DS_GEMM_UNIT(gemm_c2_k1, 4, 1, 1, 1, true)
+DS_GEMM_UNIT(gemm_c2_k1, 4, 1, 1, 1, true, false)
 }  // namespace dsgemm

@@ -218,7 +218,7 @@ __device__ __forceinline__ void img_rk(int p, int& row, int& k) {
   }
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
 __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
   constexpr int BK = 32;
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
@@ -337,75 +337,114 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
     if (t + NS - 1 < ntiles) issue(kbeg + (t + NS - 1) * BK, st == 0 ? NS - 1 : st - 1);
     const float* as = Asm + st * BM * BK;
     const float* bs = Bsm + st * BN * BK;
+    // fragments: lane half lk supplies k = 16 lk + 4 q + c (c = 0..3) at step q (A and B agree)
+    auto read_a = [&](int i, int q, float* v4) {
+      const int m = arow0 + i * 32 + lr;
+      if (A_KC) {
+        const int pq = (lk * 4 + q) ^ ((m >> 1) & 7);
+        const float4 v = *reinterpret_cast<const float4*>(as + m * BK + pq * 4);
+        v4[0] = v.x; v4[1] = v.y; v4[2] = v.z; v4[3] = v.w;
+      } else {
 #pragma unroll
-    for (int q = 0; q < BK / 8; ++q) {
-      float av[WM][4], bv[WN][4];
-#pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const int m = arow0 + i * 32 + lr;
-        if (A_KC) {
-          const int pq = (lk * 4 + q) ^ ((m >> 1) & 7);
-          const float4 v = *reinterpret_cast<const float4*>(as + m * BK + pq * 4);
-          av[i][0] = v.x; av[i][1] = v.y; av[i][2] = v.z; av[i][3] = v.w;
-        } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) av[i][c] = as[(lk * 16 + q * 4 + c) * BM + m];
-        }
+        for (int c = 0; c < 4; ++c) v4[c] = as[(lk * 16 + q * 4 + c) * BM + m];
       }
+    };
+    auto read_b = [&](int j, int q, float* v4) {
+      const int n = bcol0 + j * 32 + lr;
+      if (!B_NC) {
+        const int pq = (lk * 4 + q) ^ ((n >> 1) & 7);
+        const float4 v = *reinterpret_cast<const float4*>(bs + n * BK + pq * 4);
+        v4[0] = v.x; v4[1] = v.y; v4[2] = v.z; v4[3] = v.w;
+      } else {
 #pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int n = bcol0 + j * 32 + lr;
-        if (!B_NC) {
-          const int pq = (lk * 4 + q) ^ ((n >> 1) & 7);
-          const float4 v = *reinterpret_cast<const float4*>(bs + n * BK + pq * 4);
-          bv[j][0] = v.x; bv[j][1] = v.y; bv[j][2] = v.z; bv[j][3] = v.w;
-        } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) bv[j][c] = bs[(lk * 16 + q * 4 + c) * BN + n];
-        }
+        for (int c = 0; c < 4; ++c) v4[c] = bs[(lk * 16 + q * 4 + c) * BN + n];
       }
+    };
+    if constexpr (BF) {
+      // bf16 operands (rounded to nearest even), fp32 accumulate: steps q, q+1 form the 8
+      // elements of one v_mfma_f32_32x32x16_bf16 (element e of lane half lk <-> the same k
+      // in A and B, so the k permutation cancels)
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+      for (int q = 0; q < BK / 8; q += 2) {
+        bf16x8 af[WM], bfr[WN];
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+          float v[8];
+          read_a(i, q, v);
+          read_a(i, q + 1, v + 4);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[i][e] = (__bf16)v[e];
+        }
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          float v[8];
+          read_b(j, q, v);
+          read_b(j, q + 1, v + 4);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[j][e] = (__bf16)v[e];
+        }
 #pragma unroll
         for (int i = 0; i < WM; ++i)
 #pragma unroll
           for (int j = 0; j < WN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][c], bv[j][c], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < BK / 8; ++q) {
+        float av[WM][4], bv[WN][4];
+#pragma unroll
+        for (int i = 0; i < WM; ++i) read_a(i, q, av[i]);
+#pragma unroll
+        for (int j = 0; j < WN; ++j) read_b(j, q, bv[j]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int j = 0; j < WN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][c], bv[j][c], acc[i][j], 0, 0, 0);
+      }
     }
     st = st == NS - 1 ? 0 : st + 1;
   }
   gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmK g) {
-  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB>(g);
+  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>(g);
 }
 // same code under a second name: the GEMM a profile reports as "the hot kernel" (Gemm::hot)
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
 __global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmK g) {
-  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB>(g);
+  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>(g);
 }
 }  // namespace
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
 void launch_one(const GemmK& k, dim3 grid, bool hot, hipStream_t st) {
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
+  // the "hot" name exists for the one GEMM it tags (pre_conv forward: 64x64, single-level k, fp32)
+  constexpr bool HOT_OK = WGM == 2 && WGN == 2 && WM == 1 && WN == 1 && !KTWO && !BF;
   const size_t lds = (size_t)k.nstage * (BM + BN) * 32 * sizeof(float);
-  auto ker = hot ? gemm_f32_hot_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB>
-                 : gemm_f32_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB>;
+  auto ker = gemm_f32_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>;
+  if constexpr (HOT_OK) {
+    if (hot) ker = gemm_f32_hot_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>;
+  }
   if (lds > 65536) {  // above the default dynamic-LDS limit: opt in once per kernel
     static bool set[2] = {false, false};
-    if (!set[hot]) {
+    const int h = HOT_OK && hot ? 1 : 0;
+    if (!set[h]) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ker), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(3 * (BM + BN) * 32 * sizeof(float)));
-      set[hot] = true;
+      set[h] = true;
     }
   }
   hipLaunchKernelGGL(ker, grid, dim3(256), lds, st, k);
 }
 
-template <int WGM, int WGN, int WM, int WN, bool KTWO>
+template <int WGM, int WGN, int WM, int WN, bool KTWO, bool BF>
 void launch_cfg(const GemmK& k, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   GemmK kk = k;
@@ -414,10 +453,10 @@ void launch_cfg(const GemmK& k, bool akc, bool bnc, int va, int vb, bool hot, hi
   kk.n_fast = (int64_t)k.M >= (int64_t)k.N ? 1u : 0u;  // A (M x K) is the bigger operand
   const dim3 grid((unsigned)((int64_t)kk.tiles_m * kk.tiles_n * k.batch * k.splitk));
 #define DS_V(AK, BN_)                                                                                        \
-  if (va == 4 && vb == 4)  launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4>(kk, grid, hot, st);              \
-  else if (va == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1>(kk, grid, hot, st);              \
-  else if (vb == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 4>(kk, grid, hot, st);              \
-  else                     launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 1>(kk, grid, hot, st);
+  if (va == 4 && vb == 4)  launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4, BF>(kk, grid, hot, st);              \
+  else if (va == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1, BF>(kk, grid, hot, st);              \
+  else if (vb == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 4, BF>(kk, grid, hot, st);              \
+  else                     launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 1, BF>(kk, grid, hot, st);
   if (akc && bnc) { DS_V(true, true) }
   else if (akc)   { DS_V(true, false) }
   else if (bnc)   { DS_V(false, true) }
@@ -426,9 +465,9 @@ void launch_cfg(const GemmK& k, bool akc, bool bnc, int va, int vb, bool hot, hi
 }
 
 // one explicit instantiation per unit (gemm_c*_k*.hip)
-#define DS_GEMM_UNIT(NAME, WGM, WGN, WM, WN, KTWO)                                                       \
+#define DS_GEMM_UNIT(NAME, WGM, WGN, WM, WN, KTWO, BF)                                                   \
   void NAME(const GemmK& k, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {              \
-    launch_cfg<WGM, WGN, WM, WN, KTWO>(k, akc, bnc, va, vb, hot, st);                                    \
+    launch_cfg<WGM, WGN, WM, WN, KTWO, BF>(k, akc, bnc, va, vb, hot, st);                                \
   }
 void gemm_c0_k0(const GemmK&, bool, bool, int, int, bool, hipStream_t);
 void gemm_c0_k1(const GemmK&, bool, bool, int, int, bool, hipStream_t);
@@ -436,5 +475,11 @@ void gemm_c1_k0(const GemmK&, bool, bool, int, int, bool, hipStream_t);
 void gemm_c1_k1(const GemmK&, bool, bool, int, int, bool, hipStream_t);
 void gemm_c2_k0(const GemmK&, bool, bool, int, int, bool, hipStream_t);
 void gemm_c2_k1(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k0_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k1_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+void gemm_c1_k0_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+void gemm_c1_k1_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k0_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k1_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
 
 }  // namespace dsgemm

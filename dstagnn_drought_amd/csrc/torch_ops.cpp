@@ -643,6 +643,7 @@ std::tuple<Tensor, Tensor, Tensor> graph_topk(const Tensor& sta, int64_t k, int6
 int64_t library_version() { return dstagnn_version(); }
 
 int64_t set_splitk_target(int64_t target) { return dstagnn_set_splitk_target((int)target); }
+int64_t set_gemm_bf16(int64_t on) { return dstagnn_set_gemm_bf16((int)on); }
 
 // GEMM-family profiling: prof_start(capacity); ...; prof_stop() ->
 // [launches, flops, bytes, ms, max_ms, dropped]
@@ -683,6 +684,7 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("version() -> int", library_version);
   m.def("prof_start(int capacity) -> ()", prof_start);
   m.def("set_splitk_target(int target) -> int", set_splitk_target);
+  m.def("set_gemm_bf16(int on) -> int", set_gemm_bf16);
   m.def("prof_stop() -> float[]", prof_stop);
 }
 

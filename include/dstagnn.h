@@ -301,6 +301,14 @@ int dstagnn_prof_stop(dstagnn_prof_stats* stats);
  * tests).  Returns the previous target; target <= 0 only queries. */
 int dstagnn_set_splitk_target(int target);
 
+/* Operand precision of the GEMM family (every contraction of the block, its gradients and
+ * the head): 0 = fp32 (default; the reference's arithmetic), 1 = bf16 operands (round to
+ * nearest even) with fp32 accumulation on v_mfma_f32_32x32x16_bf16.  Softmax, LayerNorm,
+ * the fused attention kernels and all reductions stay fp32.  An opt-in variant with its own
+ * tolerance (tests/test_gpu_parity.py::test_bf16_gemm_variant); not a drop-in for the fp32
+ * reference.  Returns the previous setting; on < 0 only queries. */
+int dstagnn_set_gemm_bf16(int on);
+
 const char* dstagnn_last_error(void);
 int dstagnn_version(void);
 
