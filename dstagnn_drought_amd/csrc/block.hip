@@ -614,7 +614,7 @@ struct Fwd {
   }
   int stage_cheb() { return cheb_forward(cheb_io(), w.gemm_ws, st); }
 
-  int gtu_conv(int q, hipStream_t qs, float* ws) {
+  Gemm gtu_conv(int q) {
     // conv[(bn,t), o] = b[o] + sum_{(j,c)} X[bn, t+j, c] W[o,c,j]; with X rows (t,c) the
     // window (j, c) is one contiguous run of ks*C floats (GTU :190 as an implicit-im2col GEMM)
     const int ks = m.ks[q], Tg = m.Tg[q];
@@ -624,19 +624,13 @@ struct Fwd {
     g.B = s.Wgf[q]; g.bk = idx1(1); g.bn = idx1((int64_t)m.C * ks);  // re-laid (o, j, c)
     g.C = s.conv[q]; g.cm = idx1(2 * m.C); g.cn = idx1(1);
     g.bias = p.gtu_b[q];
-    return run_gemm(g, ws, kGemmWs, qs);
+    return g;
   }
 
-  int stage_tail(bool split) {
-    if (split) {  // the three convolutions are independent: two of them on the side stream
-      DS_TRY(ks.fork());
-      DS_TRY(gtu_conv(1, ks.sd, w.gemm_ws_side));
-      DS_TRY(gtu_conv(0, st, w.gemm_ws));
-      DS_TRY(gtu_conv(2, st, w.gemm_ws));
-      DS_TRY(ks.join());
-    } else {
-      for (int q = 0; q < 3; ++q) DS_TRY(gtu_conv(q, st, w.gemm_ws));
-    }
+  int stage_tail(bool /*split*/) {
+    // the three independent convolutions (kernel widths 3, 5, 7) as ONE grouped launch
+    const Gemm convs[3] = {gtu_conv(0), gtu_conv(1), gtu_conv(2)};
+    DS_TRY(run_gemm_group(convs, 3, w.gemm_ws, kGemmWs, st));
     GtuTailArgs t;  // gates + fcmy + dropout + residual + LN, one workgroup per node
     t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
     for (int q = 0; q < 3; ++q) t.conv[q] = s.conv[q];
@@ -709,6 +703,9 @@ struct Bwd {
   int fork() { return ks.fork(); }
   int join() { return ks.join(); }
 
+  // TAt LayerNorm backward: gamma / beta partial slabs (both fit in the (BFT, N) gcon_a)
+  bool tat_part() const { return ln_bwd_partials_ok(m.N) && 2 * ln_bwd_part_blocks(m.BFT) <= m.BFT; }
+
   int colsum_on(hipStream_t q, const float* in, int64_t A, int O, int I, float* out) {
     if (!out) return 0;
     float* part = q == st ? w.part : w.part_side;
@@ -742,38 +739,58 @@ struct Bwd {
     DS_TRY(fork());
     DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {dout, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
                     {w.dres_t, m.first ? gd.res_b : nullptr}}, m.BN, m.C, m.T));
+    // the bias gradients ride on their weight-gradient GEMMs as a column-sum column
+    // (Gemm::ones_out: sum over the reduction of the gradient operand); a bias whose weight
+    // gradient is not requested gets its own column sum
     if (gd.fcmy_w) {
-      Gemm g;  // dW[t,s] = sum_r dtc[r,t] G[r,s]
+      Gemm g;  // dW[t,s] = sum_r dtc[r,t] G[r,s]; db[t] = sum_r dtc[r,t]
       g.M = m.T; g.N = (int)m.S; g.K = (int)(m.BN * m.C);
       g.A = w.dtc; g.am = idx1(1); g.ak = idx1(m.T);
       g.B = s.G; g.bk = idx1(m.S); g.bn = idx1(1);
       g.C = gd.fcmy_w; g.cm = idx1(m.S); g.cn = idx1(1);
+      g.ones_out = gd.fcmy_b;
       DS_TRY(sgemm(g));
+    } else {
+      DS_TRY(colsum_on(sd, w.dtc, m.BN * m.C, m.T, 1, gd.fcmy_b));
     }
-    DS_TRY(colsum_on(sd, w.dtc, m.BN * m.C, m.T, 1, gd.fcmy_b));
-    for (int q = 0; q < 3; ++q) {
-      const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
-      const int64_t C2 = 2 * (int64_t)m.C;
-      const int64_t cs = C2 * Lp;  // per-(b,n) stride of the padded dconv rows (t', o)
-      if (gd.gtu_w[q]) {
-        Gemm g;  // dW[o,c,j] = sum_{(bn,t')} dconv[bn,t',o] X[bn,t'+j,c]
-        g.M = (int)C2; g.N = m.C * ks; g.K = (int)(m.BN * Tg);
-        g.A = w.dconv[q]; g.a_off = (ks - 1) * C2; g.am = idx1(1); g.ak = idx2(Tg, C2, cs);
-        g.B = s.X; g.bk = idx2(Tg, m.C, m.CT); g.bn = idx1(1);
-        g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx2(m.C, ks, 1);
-        DS_TRY(sgemm(g));
+    {
+      Gemm dws[3];
+      int nw = 0;
+      for (int q = 0; q < 3; ++q) {
+        const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
+        const int64_t C2 = 2 * (int64_t)m.C;
+        const int64_t cs = C2 * Lp;  // per-(b,n) stride of the padded dconv rows (t', o)
+        if (gd.gtu_w[q]) {
+          Gemm& g = dws[nw++];  // dW[o,c,j] = sum_{(bn,t')} dconv[bn,t',o] X[bn,t'+j,c]; db[o] = sum dconv[.,o]
+          g.M = (int)C2; g.N = m.C * ks; g.K = (int)(m.BN * Tg);
+          g.A = w.dconv[q]; g.a_off = (ks - 1) * C2; g.am = idx1(1); g.ak = idx2(Tg, C2, cs);
+          g.B = s.X; g.bk = idx2(Tg, m.C, m.CT); g.bn = idx1(1);
+          g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx2(m.C, ks, 1);
+          g.ones_out = gd.gtu_b[q];
+        } else {
+          DS_TRY(colsum_on(sd, w.dconv[q], m.BN * Lp, (int)C2, 1, gd.gtu_b[q]));
+        }
       }
-      DS_TRY(colsum_on(sd, w.dconv[q], m.BN * Lp, (int)C2, 1, gd.gtu_b[q]));
-      {
-        Gemm g;  // dX[bn,t,c] += sum_{(j',o)} dconv_pad[bn,t+j',o] W[o,c,ks-1-j']
+      if (nw) DS_TRY(run_gemm_group(dws, nw, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd));
+    }
+    {
+      // gpre = (X > 0) * (dX + sum_q sum_{(j',o)} dconv_pad_q[bn,t+j',o] W_q[o,c,ks-1-j']): the three
+      // transposed convolutions as ONE K-concatenated product (K = 2C (3 + 5 + 7)), with the
+      // tail's dX as the beta input and the ReLU backward of the Chebyshev output in the epilogue
+      Gemm segs[3];
+      for (int q = 0; q < 3; ++q) {
+        const int ks = m.ks[q];
+        const int64_t C2 = 2 * (int64_t)m.C;
+        const int64_t cs = C2 * m.Lp[q];
+        Gemm& g = segs[q];
         g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
         g.A = w.dconv[q]; g.am = idx2(m.T, C2, cs); g.ak = idx1(1);
         g.B = s.Wgb[q]; g.bk = idx1(m.C); g.bn = idx1(1);  // flipped (j', o, c)
         g.C = w.dX; g.cm = idx1(m.C); g.cn = idx1(1);
-        g.beta = 1.f;
-        if (q == 2) { g.Cout = w.gpre; g.emask = s.X; }  // fused ReLU backward of the cheb output
-        DS_TRY(gemm(g));
       }
+      segs[0].beta = 1.f;
+      segs[0].Cout = w.gpre; segs[0].emask = s.X;  // fused ReLU backward of the cheb output
+      DS_TRY(run_gemm_kcat(segs, 3, st));
     }
     return 0;
   }
@@ -893,7 +910,8 @@ struct Bwd {
       a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s; a.g = p.embS_g;
       if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
       a.dx = w.dY; a.dxrow = idx1(m.D);
-      a.gcontrib = w.gcon_s; a.bcontrib = w.bcon_s;
+      if (ln_bwd_partials_ok(m.D)) { a.gpart = w.gcon_s; a.bpart = w.bcon_s; }
+      else { a.gcontrib = w.gcon_s; a.bcontrib = w.bcon_s; }
       DS_TRY(op_ln_bwd(a, st));
     }
     // --- side: SAt projection, EmbedS gamma / beta / pos-embedding, pre_conv bias and weight grads
@@ -915,7 +933,12 @@ struct Bwd {
         DS_TRY(op_pack_rows(pk, sd));
       }
     }
-    DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}, {w.dY, gd.pre_conv_b}}, m.BN, m.D, 1));
+    // gamma / beta: column sums of the LN backward's partial slabs (or contribution tensors)
+    DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}},
+                   ln_bwd_partials_ok(m.D) ? ln_bwd_part_blocks(m.BN) : m.BN, m.D, 1));
+    // pre_conv bias: its own column sum (as a column-sum column of the dW GEMM it would add a
+    // whole 64-wide column tile to the 384-wide output: measured slower)
+    DS_TRY(colsum_on(sd, w.dY, m.BN, m.D, 1, gd.pre_conv_b));
     if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sd));
     if (gd.pre_conv_w) {
       Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
@@ -946,7 +969,11 @@ struct Bwd {
       a.dy = w.dO; a.dyrow = idx1(N);
       a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat; a.g = p.tat_ln_g;
       a.dx = w.dU; a.dxrow = idx1(N);
-      a.gcontrib = w.gcon_a; a.bcontrib = nullptr;
+      if (tat_part()) {  // both slabs in gcon_a ((BFT, N) holds 2 slabs)
+        a.gpart = w.gcon_a; a.bpart = w.gcon_a + ln_bwd_part_blocks(m.BFT) * N;
+      } else {
+        a.gcontrib = w.gcon_a;
+      }
       DS_TRY(op_ln_bwd(a, st));
     }
     {  // dctx = dU Wfc
@@ -963,7 +990,12 @@ struct Bwd {
       DS_TRY(op_sum_middle(w.dscore, m.B, m.F, (int64_t)m.h * m.T * m.T, dres, 0.f, st));
     // --- side: TAt LN gamma / beta, fc and Q|K|V weight grads (one fork)
     DS_TRY(fork());
-    DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
+    if (tat_part()) {
+      const int64_t pb = ln_bwd_part_blocks(m.BFT);
+      DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1));
+    } else {
+      DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
+    }
     if (gd.tat_fc) {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
       Gemm g;
       g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
@@ -1006,10 +1038,14 @@ struct Bwd {
       a.dy = w.dE; a.dyrow = idx1(N);
       a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et; a.g = p.embT_g;
       a.dx = w.du_et; a.dxrow = idx1(N);
-      a.gcontrib = w.gcon_e; a.bcontrib = nullptr;
+      const int64_t pb = ln_bwd_part_blocks((int64_t)m.B * m.T);
+      const bool part = ln_bwd_partials_ok(m.N) && 2 * pb <= (int64_t)m.B * m.T;
+      if (part) { a.gpart = w.gcon_e; a.bpart = w.gcon_e + pb * N; }
+      else a.gcontrib = w.gcon_e;
       DS_TRY(op_ln_bwd(a, st));
       DS_TRY(fork());
-      DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dE, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
+      if (part) DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.gcon_e + pb * N, gd.embT_b}}, pb, m.N, 1));
+      else DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dE, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
       if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sd));
       DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
     } else {

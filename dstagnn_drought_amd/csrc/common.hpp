@@ -226,10 +226,19 @@ struct Gemm {
   const float* emask = nullptr;
   float* Cout = nullptr;
   int hot = 0;  // 1: launch under the separately named gemm_f32_hot_kernel (profiling tag)
+  // optional column sums of A over k: ones_out[m * ones_stride] = alpha * sum_k A[m][k] (a bias
+  // gradient folded into its weight-gradient GEMM); plain epilogue only (no beta/bias/relu/emask)
+  float* ones_out = nullptr; int64_t ones_stride = 1;
   Gemm() { am = ak = az = bk = bn = bz = cm = cn = cz = idx1(0); }
 };
 // ws: split-K partial slab scratch (may be null -> no split)
 int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st);
+// 1..3 independent problems (disjoint outputs) as one grouped launch where their kernel
+// configurations agree; each takes its own slice of the split-K slab space ws
+int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream_t st);
+// 1..3 products summed over their concatenated K ranges into problem 0's output and
+// epilogue (same M, N, batch): C = epilogue_0(sum_p A_p B_p), one launch, no split-K
+int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st);
 // GEMM-family profiling (gemm.hip): while on, the block runs on ONE stream (no side-stream
 // overlap) so every recorded GEMM duration is its own
 bool gemm_prof_on();

@@ -28,21 +28,34 @@ namespace {
 
 
 // out[zb][m][n] = epilogue( sum_s ws[zb][s][m][n] ).  A workgroup takes 256/G outputs and
-// G split groups per output (G = power of two ~ splitk/8), combined by an LDS tree.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmK gin, int G) {
+// G split groups per output (G = power of two ~ splitk/8, per problem), combined by an LDS
+// tree.  Grouped like the GEMM: problem p owns workgroups [start[p], start[p+1]).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmG gin) {
   __shared__ float red[256];
-  const GemmK g = load_args(gin);
+  uint32_t lbid, lnwg;
+  const GemmK g = load_group(gin, lbid, lnwg);
+  const int G = g.red_g;
   const int64_t MN = (int64_t)g.M * g.N;
   const int64_t total = (int64_t)g.batch * MN;
   const int per = 256 / G;
   const int c = threadIdx.x / G, q = threadIdx.x % G;
-  const int64_t idx = (int64_t)blockIdx.x * per + c;
+  const int64_t idx = (int64_t)lbid * per + c;
   float s = 0.f;
   if (idx < total) {
     const int zb = (int)(idx / MN);
     const int64_t mn = idx % MN;
     const float* p = g.ws + (int64_t)zb * g.splitk * MN + mn;
-    for (int sp = q; sp < g.splitk; sp += G) s += p[(int64_t)sp * MN];
+    // four independent chains so the loads of one thread overlap (fixed order: deterministic)
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int sp = q;
+    for (; sp + 3 * G < g.splitk; sp += 4 * G) {
+      s += p[(int64_t)sp * MN];
+      s1 += p[(int64_t)(sp + G) * MN];
+      s2 += p[(int64_t)(sp + 2 * G) * MN];
+      s3 += p[(int64_t)(sp + 3 * G) * MN];
+    }
+    for (; sp < g.splitk; sp += G) s += p[(int64_t)sp * MN];
+    s = (s + s1) + (s2 + s3);
   }
   red[threadIdx.x] = s;
   __syncthreads();
@@ -161,22 +174,38 @@ int gemm_prof_stop(dstagnn_prof_stats* out) {
   return 0;
 }
 
-int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
-  if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return 0;
-  ProfRec* prec = nullptr;
-  if (g_prof.on) {
-    if (g_prof.n < g_prof.cap) {
-      prec = &g_prof.rec[g_prof.n++];
-      prec->flops = 2.0 * g.M * g.N * (double)g.K * g.batch;
-      prec->bytes = 4.0 * g.batch * ((double)g.M * g.K + (double)g.K * g.N + (double)g.M * g.N * (g.beta != 0.f ? 2 : 1));
-      (void)hipEventRecord(prec->e0, st);
-    } else {
-      ++g_prof.dropped;
-    }
-  }
-  if (!g.A || !g.B || !g.C) { set_last_error("gemm: null operand"); return DSTAGNN_E_ARG; }
+namespace {
+
+// one problem's launch plan: its kernel descriptor and the kernel configuration it needs
+bool gemm_log_on() {
+  static const bool on = getenv("DSTAGNN_GEMM_LOG") != nullptr;
+  return on;
+}
+
+struct Plan {
   GemmK k;
-  k.M = g.M; k.N = g.N; k.K = g.K; k.batch = g.batch;
+  char log[200];
+  int best, va, vb, ns;
+  bool akc, bnc, ktwo, hot;
+  bool same_kernel(const Plan& o) const {
+    return best == o.best && va == o.va && vb == o.vb && ns == o.ns && akc == o.akc && bnc == o.bnc &&
+           ktwo == o.ktwo && hot == o.hot;
+  }
+};
+
+// Plan one problem (tile shape, split-K, DMA widths, stages); ws: its split-K slab space.
+int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
+  if (!g.A || !g.B || !g.C) { set_last_error("gemm: null operand"); return DSTAGNN_E_ARG; }
+  if (g.ones_out && (g.cm.two || g.beta != 0.f || g.emask || g.bias || g.relu)) {
+    set_last_error("gemm: column-sum output only with a plain epilogue");
+    return DSTAGNN_E_ARG;
+  }
+  Plan& pl = *out;
+  GemmK& k = pl.k;
+  k = GemmK{};
+  const int Nk = g.N + (g.ones_out ? 1 : 0);  // kernel columns (the column-sum column last)
+  k.M = g.M; k.N = Nk; k.K = g.K; k.batch = g.batch;
+  k.nload = g.N; k.ones_out = g.ones_out; k.ones_stride = (int32_t)g.ones_stride;
   // negative strides (the flipped-kernel convolution gradient): rebase the operand
   // pointer so every per-element offset the kernel forms is >= 0 and fits uint32
   k.abias = (int32_t)-(idx_min(g.am, g.M) + idx_min(g.ak, g.K));
@@ -189,6 +218,7 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
       idx_span(g.am, g.M) + idx_span(g.ak, g.K) >= (1ll << 30) - 2048 ||
       idx_span(g.bn, g.N) + idx_span(g.bk, g.K) >= (1ll << 30) - 2048 ||
       idx_span(g.cm, g.M) + idx_span(g.cn, g.N) >= (1ll << 31) ||
+      (int64_t)g.M * g.ones_stride >= (1ll << 31) ||
       g.bias_stride >= (1ll << 31) || (int64_t)g.N * g.bias_stride >= (1ll << 31)) {
     set_last_error("gemm: operand offsets exceed int32 (split the batch)");
     return DSTAGNN_E_SHAPE;
@@ -207,24 +237,23 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   // or the grid is large enough for 128x128 tiles to fill the chip several times over.
   int best = 0;
   {
-    const int64_t b64 = cdiv64(g.M, 64) * cdiv64(g.N, 64) * g.batch;
-    if (g.N <= 32) best = 2;
+    const int64_t b64 = cdiv64(g.M, 64) * cdiv64(Nk, 64) * g.batch;
+    if (Nk <= 32) best = 2;
     else if (b64 >= 4096 && g.K >= 1024) best = 1;
     else best = 0;
   }
   if (env_cfg >= 0 && env_cfg < (int)(sizeof(kCfgs) / sizeof(kCfgs[0]))) best = env_cfg;
-  Cfg cfg = kCfgs[best];
-  int64_t blocks = cdiv64(g.M, cfg.bm()) * cdiv64(g.N, cfg.bn()) * g.batch;
+  const Cfg cfg = kCfgs[best];
+  const int64_t blocks = cdiv64(g.M, cfg.bm()) * cdiv64(Nk, cfg.bn()) * g.batch;
 
   // split-K when the grid leaves CUs idle and the reduction is long
   int splitk = 1;
-  const int split_target = g_splitk_target;
   if (g.K > 0 && blocks < 128 && g.K >= 512 && ws) {
-    int want = (int)std::min<int64_t>(512, cdiv64(split_target, blocks));
+    int want = (int)std::min<int64_t>(512, cdiv64(g_splitk_target, blocks));
     int maxk = g.K / 128;  // keep >= 128 k per split
     splitk = std::max(1, std::min(want, maxk));
     if (env_split > 0) splitk = std::min(env_split, std::max(1, g.K / 64));
-    while (splitk > 1 && (size_t)g.batch * splitk * g.M * g.N > ws_floats) --splitk;
+    while (splitk > 1 && (size_t)g.batch * splitk * g.M * Nk > ws_floats) --splitk;
   }
   int kchunk = g.K;
   if (splitk > 1) {
@@ -233,40 +262,203 @@ int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) {
   }
   if (g.K <= 0) { splitk = 1; kchunk = 0; }
   k.splitk = splitk; k.kchunk = kchunk;
+  k.tiles_m = (uint32_t)cdiv64(g.M, cfg.bm());
+  k.tiles_n = (uint32_t)cdiv64(Nk, cfg.bn());
+  k.n_fast = (int64_t)g.M >= (int64_t)Nk ? 1u : 0u;  // A (M x K) is the bigger operand
+  k.count = (uint32_t)(blocks * splitk);
+  k.red_g = 1;
+  while (k.red_g < 64 && k.red_g * 8 < splitk) k.red_g *= 2;
 
-  const bool akc = !g.ak.two && g.ak.s0 == 1;
-  const bool bnc = !g.bn.two && g.bn.s0 == 1;
-  const bool hot = g.hot != 0;
+  pl.best = best;
+  pl.akc = !g.ak.two && g.ak.s0 == 1;
+  pl.bnc = !g.bn.two && g.bn.s0 == 1;
+  pl.ktwo = g.ak.two || g.bk.two;
+  pl.hot = g.hot != 0;
   static const int env_v = getenv("DSTAGNN_GEMM_DMA16") ? atoi(getenv("DSTAGNN_GEMM_DMA16")) : 1;
-  const int va = env_v ? dma_width(g.A + g.a_off, g.am, g.M, g.ak, g.az, akc) : 1;
-  const int vb = env_v ? dma_width(g.B + g.b_off, g.bn, g.N, g.bk, g.bz, !bnc) : 1;
+  pl.va = env_v ? dma_width(g.A + g.a_off, g.am, g.M, g.ak, g.az, pl.akc) : 1;
+  pl.vb = env_v ? dma_width(g.B + g.b_off, g.bn, g.N, g.bk, g.bz, !pl.bnc) : 1;
   // LDS pipeline depth: 3 stages keep two k-tiles in flight per workgroup (needed when a CU
   // holds about one workgroup: long split-K reductions); 2 stages cut the workgroup's LDS by a
   // third, so more workgroups are resident per CU and latency is hidden across workgroups
   // (measured on the bench step: -1.5 % with 2 stages wherever the grid exceeds the CUs)
-  int ns = blocks * splitk > 256 ? 2 : 3;
+  pl.ns = blocks * splitk > 256 ? 2 : 3;
   static const int env_ns = getenv("DSTAGNN_GEMM_NS") ? atoi(getenv("DSTAGNN_GEMM_NS")) : 0;
-  if (env_ns == 2 || env_ns == 3) ns = env_ns;
-  k.nstage = ns;
-  const bool ktwo = g.ak.two || g.bk.two;
-  static const bool glog = getenv("DSTAGNN_GEMM_LOG") != nullptr;
-  if (glog)
-    fprintf(stderr, "[gemm] M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d bf=%d\n",
-            g.M, g.N, g.K, g.batch, best, splitk, (int)akc, (int)bnc, (int)ktwo, (long long)blocks * splitk, ns, va, vb, g_bf16);
-  using Unit = void (*)(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+  if (env_ns == 2 || env_ns == 3) pl.ns = env_ns;
+  k.nstage = pl.ns;
+  if (gemm_log_on()) {
+    // one "[gemm]" line per kernel launch (run_gemm_group joins a group's problems with " | ")
+    snprintf(pl.log, sizeof(pl.log), "M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d bf=%d ones=%d",
+             g.M, Nk, g.K, g.batch, best, splitk, (int)pl.akc, (int)pl.bnc, (int)pl.ktwo, (long long)blocks * splitk,
+             pl.ns, pl.va, pl.vb, g_bf16, g.ones_out ? 1 : 0);
+  }
+  return 0;
+}
+
+// one grouped argument: slices padded to multiples of 8 workgroups; returns the grid size
+uint32_t make_group(const GemmK* const* ks, const uint32_t* counts, int n, GemmG* gg) {
+  *gg = GemmG{};
+  uint32_t at = 0;
+  for (int p = 0; p < n; ++p) {
+    gg->start[p] = at;
+    gg->k[p] = *ks[p];
+    at += (counts[p] + 7u) & ~7u;
+  }
+  for (int p = n; p < 4; ++p) gg->start[p] = at;
+  return at;
+}
+
+void launch_plans(Plan* const* ps, int n, hipStream_t st) {
+  const GemmK* ks[kGroupMax];
+  uint32_t counts[kGroupMax];
+  for (int p = 0; p < n; ++p) { ks[p] = &ps[p]->k; counts[p] = ps[p]->k.count; }
+  GemmG gg;
+  const uint32_t grid = make_group(ks, counts, n, &gg);
+  using Unit = void (*)(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
   static const Unit units[2][3][2] = {
       {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}},
       {{gemm_c0_k0_bf, gemm_c0_k1_bf}, {gemm_c1_k0_bf, gemm_c1_k1_bf}, {gemm_c2_k0_bf, gemm_c2_k1_bf}}};
-  units[g_bf16 ? 1 : 0][best][ktwo ? 1 : 0](k, akc, bnc, va, vb, hot, st);
-  DS_CHECK_LAUNCH();
-  if (splitk > 1) {
-    int64_t total = (int64_t)g.batch * g.M * g.N;
-    int G = 1;
-    while (G < 64 && G * 8 < splitk) G *= 2;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv64(total, 256 / G)), dim3(256), 0, st, k, G);
+  const Plan& pl = *ps[0];
+  units[g_bf16 ? 1 : 0][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, pl.hot, st);
+}
+
+}  // namespace
+
+// Up to kGroupMax independent problems: planned one by one (each its own slice of the
+// split-K slab space), launched as ONE grouped kernel when their kernel configurations agree
+// (else one launch per run of equal configurations), their split-K folds as one grouped
+// reduce.  The problems must not write overlapping outputs.
+int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream_t st) {
+  if (n < 1 || n > kGroupMax) { set_last_error("gemm: 1..3 problems per group"); return DSTAGNN_E_ARG; }
+  ProfRec* prec = nullptr;
+  Plan plans[kGroupMax];
+  Plan* live[kGroupMax];
+  int nl = 0;
+  size_t ws_used = 0;
+  double flops = 0, bytes = 0;
+  for (int i = 0; i < n; ++i) {
+    const Gemm& g = gs[i];
+    if (g.M <= 0 || g.N <= 0 || g.batch <= 0) continue;
+    DS_TRY(plan_gemm(g, ws ? ws + ws_used : nullptr, ws_floats - ws_used, &plans[i]));
+    const GemmK& k = plans[i].k;
+    if (k.splitk > 1) ws_used += (size_t)k.batch * k.splitk * k.M * k.N;
+    flops += 2.0 * g.M * g.N * (double)g.K * g.batch;
+    bytes += 4.0 * g.batch * ((double)g.M * g.K + (double)g.K * g.N + (double)g.M * g.N * (g.beta != 0.f ? 2 : 1));
+    live[nl++] = &plans[i];
+  }
+  if (!nl) return 0;
+  if (g_prof.on) {
+    if (g_prof.n < g_prof.cap) {
+      prec = &g_prof.rec[g_prof.n++];
+      prec->flops = flops;
+      prec->bytes = bytes;
+      (void)hipEventRecord(prec->e0, st);
+    } else {
+      ++g_prof.dropped;
+    }
+  }
+  for (int i = 0; i < nl;) {
+    int j = i + 1;
+    while (j < nl && live[j]->same_kernel(*live[i])) ++j;
+    launch_plans(live + i, j - i, st);
+    DS_CHECK_LAUNCH();
+    if (gemm_log_on()) {
+      fprintf(stderr, "[gemm] %s", live[i]->log);
+      for (int q = i + 1; q < j; ++q) fprintf(stderr, " | %s", live[q]->log);
+      fprintf(stderr, "\n");
+    }
+    i = j;
+  }
+  // split-K folds of every problem that split, as one grouped launch
+  const GemmK* rk[kGroupMax];
+  uint32_t rc[kGroupMax];
+  int nr = 0;
+  for (int i = 0; i < nl; ++i) {
+    const GemmK& k = live[i]->k;
+    if (k.splitk <= 1) continue;
+    rk[nr] = &k;
+    rc[nr] = (uint32_t)cdiv64((int64_t)k.batch * k.M * k.N, 256 / k.red_g);
+    ++nr;
+  }
+  if (nr) {
+    GemmG gg;
+    const uint32_t grid = make_group(rk, rc, nr, &gg);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, gg);
     DS_CHECK_LAUNCH();
   }
   if (prec) (void)hipEventRecord(prec->e1, st);
   return 0;
 }
+
+// ONE product over the concatenation of the problems' K ranges:
+//   C = epilogue_0( sum_p A_p B_p )
+// (same M, N, batch and kernel configuration; each A_p / B_p with its own pointer and maps;
+// the epilogue, C and its maps are problem 0's).  One launch, no split-K, no intermediate C
+// round trips: the GTU transposed convolutions of widths 3, 5, 7 accumulating into one dX.
+int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
+  if (n < 1 || n > kGroupMax) { set_last_error("gemm: 1..3 K segments"); return DSTAGNN_E_ARG; }
+  const Gemm& g0 = gs[0];
+  if (g0.M <= 0 || g0.N <= 0 || g0.batch <= 0) return 0;
+  Plan plans[kGroupMax];
+  double flops = 0, bytes = 0;
+  for (int p = 0; p < n; ++p) {
+    const Gemm& g = gs[p];
+    if (g.M != g0.M || g.N != g0.N || g.batch != g0.batch || g.ones_out || g.hot) {
+      set_last_error("gemm kcat: segments must share M, N, batch (no column sums)");
+      return DSTAGNN_E_ARG;
+    }
+    DS_TRY(plan_gemm(g, nullptr, 0, &plans[p]));
+    const Plan& q0 = plans[0];
+    const bool kcat_ok = q0.best == 2 && !q0.ktwo && q0.akc && q0.bnc && q0.va == 4 && q0.vb == 4;  // kcat_supported
+    if (!kcat_ok || (p && !plans[p].same_kernel(plans[0]))) {
+      // different kernels (DMA widths / map kinds): fall back to a chain of launches
+      Gemm first = g0, next;
+      first.Cout = nullptr; first.emask = nullptr;
+      DS_TRY(run_gemm(first, nullptr, 0, st));
+      for (int q = 1; q < n; ++q) {
+        next = gs[q];
+        next.C = g0.C; next.cm = g0.cm; next.cn = g0.cn; next.cz = g0.cz; next.c_off = g0.c_off;
+        next.beta = 1.f; next.bias = nullptr; next.relu = 0;
+        next.Cout = q == n - 1 ? g0.Cout : nullptr;
+        next.emask = q == n - 1 ? g0.emask : nullptr;
+        DS_TRY(run_gemm(next, nullptr, 0, st));
+      }
+      return 0;
+    }
+    flops += 2.0 * g.M * g.N * (double)g.K * g.batch;
+    bytes += 4.0 * g.batch * ((double)g.M * g.K + (double)g.K * g.N);
+  }
+  bytes += 4.0 * g0.batch * (double)g0.M * g0.N * (g0.beta != 0.f ? 2 : 1);
+  ProfRec* prec = nullptr;
+  if (g_prof.on) {
+    if (g_prof.n < g_prof.cap) {
+      prec = &g_prof.rec[g_prof.n++];
+      prec->flops = flops;
+      prec->bytes = bytes;
+      (void)hipEventRecord(prec->e0, st);
+    } else {
+      ++g_prof.dropped;
+    }
+  }
+  GemmG gg{};
+  const uint32_t grid = (plans[0].k.count + 7u) & ~7u;
+  gg.start[0] = (uint32_t)n;  // K-concatenated
+  for (int p = 1; p < 4; ++p) gg.start[p] = grid;
+  for (int p = 0; p < n; ++p) gg.k[p] = plans[p].k;
+  using Unit = void (*)(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+  static const Unit units[2][3][2] = {
+      {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}},
+      {{gemm_c0_k0_bf, gemm_c0_k1_bf}, {gemm_c1_k0_bf, gemm_c1_k1_bf}, {gemm_c2_k0_bf, gemm_c2_k1_bf}}};
+  const Plan& pl = plans[0];
+  units[g_bf16 ? 1 : 0][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, false, st);
+  DS_CHECK_LAUNCH();
+  if (gemm_log_on()) {
+    fprintf(stderr, "[gemm] kcat %s", plans[0].log);
+    for (int q = 1; q < n; ++q) fprintf(stderr, " + %s", plans[q].log);
+    fprintf(stderr, "\n");
+  }
+  if (prec) (void)hipEventRecord(prec->e1, st);
+  return 0;
+}
+
+int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st) { return run_gemm_group(&g, 1, ws, ws_floats, st); }
 

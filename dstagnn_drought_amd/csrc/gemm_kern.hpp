@@ -26,17 +26,95 @@ struct GemmK {
   const float* emask;  // optional: zero where emask <= 0 (same maps as C, offset c_off)
   float* Cout;         // optional: destination instead of C (beta still reads C)
   int nstage;          // LDS pipeline stages (2 or 3; dynamic LDS)
+  // optional column-sum column: N = nload + 1 and column nload of B reads as 1.0, so
+  // C[m][nload] = sum_k A[m][k] (a bias gradient folded into its weight-gradient GEMM);
+  // it is stored to ones_out[m * ones_stride], never into C.  Without it nload = N.
+  int nload;
+  float* ones_out;
+  int32_t ones_stride;
+  uint32_t count;      // workgroups of this problem (tiles x batch x splitk; the grid slice is padded to 8)
+  int red_g;           // split-K fold: split groups per output (splitk_reduce_kernel)
+};
+
+// One launch runs up to kGroupMax independent problems of the same kernel configuration
+// (the three GTU convolutions, their three weight gradients): problem p owns workgroups
+// [start[p], start[p+1]); each slice starts at a multiple of 8, so a workgroup's XCD (id % 8)
+// is the same in the slice as in the grid and the XCD-aware tile order holds per problem.
+constexpr int kGroupMax = 3;
+struct GemmG {
+  // start[p] (p = 1..3): first workgroup of problem p (the grid size for p >= n).
+  // start[0] = 0 for independent problems; = n >= 2 for ONE K-concatenated problem
+  // (run_gemm_kcat): every workgroup runs its tile over the K ranges of problems 0..n-1 in
+  // turn (same M, N, tiles; own A / B operands and maps) into one accumulator and stores it
+  // with problem 0's epilogue.
+  uint32_t start[4];
+  GemmK k[kGroupMax];
 };
 
 namespace {
 
 constexpr int BKMAX = 32;  // k-tile depth
 
-
-
+// The problem of this workgroup and its descriptor, in one memory round: every lane loads
+// dwords lane, lane+64, ... of the whole group argument, the slice starts come back by
+// readlane, and the selected problem's dwords by readlane from compile-time positions (one
+// uniform branch per problem index).  See load_args.
+template <int P, int NV>
+__device__ __forceinline__ void pick_problem(const uint32_t (&v)[NV], uint32_t* w) {
+  constexpr int NK = (int)(sizeof(GemmK) / 4);
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    constexpr int H = 4;  // start[4]
+    const int x = H + P * NK + i;
+    w[i] = (uint32_t)__builtin_amdgcn_readlane((int)v[x >> 6], x & 63);
+  }
+}
+constexpr int kGroupWords = (int)(sizeof(GemmG) / 4), kGroupVregs = (kGroupWords + 63) / 64;
+__device__ __forceinline__ void load_group_words(const GemmG& in, uint32_t (&v)[kGroupVregs]) {
+  static_assert(sizeof(GemmK) % 4 == 0 && sizeof(GemmG) % 4 == 0, "dword structs");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&in);
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int r = 0; r < kGroupVregs; ++r)
+    v[r] = src[lane + 64 * r < kGroupWords ? lane + 64 * r : kGroupWords - 1];
+}
+__device__ __forceinline__ uint32_t group_word(const uint32_t (&v)[kGroupVregs], int i) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v[0], i);
+}
+// problem p's descriptor (p wave-uniform)
+__device__ __forceinline__ GemmK pick(const uint32_t (&v)[kGroupVregs], int p) {
+  constexpr int NK = (int)(sizeof(GemmK) / 4);
+  union U {
+    GemmK t;
+    uint32_t w[NK];
+    __device__ U() {}
+  } u;
+  if (p == 2) pick_problem<2>(v, u.w);
+  else if (p == 1) pick_problem<1>(v, u.w);
+  else pick_problem<0>(v, u.w);
+  return u.t;
+}
+// this workgroup's problem, its workgroup index within the problem's slice and the slice size
+__device__ __forceinline__ int group_slot(const uint32_t (&v)[kGroupVregs], uint32_t& lbid, uint32_t& lnwg) {
+  const uint32_t s1 = group_word(v, 1), s2 = group_word(v, 2), s3 = group_word(v, 3);
+  const uint32_t bid = blockIdx.x;
+  if (bid >= s2) { lbid = bid - s2; lnwg = s3 - s2; return 2; }
+  if (bid >= s1) { lbid = bid - s1; lnwg = s2 - s1; return 1; }
+  lbid = bid; lnwg = s1;
+  return 0;
+}
+__device__ __forceinline__ GemmK load_group(const GemmG& in, uint32_t& lbid, uint32_t& lnwg) {
+  uint32_t v[kGroupVregs];
+  load_group_words(in, v);
+  return pick(v, group_slot(v, lbid, lnwg));
+}
 
 
 __device__ __forceinline__ void epilogue_store(const GemmK& g, int zb, int m, int n, float v) {
+  if (n == g.nload) {  // the column-sum column (only exists with ones_out)
+    g.ones_out[(int64_t)m * g.ones_stride] = v * g.alpha;
+    return;
+  }
   const int64_t zo = zoff(g.cz, zb);
   const int32_t o = koff(g.cm, m) + koff(g.cn, n);
   v *= g.alpha;
@@ -56,10 +134,10 @@ struct TileCoord {
 // blocks that re-read one panel of the big operand sit behind the same L2.
 // Bijective for any count.
 template <int BM, int BN>
-__device__ __forceinline__ TileCoord decode_tile(const GemmK& g) {
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
+__device__ __forceinline__ TileCoord decode_tile(const GemmK& g, uint32_t bid, uint32_t nwg, bool& idle) {
   const uint32_t q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
   const uint32_t t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  idle = t >= g.count;  // padding of the problem's grid slice
   const uint32_t gn = g.tiles_n, gm = g.tiles_m;
   const uint32_t tf = g.n_fast ? gn : gm, ts = g.n_fast ? gm : gn;
   const uint32_t f = t % tf, tr = t / tf, sl = tr % ts;
@@ -84,6 +162,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK& g, const TileCoord& c
     for (int j = 0; j < WN; ++j) {
       const int n = c.n0 + wcol0 + j * 32 + lr;
       if (n >= g.N) continue;
+      if (n == g.nload) {  // column-sum column
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (m >= g.M) continue;
+          if (g.splitk > 1) g.ws[(((int64_t)c.zb * g.splitk + c.sp) * g.M + m) * g.N + n] = acc[i][j][r];
+          else epilogue_store(g, c.zb, m, n, acc[i][j][r]);
+        }
+        continue;
+      }
       if (reads) {
         // beta * C and the ReLU mask: all 16 loads issued before the first store (the
         // stores may alias C, so element-wise load/store pairs would serialise 16 memory
@@ -149,6 +237,16 @@ __device__ float g_zero_page[64];  // k >= K lanes of the last tile fetch zeros 
 // four DMAs into consecutive 1 KiB LDS slots under one M0: the instruction offset moves
 // both the LDS destination and the global source (probed: tools/glds_probe.hip), so the
 // VGPR offsets carry -1024*i and the SGPR base is pre-lowered by 4 KiB to keep them >= 0.
+// wave-uniform values for the SGPR operands of the DMA asm (the compiler may keep a uniform
+// value in a VGPR after the per-problem branch of load_group; readfirstlane is free when not)
+__device__ __forceinline__ const float* sgpr_ptr(const float* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t sgpr_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
 __device__ __forceinline__ void glds4_saddr(const float* base_m4k, uint32_t o0, uint32_t o1, uint32_t o2,
                                             uint32_t o3, uint32_t lds_addr) {
   uint32_t keep;
@@ -161,7 +259,7 @@ __device__ __forceinline__ void glds4_saddr(const float* base_m4k, uint32_t o0, 
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"((o0 << 2) + 4096u), "v"((o1 << 2) + 3072u), "v"((o2 << 2) + 2048u), "v"((o3 << 2) + 1024u),
-        "s"(base_m4k), "s"(lds_addr)
+        "s"(sgpr_ptr(base_m4k)), "s"(sgpr_u32(lds_addr))
       : "memory");
 }
 __device__ __forceinline__ void glds_vaddr(const void* p, uint32_t lds_addr) {
@@ -169,7 +267,7 @@ __device__ __forceinline__ void glds_vaddr(const void* p, uint32_t lds_addr) {
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(p), "s"(lds_addr)
+      : "v"(p), "s"(sgpr_u32(lds_addr))
       : "memory");
 }
 __device__ __forceinline__ uint32_t lds_addr_of(const float* p) {
@@ -192,7 +290,7 @@ __device__ __forceinline__ void glds16_saddr(const float* base, uint32_t off_byt
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(off_bytes), "s"(base), "s"(lds_addr)
+      : "v"(off_bytes), "s"(sgpr_ptr(base)), "s"(sgpr_u32(lds_addr))
       : "memory");
 }
 
@@ -218,8 +316,8 @@ __device__ __forceinline__ void img_rk(int p, int& row, int& k) {
   }
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
-__device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
+__device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   constexpr int BK = 32;
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   constexpr int NA = BM * BK / (256 * VA), NB = BN * BK / (256 * VB);  // DMA instructions per thread per k-tile
@@ -227,14 +325,32 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
   static_assert(NA + NB < 64 && LA1 % 4 == 0 && LB1 % 4 == 0, "vmcnt range / DMA batches");
   extern __shared__ __attribute__((aligned(16))) float gsm[];
 
-  const GemmK g = load_args(gin);
+  uint32_t gv[kGroupVregs];
+  load_group_words(gin, gv);
+  uint32_t lbid, lnwg;
+  const GemmK g = pick(gv, group_slot(gv, lbid, lnwg));
+  bool idle;
+  const TileCoord tc = decode_tile<BM, BN>(g, lbid, lnwg, idle);
+  if (idle) return;  // uniform over the workgroup, before any barrier
   const int NS = g.nstage;  // 2 or 3 LDS stages (dynamic LDS)
   float* const Asm = gsm;
   float* const Bsm = gsm + NS * BM * BK;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WGN, wc = wid % WGN;
-  const TileCoord tc = decode_tile<BM, BN>(g);
+  // lane half h (lane >> 5) supplies k = 16 h + s at MFMA step s (A and B agree)
+  const int lr = lane & 31, lk = lane >> 5;
+  const int arow0 = wr * 32 * WM, bcol0 = wc * 32 * WN;
+  floatx16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // the K loop of one problem (of one K segment) into acc
+  auto kseg = [&](const GemmK& g) {
   const int kbeg = tc.sp * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   const float* A = g.A + zoff(g.az, tc.zb);
@@ -259,7 +375,7 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
     img_rk<BN, !B_NC>(VB == 4 ? 1024 * j + 256 * wid + 4 * lane : 256 * j + 64 * wid + lane, col, k);
     b_kl[j] = k;
     const int n = tc.n0 + col;
-    bo[j] = (uint32_t)g.bbias + (n < g.N ? (uint32_t)koff(g.bn, n) : 0u);
+    bo[j] = (uint32_t)g.bbias + (n < g.nload ? (uint32_t)koff(g.bn, n) : 0u);
     if (!KTWO) bo[j] += (uint32_t)(k * g.bk.s0);
   }
   auto aoff = [&](int j, int k0) -> uint32_t {
@@ -307,26 +423,16 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
         int col, k;
         img_rk<BN, !B_NC>(256 * j + 64 * wid + lane, col, k);
         const int n = tc.n0 + col;
-        const uint32_t o = (uint32_t)g.bbias + (n < g.N ? (uint32_t)koff(g.bn, n) : 0u) + (uint32_t)koff(g.bk, k0 + k);
+        const uint32_t o = (uint32_t)g.bbias + (n < g.nload ? (uint32_t)koff(g.bn, n) : 0u) + (uint32_t)koff(g.bk, k0 + k);
         glds_vaddr(k0 + k < kend ? gp(Bp, o) : (const void*)g_zero_page, sb + 4 * (256 * j + 64 * wid));
       }
     }
   };
 
-  floatx16 acc[WM][WN];
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
   const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const bool ones_tile = g.nload < g.N && tc.n0 + BN > g.nload;  // uniform
   for (int s0 = 0; s0 < NS - 1; ++s0)
     if (s0 < ntiles) issue(kbeg + s0 * BK, s0);
-  // lane half h (lane >> 5) supplies k = 16 h + s at MFMA step s (A and B agree)
-  const int lr = lane & 31, lk = lane >> 5;
-  const int arow0 = wr * 32 * WM, bcol0 = wc * 32 * WN;
   int st = 0;
   for (int t = 0; t < ntiles; ++t) {
     // retire tile t.  With 3 stages tile t+1 is in flight (issued one iteration earlier) and
@@ -358,6 +464,10 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
       } else {
 #pragma unroll
         for (int c = 0; c < 4; ++c) v4[c] = bs[(lk * 16 + q * 4 + c) * BN + n];
+      }
+      if (ones_tile && tc.n0 + n == g.nload) {  // column-sum column: B = 1 (A is 0 past K)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v4[c] = 1.f;
       }
     };
     if constexpr (BF) {
@@ -408,29 +518,41 @@ __device__ __forceinline__ void gemm_glds_body(const GemmK& gin) {
     }
     st = st == NS - 1 ? 0 : st + 1;
   }
+  };
+  if constexpr (KCAT) {
+    // K-concatenated segments (a separate instantiation: the runtime descriptor choice costs
+    // the plain kernel about twice the VGPRs)
+    const int nseg = (int)group_word(gv, 0);
+    for (int p = 0; p < nseg; ++p) {
+      if (p) __syncthreads();  // every wave is done with the LDS stages before the next segment's DMA
+      kseg(p ? pick(gv, p) : g);
+    }
+  } else {
+    kseg(g);
+  }
   gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmK g) {
-  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>(g);
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmG g) {
+  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
 }
 // same code under a second name: the GEMM a profile reports as "the hot kernel" (Gemm::hot)
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
-__global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmK g) {
-  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>(g);
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
+__global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmG g) {
+  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
 }
 }  // namespace
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF>
-void launch_one(const GemmK& k, dim3 grid, bool hot, hipStream_t st) {
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
+void launch_one(const GemmG& k, dim3 grid, bool hot, hipStream_t st) {
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   // the "hot" name exists for the one GEMM it tags (pre_conv forward: 64x64, single-level k, fp32)
-  constexpr bool HOT_OK = WGM == 2 && WGN == 2 && WM == 1 && WN == 1 && !KTWO && !BF;
-  const size_t lds = (size_t)k.nstage * (BM + BN) * 32 * sizeof(float);
-  auto ker = gemm_f32_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>;
+  constexpr bool HOT_OK = WGM == 2 && WGN == 2 && WM == 1 && WN == 1 && !KTWO && !BF && !KCAT;
+  const size_t lds = (size_t)k.k[0].nstage * (BM + BN) * 32 * sizeof(float);
+  auto ker = gemm_f32_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>;
   if constexpr (HOT_OK) {
-    if (hot) ker = gemm_f32_hot_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF>;
+    if (hot) ker = gemm_f32_hot_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>;
   }
   if (lds > 65536) {  // above the default dynamic-LDS limit: opt in once per kernel
     static bool set[2] = {false, false};
@@ -444,14 +566,18 @@ void launch_one(const GemmK& k, dim3 grid, bool hot, hipStream_t st) {
   hipLaunchKernelGGL(ker, grid, dim3(256), lds, st, k);
 }
 
+// the K-concatenated form exists for one configuration (the GTU transposed convolutions:
+// 128x32 tiles, single-level k maps, both operands k-/n-contiguous with 16-B DMA)
+constexpr bool kcat_supported(int wgm, int wgn, int wm, int wn, bool ktwo) {
+  return wgm == 4 && wgn == 1 && wm == 1 && wn == 1 && !ktwo;
+}
 template <int WGM, int WGN, int WM, int WN, bool KTWO, bool BF>
-void launch_cfg(const GemmK& k, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {
-  constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
-  GemmK kk = k;
-  kk.tiles_m = (uint32_t)cdiv64(k.M, BM);
-  kk.tiles_n = (uint32_t)cdiv64(k.N, BN);
-  kk.n_fast = (int64_t)k.M >= (int64_t)k.N ? 1u : 0u;  // A (M x K) is the bigger operand
-  const dim3 grid((unsigned)((int64_t)kk.tiles_m * kk.tiles_n * k.batch * k.splitk));
+void launch_cfg(const GemmG& kk, dim3 grid, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {
+  if (kk.start[0] > 0) {  // K-concatenated (run_gemm_kcat checked kcat_ok)
+    if constexpr (kcat_supported(WGM, WGN, WM, WN, KTWO))
+      launch_one<WGM, WGN, WM, WN, true, true, KTWO, 4, 4, BF, true>(kk, grid, false, st);
+    return;
+  }
 #define DS_V(AK, BN_)                                                                                        \
   if (va == 4 && vb == 4)  launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4, BF>(kk, grid, hot, st);              \
   else if (va == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1, BF>(kk, grid, hot, st);              \
@@ -466,20 +592,20 @@ void launch_cfg(const GemmK& k, bool akc, bool bnc, int va, int vb, bool hot, hi
 
 // one explicit instantiation per unit (gemm_c*_k*.hip)
 #define DS_GEMM_UNIT(NAME, WGM, WGN, WM, WN, KTWO, BF)                                                   \
-  void NAME(const GemmK& k, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {              \
-    launch_cfg<WGM, WGN, WM, WN, KTWO, BF>(k, akc, bnc, va, vb, hot, st);                                \
+  void NAME(const GemmG& k, dim3 grid, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {  \
+    launch_cfg<WGM, WGN, WM, WN, KTWO, BF>(k, grid, akc, bnc, va, vb, hot, st);                          \
   }
-void gemm_c0_k0(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c0_k1(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c1_k0(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c1_k1(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c2_k0(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c2_k1(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c0_k0_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c0_k1_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c1_k0_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c1_k1_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c2_k0_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
-void gemm_c2_k1_bf(const GemmK&, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k0(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k1(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c1_k0(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c1_k1(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k0(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k1(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k0_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k1_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c1_k0_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c1_k1_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k0_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k1_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 
 }  // namespace dsgemm

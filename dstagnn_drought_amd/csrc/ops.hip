@@ -555,41 +555,72 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd a) {
   }
 }
 
-template <int VPT>
+// PART: gamma / beta gradient partial sums per workgroup instead of per-element contribution
+// tensors: a wave takes kLnRowsPerWave consecutive rows, keeps the sums over them in
+// registers, and the 4 waves combine through LDS into one row of the (blocks, L) slabs
+// gpart / bpart (reduced over blocks by a column sum afterwards).  Cuts the (R, L) contribution
+// write and its re-read.
+template <int VPT, bool PART>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.R) return;
-  const float mean = a.mu[row], rs = a.rs[row];
-  const int64_t yo = ioff(a.dyrow, row);
-  float dyv[VPT], xh[VPT];
-  float s1 = 0.f, s2 = 0.f;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int RPW = PART ? kLnRowsPerWave : 1;
+  float gp[VPT], bp[VPT];
 #pragma unroll
-  for (int q = 0; q < VPT; ++q) {
-    int e = lane + 64 * q;
-    dyv[q] = 0.f; xh[q] = 0.f;
-    if (e < a.L) {
-      float dy = a.dy[yo + (int64_t)e * a.dyes];
-      if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * a.L + e, a.drop_p);
-      float x = (a.u[(int64_t)row * a.L + e] - mean) * rs;
-      dyv[q] = dy; xh[q] = x;
-      float dxh = dy * a.g[e];
-      s1 += dxh; s2 += dxh * x;
-      if (a.gcontrib) a.gcontrib[(int64_t)row * a.L + e] = dy * x;
-      if (a.bcontrib) a.bcontrib[(int64_t)row * a.L + e] = dy;
+  for (int q = 0; q < VPT; ++q) { gp[q] = 0.f; bp[q] = 0.f; }
+  for (int i = 0; i < RPW; ++i) {
+    const int row = (blockIdx.x * 4 + wv) * RPW + i;
+    if (row >= a.R) break;  // wave-uniform
+    const float mean = a.mu[row], rs = a.rs[row];
+    const int64_t yo = ioff(a.dyrow, row);
+    float dyv[VPT], xh[VPT];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      int e = lane + 64 * q;
+      dyv[q] = 0.f; xh[q] = 0.f;
+      if (e < a.L) {
+        float dy = a.dy[yo + (int64_t)e * a.dyes];
+        if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * a.L + e, a.drop_p);
+        float x = (a.u[(int64_t)row * a.L + e] - mean) * rs;
+        dyv[q] = dy; xh[q] = x;
+        float dxh = dy * a.g[e];
+        s1 += dxh; s2 += dxh * x;
+        if (PART) {
+          gp[q] += dy * x;
+          bp[q] += dy;
+        } else {
+          if (a.gcontrib) a.gcontrib[(int64_t)row * a.L + e] = dy * x;
+          if (a.bcontrib) a.bcontrib[(int64_t)row * a.L + e] = dy;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / a.L;
+    s2 = wave_sum(s2) / a.L;
+    const int64_t xo = ioff(a.dxrow, row);
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      int e = lane + 64 * q;
+      if (e < a.L) {
+        float dx = rs * (dyv[q] * a.g[e] - s1 - xh[q] * s2);
+        int64_t oo = xo + (int64_t)e * a.dxes;
+        if (a.beta != 0.f) dx += a.beta * a.dx[oo];
+        a.dx[oo] = dx;
+      }
     }
   }
-  s1 = wave_sum(s1) / a.L;
-  s2 = wave_sum(s2) / a.L;
-  const int64_t xo = ioff(a.dxrow, row);
+  if constexpr (PART) {
+    __shared__ float red[2][4][64 * VPT];
 #pragma unroll
-  for (int q = 0; q < VPT; ++q) {
-    int e = lane + 64 * q;
-    if (e < a.L) {
-      float dx = rs * (dyv[q] * a.g[e] - s1 - xh[q] * s2);
-      int64_t oo = xo + (int64_t)e * a.dxes;
-      if (a.beta != 0.f) dx += a.beta * a.dx[oo];
-      a.dx[oo] = dx;
+    for (int q = 0; q < VPT; ++q) {
+      red[0][wv][lane + 64 * q] = gp[q];
+      red[1][wv][lane + 64 * q] = bp[q];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < a.L; e += 256) {
+      const float g = red[0][0][e] + red[0][1][e] + red[0][2][e] + red[0][3][e];
+      const float b = red[1][0][e] + red[1][1][e] + red[1][2][e] + red[1][3][e];
+      if (a.gpart) a.gpart[(int64_t)blockIdx.x * a.L + e] = g;
+      if (a.bpart) a.bpart[(int64_t)blockIdx.x * a.L + e] = b;
     }
   }
 }
@@ -823,16 +854,29 @@ __global__ __launch_bounds__(256) void colsum2d_kernel(Colsum2dArgs a) {
 }
 
 // out[a][i] = beta*out + sum_m in[a][m][i]; grid (i blocks, a)
+// out[a][i] = beta*out[a][i] + sum_m in[a][m][i]: a workgroup owns 32 consecutive i of one a;
+// its 8 wave-quarters sum interleaved m (8-way parallel chains per output instead of one
+// Mm-long chain), combined through LDS in a fixed order.
 __global__ __launch_bounds__(256) void sum_middle_kernel(const float* __restrict__ in, int64_t A, int Mm, int64_t I,
                                                          float* __restrict__ out, float beta) {
+  __shared__ float red[8][33];
   const int64_t a = blockIdx.y;
+  const int il = threadIdx.x & 31, mg = threadIdx.x >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 32 + il;
   const float* src = in + a * Mm * I;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < I; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
+  float s = 0.f;
+  if (i < I) {
 #pragma unroll 4
-    for (int m = 0; m < Mm; ++m) s += src[(int64_t)m * I + i];
+    for (int m = mg; m < Mm; m += 8) s += src[(int64_t)m * I + i];
+  }
+  red[mg][il] = s;
+  __syncthreads();
+  if (mg == 0 && i < I) {
+    float t = red[0][il];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) t += red[g][il];
     float* d = out + a * I + i;
-    *d = (beta != 0.f ? beta * *d : 0.f) + s;
+    *d = (beta != 0.f ? beta * *d : 0.f) + t;
   }
 }
 
@@ -1225,14 +1269,25 @@ int op_ln_fwd(const LnFwd& a, hipStream_t st) {
 }
 
 int op_ln_bwd(const LnBwd& a, hipStream_t st) {
-  dim3 grid((unsigned)cdiv64(a.R, 4));
   int vpt = (int)cdiv64(a.L, 64);
-  if (vpt <= 1) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 2) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 4) hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 8) hipLaunchKernelGGL(ln_bwd_kernel<8>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 16) hipLaunchKernelGGL(ln_bwd_kernel<16>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 64) hipLaunchKernelGGL(ln_bwd_kernel<64>, grid, dim3(256), 0, st, a);
+  if (a.gpart || a.bpart) {
+    if (!ln_bwd_partials_ok(a.L)) { set_last_error("ln_bwd: partial slabs need L <= 1024"); return DSTAGNN_E_SHAPE; }
+    dim3 grid((unsigned)ln_bwd_part_blocks(a.R));
+    if (vpt <= 1) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, st, a);
+    else if (vpt <= 2) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, st, a);
+    else if (vpt <= 4) hipLaunchKernelGGL((ln_bwd_kernel<4, true>), grid, dim3(256), 0, st, a);
+    else if (vpt <= 8) hipLaunchKernelGGL((ln_bwd_kernel<8, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((ln_bwd_kernel<16, true>), grid, dim3(256), 0, st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
+  dim3 grid((unsigned)cdiv64(a.R, 4));
+  if (vpt <= 1) hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(256), 0, st, a);
+  else if (vpt <= 2) hipLaunchKernelGGL((ln_bwd_kernel<2, false>), grid, dim3(256), 0, st, a);
+  else if (vpt <= 4) hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, st, a);
+  else if (vpt <= 8) hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, st, a);
+  else if (vpt <= 16) hipLaunchKernelGGL((ln_bwd_kernel<16, false>), grid, dim3(256), 0, st, a);
+  else if (vpt <= 64) hipLaunchKernelGGL((ln_bwd_kernel<64, false>), grid, dim3(256), 0, st, a);
   else { set_last_error("ln_bwd: row too long"); return DSTAGNN_E_SHAPE; }
   DS_CHECK_LAUNCH();
   return 0;
@@ -1297,8 +1352,9 @@ int op_colsum(const float* in, int64_t A, int O, int I, float* out, int64_t ostr
 int op_sum_middle(const float* in, int64_t A, int Mm, int64_t I, float* out, float beta, hipStream_t st) {
   if (A <= 0 || I <= 0) return 0;
   if (A > 65535) { set_last_error("sum_middle: A > 65535"); return DSTAGNN_E_SHAPE; }
-  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv64(I, 256), std::max<int64_t>(1, 2048 / A)));
-  hipLaunchKernelGGL(sum_middle_kernel, dim3(gx, (unsigned)A), dim3(256), 0, st, in, A, Mm, I, out, beta);
+  if (cdiv64(I, 32) > 0x7fffffff) { set_last_error("sum_middle: I too large"); return DSTAGNN_E_SHAPE; }
+  hipLaunchKernelGGL(sum_middle_kernel, dim3((unsigned)cdiv64(I, 32), (unsigned)A), dim3(256), 0, st, in, A, Mm, I, out,
+                     beta);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -29,7 +29,14 @@ struct LnBwd {
   float* dx = nullptr; Idx2 dxrow; int64_t dxes = 1; float beta = 0.f;
   float* gcontrib = nullptr;    // optional (R, L): dy' * xhat  (gamma grad contributions)
   float* bcontrib = nullptr;    // optional (R, L): dy'         (beta grad contributions)
+  // or (instead of the contribution tensors) per-workgroup partial sums over its rows:
+  // (ln_bwd_part_blocks(R), L) slabs, L <= 1024 (ln_bwd_partials_ok)
+  float* gpart = nullptr;
+  float* bpart = nullptr;
 };
+constexpr int kLnRowsPerWave = 1;  // rows per wave of the partial-slab LN backward (measured: 4 is slower)
+inline int64_t ln_bwd_part_blocks(int64_t R) { return (R + 4 * kLnRowsPerWave - 1) / (4 * kLnRowsPerWave); }
+inline bool ln_bwd_partials_ok(int L) { return L <= 1024; }
 
 struct ChebSm {
   int B = 0, K = 0, N = 0;
