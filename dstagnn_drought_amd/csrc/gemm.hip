@@ -277,13 +277,8 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   static const int env_v = getenv("DSTAGNN_GEMM_DMA16") ? atoi(getenv("DSTAGNN_GEMM_DMA16")) : 1;
   pl.va = env_v ? dma_width(g.A + g.a_off, g.am, g.M, g.ak, g.az, pl.akc) : 1;
   pl.vb = env_v ? dma_width(g.B + g.b_off, g.bn, g.N, g.bk, g.bz, !pl.bnc) : 1;
-  // LDS pipeline depth: 3 stages keep two k-tiles in flight per workgroup (needed when a CU
-  // holds about one workgroup: long split-K reductions); 2 stages cut the workgroup's LDS by a
-  // third, so more workgroups are resident per CU and latency is hidden across workgroups
-  // (measured on the bench step: -1.5 % with 2 stages wherever the grid exceeds the CUs)
-  pl.ns = blocks * splitk > 256 ? 2 : 3;
-  static const int env_ns = getenv("DSTAGNN_GEMM_NS") ? atoi(getenv("DSTAGNN_GEMM_NS")) : 0;
-  if (env_ns == 2 || env_ns == 3) pl.ns = env_ns;
+  // LDS pipeline depth: two stages, compile-time (gemm_glds_body)
+  pl.ns = 2;
   k.nstage = pl.ns;
   if (gemm_log_on()) {
     // one "[gemm]" line per kernel launch (run_gemm_group joins a group's problems with " | ")
@@ -328,10 +323,10 @@ void launch_plans(Plan* const* ps, int n, hipStream_t st) {
 // (else one launch per run of equal configurations), their split-K folds as one grouped
 // reduce.  The problems must not write overlapping outputs.
 int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream_t st) {
-  if (n < 1 || n > kGroupMax) { set_last_error("gemm: 1..3 problems per group"); return DSTAGNN_E_ARG; }
+  if (n < 1 || n > 3) { set_last_error("gemm: 1..3 problems per group"); return DSTAGNN_E_ARG; }
   ProfRec* prec = nullptr;
-  Plan plans[kGroupMax];
-  Plan* live[kGroupMax];
+  Plan plans[3];
+  Plan* live[3];
   int nl = 0;
   size_t ws_used = 0;
   double flops = 0, bytes = 0;
@@ -358,7 +353,7 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
   }
   for (int i = 0; i < nl;) {
     int j = i + 1;
-    while (j < nl && live[j]->same_kernel(*live[i])) ++j;
+    while (j < nl && j - i < kGroupMax && live[j]->same_kernel(*live[i])) ++j;
     launch_plans(live + i, j - i, st);
     DS_CHECK_LAUNCH();
     if (gemm_log_on()) {
@@ -369,8 +364,8 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
     i = j;
   }
   // split-K folds of every problem that split, as one grouped launch
-  const GemmK* rk[kGroupMax];
-  uint32_t rc[kGroupMax];
+  const GemmK* rk[3];
+  uint32_t rc[3];
   int nr = 0;
   for (int i = 0; i < nl; ++i) {
     const GemmK& k = live[i]->k;
@@ -379,9 +374,9 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
     rc[nr] = (uint32_t)cdiv64((int64_t)k.batch * k.M * k.N, 256 / k.red_g);
     ++nr;
   }
-  if (nr) {
+  for (int i = 0; i < nr; i += kGroupMax) {
     GemmG gg;
-    const uint32_t grid = make_group(rk, rc, nr, &gg);
+    const uint32_t grid = make_group(rk + i, rc + i, std::min(kGroupMax, nr - i), &gg);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, gg);
     DS_CHECK_LAUNCH();
   }
@@ -395,10 +390,10 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
 // the epilogue, C and its maps are problem 0's).  One launch, no split-K, no intermediate C
 // round trips: the GTU transposed convolutions of widths 3, 5, 7 accumulating into one dX.
 int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
-  if (n < 1 || n > kGroupMax) { set_last_error("gemm: 1..3 K segments"); return DSTAGNN_E_ARG; }
+  if (n < 1 || n > 3) { set_last_error("gemm: 1..3 K segments"); return DSTAGNN_E_ARG; }
   const Gemm& g0 = gs[0];
   if (g0.M <= 0 || g0.N <= 0 || g0.batch <= 0) return 0;
-  Plan plans[kGroupMax];
+  Plan plans[3];
   double flops = 0, bytes = 0;
   for (int p = 0; p < n; ++p) {
     const Gemm& g = gs[p];
@@ -408,7 +403,8 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
     }
     DS_TRY(plan_gemm(g, nullptr, 0, &plans[p]));
     const Plan& q0 = plans[0];
-    const bool kcat_ok = q0.best == 2 && !q0.ktwo && q0.akc && q0.bnc && q0.va == 4 && q0.vb == 4;  // kcat_supported
+    const bool kcat_ok = n <= kGroupMax && q0.best == 2 && !q0.ktwo && q0.akc && q0.bnc && q0.va == 4 &&
+                         q0.vb == 4;  // kcat_supported
     if (!kcat_ok || (p && !plans[p].same_kernel(plans[0]))) {
       // different kernels (DMA widths / map kinds): fall back to a chain of launches
       Gemm first = g0, next;

@@ -40,7 +40,10 @@ struct GemmK {
 // (the three GTU convolutions, their three weight gradients): problem p owns workgroups
 // [start[p], start[p+1]); each slice starts at a multiple of 8, so a workgroup's XCD (id % 8)
 // is the same in the slice as in the grid and the XCD-aware tile order holds per problem.
-constexpr int kGroupMax = 3;
+#ifndef DSTAGNN_GEMM_GROUP_MAX
+#define DSTAGNN_GEMM_GROUP_MAX 3
+#endif
+constexpr int kGroupMax = DSTAGNN_GEMM_GROUP_MAX;
 struct GemmG {
   // start[p] (p = 1..3): first workgroup of problem p (the grid size for p >= n).
   // start[0] = 0 for independent problems; = n >= 2 for ONE K-concatenated problem
@@ -89,9 +92,13 @@ __device__ __forceinline__ GemmK pick(const uint32_t (&v)[kGroupVregs], int p) {
     uint32_t w[NK];
     __device__ U() {}
   } u;
-  if (p == 2) pick_problem<2>(v, u.w);
-  else if (p == 1) pick_problem<1>(v, u.w);
-  else pick_problem<0>(v, u.w);
+  if constexpr (kGroupMax >= 3) {
+    if (p == 2) { pick_problem<2>(v, u.w); return u.t; }
+  }
+  if constexpr (kGroupMax >= 2) {
+    if (p == 1) { pick_problem<1>(v, u.w); return u.t; }
+  }
+  pick_problem<0>(v, u.w);
   return u.t;
 }
 // this workgroup's problem, its workgroup index within the problem's slice and the slice size
@@ -323,7 +330,6 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   constexpr int NA = BM * BK / (256 * VA), NB = BN * BK / (256 * VB);  // DMA instructions per thread per k-tile
   constexpr int LA1 = BM * BK / 256, LB1 = BN * BK / 256;              // element DMAs of the partial tile
   static_assert(NA + NB < 64 && LA1 % 4 == 0 && LB1 % 4 == 0, "vmcnt range / DMA batches");
-  extern __shared__ __attribute__((aligned(16))) float gsm[];
 
   uint32_t gv[kGroupVregs];
   load_group_words(gin, gv);
@@ -332,9 +338,11 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   bool idle;
   const TileCoord tc = decode_tile<BM, BN>(g, lbid, lnwg, idle);
   if (idle) return;  // uniform over the workgroup, before any barrier
-  const int NS = g.nstage;  // 2 or 3 LDS stages (dynamic LDS)
-  float* const Asm = gsm;
-  float* const Bsm = gsm + NS * BM * BK;
+  // two LDS stages, compile-time (static LDS: the stage addresses fold into the ds_read /
+  // M0 immediates; a runtime stage count cost ~10 % of the GEMM family, measured)
+  constexpr int NS = 2;
+  __shared__ __attribute__((aligned(16))) float Asm[NS * BM * BK];
+  __shared__ __attribute__((aligned(16))) float Bsm[NS * BN * BK];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WGN, wc = wid % WGN;
@@ -435,11 +443,16 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
     if (s0 < ntiles) issue(kbeg + s0 * BK, s0);
   int st = 0;
   for (int t = 0; t < ntiles; ++t) {
-    // retire tile t.  With 3 stages tile t+1 is in flight (issued one iteration earlier) and
-    // stays so: NA + NB is the DMA count of a full tile, and a younger partial tile has more,
-    // so the count can only over-wait.  With 2 stages nothing younger is in flight.
-    if (NS >= 3 && t + 1 < ntiles) wait_vm_barrier<NA + NB>();
-    else wait_vm_barrier<0>();
+    // retire tile t: with two stages nothing younger is in flight
+    wait_vm_barrier<0>();
+    if (ones_tile) {
+      // column-sum column: B = 1 in this stage's image (A is 0 past K); written after the
+      // DMA landed, read after one more barrier (only the tile column that holds it pays)
+      float* bst = Bsm + st * BN * BK;
+      const int c = g.nload - tc.n0;
+      if (tid < BK) bst[B_NC ? tid * BN + c : c * BK + tid] = 1.f;
+      __syncthreads();
+    }
     if (t + NS - 1 < ntiles) issue(kbeg + (t + NS - 1) * BK, st == 0 ? NS - 1 : st - 1);
     const float* as = Asm + st * BM * BK;
     const float* bs = Bsm + st * BN * BK;
@@ -464,10 +477,6 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
       } else {
 #pragma unroll
         for (int c = 0; c < 4; ++c) v4[c] = bs[(lk * 16 + q * 4 + c) * BN + n];
-      }
-      if (ones_tile && tc.n0 + n == g.nload) {  // column-sum column: B = 1 (A is 0 past K)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v4[c] = 1.f;
       }
     };
     if constexpr (BF) {
@@ -500,21 +509,25 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     } else {
+      // every fragment of the k-tile first (ds_reads complete in order: the MFMAs of step q
+      // wait only for step q's reads), then the 16 MFMAs per accumulator
+      float av[BK / 8][WM][4], bv[BK / 8][WN][4];
 #pragma unroll
       for (int q = 0; q < BK / 8; ++q) {
-        float av[WM][4], bv[WN][4];
 #pragma unroll
-        for (int i = 0; i < WM; ++i) read_a(i, q, av[i]);
+        for (int i = 0; i < WM; ++i) read_a(i, q, av[q][i]);
 #pragma unroll
-        for (int j = 0; j < WN; ++j) read_b(j, q, bv[j]);
+        for (int j = 0; j < WN; ++j) read_b(j, q, bv[q][j]);
+      }
+#pragma unroll
+      for (int q = 0; q < BK / 8; ++q)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
           for (int i = 0; i < WM; ++i)
 #pragma unroll
             for (int j = 0; j < WN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][c], bv[j][c], acc[i][j], 0, 0, 0);
-      }
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q][i][c], bv[q][j][c], acc[i][j], 0, 0, 0);
     }
     st = st == NS - 1 ? 0 : st + 1;
   }
@@ -534,36 +547,25 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
 }
 
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmG g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void gemm_f32_kernel(GemmG g) {
   gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
 }
 // same code under a second name: the GEMM a profile reports as "the hot kernel" (Gemm::hot)
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
-__global__ __launch_bounds__(256) void gemm_f32_hot_kernel(GemmG g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void gemm_f32_hot_kernel(GemmG g) {
   gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
 }
 }  // namespace
 
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
 void launch_one(const GemmG& k, dim3 grid, bool hot, hipStream_t st) {
-  constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   // the "hot" name exists for the one GEMM it tags (pre_conv forward: 64x64, single-level k, fp32)
   constexpr bool HOT_OK = WGM == 2 && WGN == 2 && WM == 1 && WN == 1 && !KTWO && !BF && !KCAT;
-  const size_t lds = (size_t)k.k[0].nstage * (BM + BN) * 32 * sizeof(float);
   auto ker = gemm_f32_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>;
   if constexpr (HOT_OK) {
     if (hot) ker = gemm_f32_hot_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>;
   }
-  if (lds > 65536) {  // above the default dynamic-LDS limit: opt in once per kernel
-    static bool set[2] = {false, false};
-    const int h = HOT_OK && hot ? 1 : 0;
-    if (!set[h]) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ker), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(3 * (BM + BN) * 32 * sizeof(float)));
-      set[h] = true;
-    }
-  }
-  hipLaunchKernelGGL(ker, grid, dim3(256), lds, st, k);
+  hipLaunchKernelGGL(ker, grid, dim3(256), 0, st, k);
 }
 
 // the K-concatenated form exists for one configuration (the GTU transposed convolutions:
