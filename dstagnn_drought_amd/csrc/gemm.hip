@@ -274,9 +274,10 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   pl.bnc = !g.bn.two && g.bn.s0 == 1;
   pl.ktwo = g.ak.two || g.bk.two;
   pl.hot = g.hot != 0;
-  static const int env_v = getenv("DSTAGNN_GEMM_DMA16") ? atoi(getenv("DSTAGNN_GEMM_DMA16")) : 1;
-  pl.va = env_v ? dma_width(g.A + g.a_off, g.am, g.M, g.ak, g.az, pl.akc) : 1;
-  pl.vb = env_v ? dma_width(g.B + g.b_off, g.bn, g.N, g.bk, g.bz, !pl.bnc) : 1;
+  // DSTAGNN_GEMM_DMA16: bit 0 allows the 16-B DMA for A, bit 1 for B (default both)
+  static const int env_v = getenv("DSTAGNN_GEMM_DMA16") ? atoi(getenv("DSTAGNN_GEMM_DMA16")) : 3;
+  pl.va = (env_v & 1) ? dma_width(g.A + g.a_off, g.am, g.M, g.ak, g.az, pl.akc) : 1;
+  pl.vb = (env_v & 2) ? dma_width(g.B + g.b_off, g.bn, g.N, g.bk, g.bz, !pl.bnc) : 1;
   // LDS pipeline depth: two stages, compile-time (gemm_glds_body)
   pl.ns = 2;
   k.nstage = pl.ns;

@@ -418,21 +418,24 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
                       sb + 4 * (256 * j + 64 * wid));
       }
     } else {  // partial tile: element by element, zeros past kend
+      // (from the loop-invariant start of the last tile, not k0: with k0 the compiler keeps
+      // every element's k as an induction variable, +32 VALU adds per k-tile iteration)
+      const int kt = kbeg + (kend - kbeg - 1) / BK * BK;
 #pragma unroll
       for (int j = 0; j < LA1; ++j) {
         int row, k;
         img_rk<BM, A_KC>(256 * j + 64 * wid + lane, row, k);
         const int m = tc.m0 + row;
-        const uint32_t o = (uint32_t)g.abias + (m < g.M ? (uint32_t)koff(g.am, m) : 0u) + (uint32_t)koff(g.ak, k0 + k);
-        glds_vaddr(k0 + k < kend ? gp(A, o) : (const void*)g_zero_page, sa + 4 * (256 * j + 64 * wid));
+        const uint32_t o = (uint32_t)g.abias + (m < g.M ? (uint32_t)koff(g.am, m) : 0u) + (uint32_t)koff(g.ak, kt + k);
+        glds_vaddr(kt + k < kend ? gp(A, o) : (const void*)g_zero_page, sa + 4 * (256 * j + 64 * wid));
       }
 #pragma unroll
       for (int j = 0; j < LB1; ++j) {
         int col, k;
         img_rk<BN, !B_NC>(256 * j + 64 * wid + lane, col, k);
         const int n = tc.n0 + col;
-        const uint32_t o = (uint32_t)g.bbias + (n < g.nload ? (uint32_t)koff(g.bn, n) : 0u) + (uint32_t)koff(g.bk, k0 + k);
-        glds_vaddr(k0 + k < kend ? gp(Bp, o) : (const void*)g_zero_page, sb + 4 * (256 * j + 64 * wid));
+        const uint32_t o = (uint32_t)g.bbias + (n < g.nload ? (uint32_t)koff(g.bn, n) : 0u) + (uint32_t)koff(g.bk, kt + k);
+        glds_vaddr(kt + k < kend ? gp(Bp, o) : (const void*)g_zero_page, sb + 4 * (256 * j + 64 * wid));
       }
     }
   };
@@ -528,6 +531,17 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
 #pragma unroll
             for (int j = 0; j < WN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q][i][c], bv[q][j][c], acc[i][j], 0, 0, 0);
+      // software-pipeline the k-tile by one step: the reads of steps 0 and 1, then the MFMAs of
+      // step q beside the reads of step q + 2 (DS reads per step: b128 per row-major operand,
+      // two read2 pairs per column-major one)
+      constexpr int DSQ = (A_KC ? WM : 2 * WM) + (!B_NC ? WN : 2 * WN);
+      constexpr int MFQ = 4 * WM * WN;
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * DSQ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, MFQ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, DSQ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, MFQ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, DSQ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * MFQ, 0);
     }
     st = st == NS - 1 ? 0 : st + 1;
   }
