@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
     # spec = <tile config | auto>:<LDS pipeline stages: 2, 3, or auto>
-    ap.add_argument("--configs", default="auto:auto,auto:2,auto:3,0:2,0:3,1:3,2:3,3:2,3:3,4:3")
+    ap.add_argument("--configs", default="auto:auto,0:2,1:2,2:2")
     ap.add_argument("--only", default=None)
     ap.add_argument("--big", action="store_true", help="add large square steady-state probes")
     ap.add_argument("--large", action="store_true", help="add the GAMBIA / SYN large-M shapes")
