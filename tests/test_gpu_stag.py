@@ -202,3 +202,53 @@ def test_fast_process_dataset(dev, tmp_path):
     np.testing.assert_allclose(sta, s0, rtol=0, atol=1e-10)
     check_topk(A, R, sta, 6, lambda i: 1 - sta[i], sta)
     assert os.path.exists(tmp_path / "stag_001_SMALL.csv") and os.path.exists(tmp_path / "strg_001_SMALL.csv")
+
+
+# ---------------------------------------------------------------------------------------
+# fast_STAG_gen PCA at the reference's own sizes (data/fast_STAG_gen.py:42-45 calls
+# sklearn.decomposition.PCA(n_components=12).fit_transform on the (N, T*F) node matrix).
+# The device path is an exact SVD; sklearn is importable here, so the reduced data are pinned
+# against it at N = 2139 (GAMBIA, T=287, F=4 as the reference's comment) and N = 4096:
+#   svd_solver="full"          components equal up to sign, 1e-10 x scale
+#   default (randomized) solver the same bound (random_state fixed; the reference leaves it
+#                               None; with this decaying spectrum its power iterations converge
+#                               to ~4e-15, numpy check), and the top-k graph built from either
+#                               is identical
+# Inputs: a seeded low-rank signal (24 components, decaying spectrum) plus noise.
+# ---------------------------------------------------------------------------------------
+def _pca_case(N, T=287, F=4, seed=11):
+    rng = np.random.default_rng(seed)
+    r = 24
+    basis = rng.standard_normal((r, T * F))
+    w = rng.standard_normal((N, r)) * (0.7 ** np.arange(r))[None, :] * 10.0
+    X = w @ basis + 0.05 * rng.standard_normal((N, T * F))
+    return X.reshape(N, T, F).transpose(1, 0, 2).copy()  # (T, N, F) as the reference's file
+
+
+def _align(a, b):
+    """a's columns sign-flipped to match b's."""
+    s = np.sign(np.sum(a * b, axis=0))
+    s[s == 0] = 1
+    return a * s[None, :]
+
+
+@pytest.mark.parametrize("N", [2139, 4096])
+def test_fast_pca_vs_sklearn(dev, N):
+    from sklearn.decomposition import PCA
+    from dstagnn_drought_amd import fast_stag_gen as fsg
+    data = _pca_case(N)
+    X = data.transpose(1, 0, 2).reshape(N, -1)
+    ours = fsg.pca_reduce(data, 12, device=dev).cpu().numpy()
+    full = PCA(n_components=12, svd_solver="full").fit_transform(X)
+    rand = PCA(n_components=12, random_state=0).fit_transform(X)
+    scale = float(np.abs(full).max())
+    assert np.abs(_align(ours, full) - full).max() <= 1e-10 * scale
+    assert np.abs(_align(ours, rand) - rand).max() <= 1e-10 * scale
+    # the graph the reference builds from its reduced data = the one built from ours
+    coords = np.arange(N, dtype=np.float64)
+    k = max(1, int(N * 0.01))
+    A_ours = fsg.adjacency(fsg.distances_device(coords, ours, device=dev), 0.01, device=dev)[0]
+    A_rand = fsg.adjacency(fsg.distances_device(coords, rand, device=dev), 0.01, device=dev)[0]
+    A_ours, A_rand = (t.cpu().numpy() if torch.is_tensor(t) else np.asarray(t) for t in (A_ours, A_rand))
+    assert int(A_ours.sum()) == N * k
+    assert np.array_equal(A_ours, A_rand)
