@@ -472,6 +472,8 @@ struct Fwd {
   hipStream_t st;
   Streams ks;
   bool params_forked = false;
+  bool e_side = false;           // E = x transposed is issued on the side stream (event e_ready)
+  hipEvent_t e_ready = nullptr;
   ChebFl fl;
 
   int stage_tat() {
@@ -487,7 +489,7 @@ struct Fwd {
       a.y = s.E; a.yrow = idx1(N); a.yes = 1;
       a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et;
       DS_TRY(op_ln_fwd(a, st));
-    } else {
+    } else if (!e_side) {
       DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, N * m.FT, m.FT * N, 0.f, st));
     }
     // Q | K | V projections (MultiHeadAttention :92-94) as ONE GEMM over the stacked weights
@@ -495,7 +497,11 @@ struct Fwd {
     {
       Gemm g;
       g.M = (int)m.BFT; g.N = (int)m.QW; g.K = m.N;
-      g.A = s.E; g.am = idx1(N); g.ak = idx1(1);
+      if (m.first) {
+        g.A = s.E; g.am = idx1(N); g.ak = idx1(1);
+      } else {  // straight from x (B,N,F,T): rows (b,(f,t)) contiguous in (f,t) -> 16-B DMA
+        g.A = x; g.am = idx2(m.FT, 1, N * m.FT); g.ak = idx1(m.FT);
+      }
       g.B = s.Wqkv; g.bk = idx1(1); g.bn = idx1(N);
       g.C = s.qkv; g.cm = idx1(m.QW); g.cn = idx1(1);
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
@@ -511,6 +517,10 @@ struct Fwd {
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
     // LN_N(fc + E) (:100)
+    if (e_side) {
+      const hipError_t r = hipStreamWaitEvent(st, e_ready, 0);
+      if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
+    }
     {
       LnFwd a;
       a.R = (int)m.BFT; a.L = m.N;
@@ -652,6 +662,14 @@ struct Fwd {
     ChebIO c = cheb_io();
     if (split) {  // x Theta needs only x and Theta: it runs beside the whole attention chain
       DS_TRY(ks.fork());
+      if (!m.first) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
+        DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, (int64_t)m.N * m.FT, m.FT * m.N, 0.f, ks.sd));
+        e_ready = ks.ss->ev[ks.ss->next];
+        ks.ss->next = (ks.ss->next + 1) % 64;
+        const hipError_t r = hipEventRecord(e_ready, ks.sd);
+        if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
+        e_side = true;
+      }
       DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
     }
     DS_TRY(stage_tat());
