@@ -1022,22 +1022,6 @@ struct Bwd {
       g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
       DS_TRY(sgemm(g));
     }
-    if (gd.tat_wq || gd.tat_wk || gd.tat_wv) {  // [dWq; dWk; dWv] = dqkv^T E
-      Gemm g;
-      g.M = (int)m.QW; g.N = m.N; g.K = (int)m.BFT;
-      g.A = w.dqkv; g.am = idx1(1); g.ak = idx1(m.QW);
-      g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
-      const bool adjacent = gd.tat_wq && gd.tat_wk == gd.tat_wq + m.HQ * N && gd.tat_wv == gd.tat_wk + m.HQ * N;
-      g.C = adjacent ? gd.tat_wq : w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
-      DS_TRY(sgemm(g));
-      if (!adjacent) {
-        PackRows pk;
-        pk.n = 3; pk.cols = m.N; pk.unpack = 1;
-        pk.src[0] = w.dWqkv; pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
-        pk.dst[0] = gd.tat_wq; pk.dst[1] = gd.tat_wk; pk.dst[2] = gd.tat_wv;
-        DS_TRY(op_pack_rows(pk, sd));
-      }
-    }
     {  // dE = dU + dqkv [Wq; Wk; Wv]
       Gemm g;
       g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.QW;
@@ -1072,6 +1056,30 @@ struct Bwd {
     return 0;
   }
 
+  // [dWq; dWk; dWv] = dqkv^T E — the last product of the backward, issued on the main
+  // stream after dx: the side stream is still busy with the earlier parameter gradients
+  // (pre_conv, SAt), while the main chain has nothing left (measured: the side stream's tail
+  // was the step's critical path)
+  int tat_wqkv_grad() {
+    if (!(gd.tat_wq || gd.tat_wk || gd.tat_wv)) return 0;
+    const int64_t N = m.N;
+    Gemm g;
+    g.M = (int)m.QW; g.N = m.N; g.K = (int)m.BFT;
+    g.A = w.dqkv; g.am = idx1(1); g.ak = idx1(m.QW);
+    g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
+    const bool adjacent = gd.tat_wq && gd.tat_wk == gd.tat_wq + m.HQ * N && gd.tat_wv == gd.tat_wk + m.HQ * N;
+    g.C = adjacent ? gd.tat_wq : w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
+    DS_TRY(gemm(g));
+    if (!adjacent) {
+      PackRows pk;
+      pk.n = 3; pk.cols = m.N; pk.unpack = 1;
+      pk.src[0] = w.dWqkv; pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
+      pk.dst[0] = gd.tat_wq; pk.dst[1] = gd.tat_wk; pk.dst[2] = gd.tat_wv;
+      DS_TRY(op_pack_rows(pk, st));
+    }
+    return 0;
+  }
+
   int run() {
     static const bool prof = getenv("DSTAGNN_HOST_PROFILE") != nullptr;
     HostTimer ht(prof, "bwd");
@@ -1088,6 +1096,7 @@ struct Bwd {
     ht.lap("preconv");
     DS_TRY(stage_tat());
     ht.lap("tat");
+    DS_TRY(tat_wqkv_grad());
     DS_TRY(join());
     ht.lap("join");
     return 0;
