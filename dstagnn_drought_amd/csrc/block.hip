@@ -720,6 +720,22 @@ struct Bwd {
   }
   int fork() { return ks.fork(); }
   int join() { return ks.join(); }
+  // an event on the side stream that the main stream can wait for later (wait_side)
+  hipEvent_t dx_ready = nullptr;
+  int mark_side(hipEvent_t* ev) {
+    if (sd == st) { *ev = nullptr; return 0; }
+    *ev = ks.ss->ev[ks.ss->next];
+    ks.ss->next = (ks.ss->next + 1) % 64;
+    const hipError_t r = hipEventRecord(*ev, sd);
+    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
+    return 0;
+  }
+  int wait_side(hipEvent_t ev) {
+    if (!ev) return 0;
+    const hipError_t r = hipStreamWaitEvent(st, ev, 0);
+    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
+    return 0;
+  }
 
   // TAt LayerNorm backward: gamma / beta partial slabs (both fit in the (BFT, N) gcon_a)
   bool tat_part() const { return ln_bwd_partials_ok(m.N) && 2 * ln_bwd_part_blocks(m.BFT) <= m.BFT; }
@@ -825,8 +841,11 @@ struct Bwd {
       if (m.flash) {  // T o P and dW compact on the support
         sp.nnz = (int)m.nnz; sp.wsupp = s.wsupp; sp.dws = w.dws; sp.csr2csc = gr.csr2csc;
       }
+      // dxth = W^T g on the side stream (only the Theta / x gradients, also on the side,
+      // read it), dW = (x Theta) g^T on the support on the main chain: independent products
+      DS_TRY(fork());
+      DS_TRY(op_cheb_spmm_t_bwd(sp, sd));
       DS_TRY(op_cheb_sddmm_bwd(sp, st));
-      DS_TRY(op_cheb_spmm_t_bwd(sp, st));
     } else {
       {
         Gemm g;  // dW[b,k,i,j] = sum_e xth[b,i,t,k,c] g[b,j,e]
@@ -886,7 +905,10 @@ struct Bwd {
       g.B = s.thcat; g.bk = idx1(1); g.bn = idx1(KC);
       g.C = dx; g.cm = idx2(T, 1, FT); g.cn = idx1(T);
       g.beta = 1.f;
-      DS_TRY(gemm(g));
+      // on the side stream: dx is an output, only the TAt stage's final accumulation into it
+      // (main) has to wait for this (event dx_ready), not the main chain in between
+      DS_TRY(sgemm(g));
+      DS_TRY(mark_side(&dx_ready));
     }
     return 0;
   }
@@ -1049,8 +1071,10 @@ struct Bwd {
       if (part) DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.gcon_e + pb * N, gd.embT_b}}, pb, m.N, 1));
       else DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dE, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
       if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sd));
+      DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
       DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
     } else {
+      DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
       DS_TRY(op_transpose(w.dE, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
     }
     return 0;
