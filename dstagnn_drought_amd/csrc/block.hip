@@ -1287,6 +1287,15 @@ int dstagnn_gemm_f32(const dstagnn_gemm_desc* d, void* scratch, size_t scratch_b
   return run_gemm(g, ws, wsf, (hipStream_t)stream);
 }
 
+int dstagnn_colsum(const float* in, int64_t A, int O, int I, float* out, int64_t ostride, float beta, void* scratch,
+                   size_t scratch_bytes, dstagnn_stream_t stream) {
+  if (A < 0 || O < 0 || I <= 0) return DSTAGNN_E_ARG;
+  if (A == 0 || O == 0) return 0;  // empty: out untouched (include/dstagnn.h)
+  if (!in || !out || !scratch) return DSTAGNN_E_ARG;
+  size_t pf = scratch_bytes > 256 ? (scratch_bytes - 256) / sizeof(float) : 0;
+  return op_colsum(in, A, O, I, out, ostride, beta, (float*)align256(scratch), pf, (hipStream_t)stream);
+}
+
 int dstagnn_dropout_mask(const dstagnn_block_dims* d, int which, float* mask, dstagnn_stream_t stream) {
   if (!d || !mask) return DSTAGNN_E_ARG;
   int64_t n = which == 0 ? (int64_t)d->B * d->N * d->d_model : (int64_t)d->B * d->N * d->C * d->T;

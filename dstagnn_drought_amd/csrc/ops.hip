@@ -766,6 +766,13 @@ __device__ __forceinline__ void st_agent(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// consumer side of the hand-off: agent acquire, then wait for the invalidate to complete
+// (the caller's workgroup barrier holds the other waves behind it)
+__device__ __forceinline__ void colsum_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // sum of n <= 32 partial rows p[q*256 + t] in fixed order; all loads issued before the
 // first add (one memory round trip: the sc1 loads are served beyond the XCD's L2)
 __device__ __forceinline__ float sum_partials(const float* p, int n, int t) {
@@ -813,17 +820,23 @@ __global__ __launch_bounds__(256) void colsum2d_kernel(Colsum2dArgs a) {
     if (t < a.E)
       for (int l = 0; l < a.RP; ++l) colv += red[l * a.E + t];
   }
-  // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): sc1 stores,
-  // every storing wave drains them (vmcnt(0)), a barrier, then ONE lane's agent-scope ticket;
-  // the block whose ticket came last reads with sc1 loads.  No fences (a release fence
-  // writes back the XCD's whole L2).
+  // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, "valid forms"): producers
+  // store sc1 (agent-scope relaxed atomics), every storing wave drains them (vmcnt(0)), a
+  // barrier, then ONE lane's agent-scope ticket add.  The block whose add came last issues
+  // an agent-scope ACQUIRE (L1 invalidate, only the winning blocks pay it) before any read
+  // of the partials, so the hand-off does not rest on the measured sc1-load table (whose
+  // row assumes one workgroup per CU).  No release fence on the producers (it would write
+  // back the XCD's whole L2): sc1 stores already bypass it.
   float* p1 = a.part + ((int64_t)gidx * a.R + r) * kCsW;
   if (t < a.W) st_agent(p1 + t, colv);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int c1 = r / kCsL1;
   const int n1 = min(kCsL1, a.R - c1 * kCsL1);
-  if (t == 0) last = atomicAdd(a.cnt + (int64_t)gidx * a.R2 + c1, 1) == n1 - 1;
+  if (t == 0) {
+    last = atomicAdd(a.cnt + (int64_t)gidx * a.R2 + c1, 1) == n1 - 1;
+    if (last) colsum_acquire();
+  }
   __syncthreads();
   if (!last) return;
   float* p2 = a.part + ((int64_t)a.nsrc * a.G * a.R + (int64_t)gidx * a.R2 + c1) * kCsW;
@@ -834,6 +847,7 @@ __global__ __launch_bounds__(256) void colsum2d_kernel(Colsum2dArgs a) {
   if (t == 0) {
     __hip_atomic_store(a.cnt + (int64_t)gidx * a.R2 + c1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = atomicAdd(cnt2, 1) == a.R2 - 1;
+    if (last) colsum_acquire();
   }
   __syncthreads();
   if (!last) return;

@@ -10,6 +10,7 @@
 //   dstagnn::cheb_sat_fwd/bwd  cheb_conv_withSAt.forward (:117-133) and its gradient
 //   dstagnn::head_fwd/bwd   DSTAGNN_submodule's cat + final_conv + final_fc (:272-280)
 //   dstagnn::gemm_f32       the strided f32-MFMA GEMM (tests / tools)
+//   dstagnn::colsum         the fixed-order column-sum reduction (bias / LayerNorm affine grads; tests)
 //   dstagnn::stag_* / emd_dense / fast_stag_distances / graph_topk   the graph builders
 //                           (data/STAG_gen.py:17-129, data/fast_STAG_gen.py:16-74)
 //
@@ -491,6 +492,19 @@ void gemm_f32(const Tensor& A, const Tensor& B, const Tensor& C, at::IntArrayRef
   check_rc(dstagnn_gemm_f32(&d, ws.data_ptr(), (size_t)ws.numel(), stream_of(C)), "dstagnn_gemm_f32");
 }
 
+// column sums: out[o] = sum_{a, i} in[a][o][i] over in viewed as (A, O, I), fixed order
+Tensor colsum(const Tensor& in, int64_t O, int64_t I) {
+  check_dev(in, at::kFloat, "in");
+  TORCH_CHECK(O > 0 && I > 0 && in.numel() % (O * I) == 0, "colsum: numel must be a multiple of O*I");
+  c10::DeviceGuard guard(in.device());
+  Tensor out = at::zeros({O}, in.options());  // A = 0 sums to zero (the launcher writes nothing)
+  Tensor ws = bytes((size_t(8) << 20) + 256, in);
+  check_rc(dstagnn_colsum(in.data_ptr<float>(), in.numel() / (O * I), (int)O, (int)I, out.data_ptr<float>(), 1, 0.f,
+                          ws.data_ptr(), (size_t)ws.numel(), stream_of(in)),
+           "dstagnn_colsum");
+  return out;
+}
+
 // -------------------------------------------------------------------------------------
 // model head
 // -------------------------------------------------------------------------------------
@@ -673,6 +687,7 @@ TORCH_LIBRARY(dstagnn, m) {
         "Tensor d_out, int C, bool sparse) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("gemm_f32(Tensor A, Tensor B, Tensor(a!) C, int[] mnkb, int[] maps, int[] offs, float alpha, float beta, "
         "Tensor? bias, int bias_stride, bool relu) -> ()");
+  m.def("colsum(Tensor x, int O, int I) -> Tensor");
   m.def("head_fwd(Tensor[] outs, Tensor w1, Tensor b1, Tensor w2, Tensor b2) -> (Tensor, Tensor)");
   m.def("head_bwd(Tensor[] outs, Tensor w1, Tensor w2, Tensor h, Tensor dy, int[] need) -> Tensor[]");
   m.def("stag_prep(Tensor data) -> (Tensor, Tensor, Tensor)");
@@ -699,6 +714,7 @@ TORCH_LIBRARY_IMPL(dstagnn, CUDA, m) {
   m.impl("cheb_sat_fwd", cheb_sat_fwd);
   m.impl("cheb_sat_bwd", cheb_sat_bwd);
   m.impl("gemm_f32", gemm_f32);
+  m.impl("colsum", colsum);
   m.impl("head_fwd", head_fwd);
   m.impl("head_bwd", head_bwd);
   m.impl("stag_prep", stag_prep);

@@ -203,6 +203,15 @@ typedef struct dstagnn_gemm_desc {
 } dstagnn_gemm_desc;
 int dstagnn_gemm_f32(const dstagnn_gemm_desc* g, void* scratch, size_t scratch_bytes, dstagnn_stream_t stream);
 
+/* Column sums used by every bias / LayerNorm-gamma/beta gradient of the block
+ * (model/DSTAGNN_my.py:207,220,252 -- the autograd reductions of nn.Linear / nn.Conv2d
+ * biases and nn.LayerNorm affine parameters):
+ *   out[o*ostride] = beta*out[o*ostride] + sum_{a<A, i<I} in[(a*O + o)*I + i]
+ * O*I <= 16384; A == 0 leaves out untouched.  Fixed summation order (bit-identical across launches); one launch with
+ * an in-kernel ticketed two-level fold when I <= 256.  scratch >= 8 MB + 256.        */
+int dstagnn_colsum(const float* in, int64_t A, int O, int I, float* out, int64_t ostride, float beta,
+                   void* scratch, size_t scratch_bytes, dstagnn_stream_t stream);
+
 /* Time `iters` back-to-back launches of one block stage with HIP events on
  * `stream`; writes the mean per-launch milliseconds.  stage: 0 = whole forward,
  * 2 = cheb_sat forward stage, 3 = pre_conv stage, 10 = the single kernel the
