@@ -249,7 +249,9 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
 
   // split-K when the grid leaves CUs idle and the reduction is long
   int splitk = 1;
-  if (g.K > 0 && blocks < 128 && g.K >= 512 && ws) {
+  static const int min_grid = getenv("DSTAGNN_SPLITK_MINGRID") ? atoi(getenv("DSTAGNN_SPLITK_MINGRID")) : 128;
+  static const int min_k = getenv("DSTAGNN_SPLITK_MINK") ? atoi(getenv("DSTAGNN_SPLITK_MINK")) : 512;
+  if (g.K > 0 && blocks < min_grid && g.K >= min_k && ws) {
     int want = (int)std::min<int64_t>(512, cdiv64(g_splitk_target, blocks));
     int maxk = g.K / 128;  // keep >= 128 k per split
     splitk = std::max(1, std::min(want, maxk));
