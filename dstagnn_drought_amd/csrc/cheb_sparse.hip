@@ -43,10 +43,22 @@ __device__ __forceinline__ void xth_offsets(const ChebSp& a, int e0, int lane, i
   }
 }
 
+// XCD-aware row-block order: blocks are dealt round-robin over the 8 XCDs (linear block id
+// % 8), so physical block p runs logical row block (p % 8) * (gridDim.x / 8) + p / 8 and each
+// XCD walks one contiguous eighth of the (b, j) rows.  The rows of one batch b then share an
+// XCD, and the neighbour gathers of xth / g (b's K*N*C*T slice, ~0.8 MB at PEMS08) hit that
+// XCD's 4 MB L2 instead of every XCD streaming the whole 25 MB tensor.  gridDim.x is a
+// multiple of 8 (the launcher pads; padded rows exit at the wv bound).
+__device__ __forceinline__ int64_t xcd_row_block() {
+  const int64_t per = gridDim.x >> 3;
+  const int64_t p = blockIdx.x;
+  return (p & 7) * per + (p >> 3);
+}
+
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t wv = xcd_row_block() * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), j = (int)(wv % a.N);
   const int e0 = blockIdx.y * kChunk;
@@ -82,7 +94,7 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t wv = xcd_row_block() * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), j = (int)(wv % a.N);
   const int64_t NN = (int64_t)a.N * a.N;
@@ -144,7 +156,7 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t wv = xcd_row_block() * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), i = (int)(wv % a.N);
   const int e0 = blockIdx.y * kChunk;
@@ -185,7 +197,7 @@ namespace {
 #define DS_NQ_DISPATCH(KER, a, st, CHUNKED)                                                        \
   do {                                                                                             \
     const int nq = (int)cdiv64(std::min((a).CT, kChunk), 64);                                      \
-    const dim3 grid((unsigned)cdiv64((int64_t)(a).B * (a).N, 4),                                   \
+    const dim3 grid((unsigned)(cdiv64(cdiv64((int64_t)(a).B * (a).N, 4), 8) * 8),                   \
                     (CHUNKED) ? (unsigned)cdiv64((a).CT, kChunk) : 1u);                            \
     if (nq <= 1) hipLaunchKernelGGL(KER<1>, grid, dim3(256), 0, st, a);                            \
     else if (nq <= 2) hipLaunchKernelGGL(KER<2>, grid, dim3(256), 0, st, a);                       \
