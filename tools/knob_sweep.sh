@@ -1,6 +1,8 @@
 #!/bin/bash
 # Same-box interleaved A/B of runtime knobs on the PEMS08 bench (ms/step per run).
 # usage: bash tools/knob_sweep.sh "ENV=a" "ENV=b" ...   (each arg: space-separated env assignments, "" = default)
+# A/B of two builds: put the baseline libdstagnn.so in a directory D and pass "LD_LIBRARY_PATH=D"
+# (the operator library _C.so resolves libdstagnn.so by RUNPATH, which LD_LIBRARY_PATH overrides).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
