@@ -48,17 +48,21 @@ __device__ __forceinline__ void xth_offsets(const ChebSp& a, int e0, int lane, i
 // XCD walks one contiguous eighth of the (b, j) rows.  The rows of one batch b then share an
 // XCD, and the neighbour gathers of xth / g (b's K*N*C*T slice, ~0.8 MB at PEMS08) hit that
 // XCD's 4 MB L2 instead of every XCD streaming the whole 25 MB tensor.  gridDim.x is a
-// multiple of 8 (the launcher pads; padded rows exit at the wv bound).
-__device__ __forceinline__ int64_t xcd_row_block() {
-  const int64_t per = gridDim.x >> 3;
+// multiple of 8 (the launcher pads; padded rows exit at the wv bound).  Only when one batch's
+// slice fits an L2 (xcd_order, set by the launcher): at GAMBIA / SYN sizes (63-79 MB per b)
+// eight XCDs on eight different batches would overflow the 256 MB Infinity Cache that the
+// plain order (all XCDs on one batch) stays inside.
+__device__ __forceinline__ int64_t xcd_row_block(int on) {
   const int64_t p = blockIdx.x;
+  if (!on) return p;
+  const int64_t per = gridDim.x >> 3;
   return (p & 7) * per + (p >> 3);
 }
 
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = xcd_row_block() * 4 + (threadIdx.x >> 6);
+  const int64_t wv = xcd_row_block(a.xcd_order) * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), j = (int)(wv % a.N);
   const int e0 = blockIdx.y * kChunk;
@@ -94,7 +98,7 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = xcd_row_block() * 4 + (threadIdx.x >> 6);
+  const int64_t wv = xcd_row_block(a.xcd_order) * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), j = (int)(wv % a.N);
   const int64_t NN = (int64_t)a.N * a.N;
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = xcd_row_block() * 4 + (threadIdx.x >> 6);
+  const int64_t wv = xcd_row_block(a.xcd_order) * 4 + (threadIdx.x >> 6);
   if (wv >= (int64_t)a.B * a.N) return;
   const int b = (int)(wv / a.N), i = (int)(wv % a.N);
   const int e0 = blockIdx.y * kChunk;
@@ -209,19 +213,28 @@ namespace {
     else if (nq <= 16) hipLaunchKernelGGL(KER<16>, grid, dim3(256), 0, st, a);                     \
     else { set_last_error("cheb sparse: bad row length"); return DSTAGNN_E_SHAPE; }               \
   } while (0)
+// XCD-aware order when one batch's gathered slice (xth: N*K*C*T floats) fits a 4 MB L2
+ChebSp with_xcd_order(const ChebSp& a0) {
+  ChebSp a = a0;
+  a.xcd_order = (int64_t)a.N * a.K * a.CT * (int64_t)sizeof(float) <= (int64_t(4) << 20) ? 1 : 0;
+  return a;
+}
 }  // namespace
 
-int op_cheb_spmm_fwd(const ChebSp& a, hipStream_t st) {
+int op_cheb_spmm_fwd(const ChebSp& a0, hipStream_t st) {
+  const ChebSp a = with_xcd_order(a0);
   DS_NQ_DISPATCH(cheb_spmm_fwd_kernel, a, st, true);
   DS_CHECK_LAUNCH();
   return 0;
 }
-int op_cheb_sddmm_bwd(const ChebSp& a, hipStream_t st) {
+int op_cheb_sddmm_bwd(const ChebSp& a0, hipStream_t st) {
+  const ChebSp a = with_xcd_order(a0);
   DS_NQ_DISPATCH(cheb_sddmm_bwd_kernel, a, st, false);
   DS_CHECK_LAUNCH();
   return 0;
 }
-int op_cheb_spmm_t_bwd(const ChebSp& a, hipStream_t st) {
+int op_cheb_spmm_t_bwd(const ChebSp& a0, hipStream_t st) {
+  const ChebSp a = with_xcd_order(a0);
   DS_NQ_DISPATCH(cheb_spmm_t_bwd_kernel, a, st, true);
   DS_CHECK_LAUNCH();
   return 0;

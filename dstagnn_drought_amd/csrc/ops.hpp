@@ -142,6 +142,7 @@ struct ChebSp {
   const float* wsupp = nullptr;  // fwd / spmm_t: replaces T_k[i,j] P[b,k,i,j]
   float* dws = nullptr;          // sddmm: written instead of dW
   const int* csr2csc = nullptr;  // CSR position -> CSC position
+  int xcd_order = 0;             // set by the launcher: XCD-aware row-block order (cheb_sparse.hip)
 };
 bool cheb_sparse_ok(int CT);
 
