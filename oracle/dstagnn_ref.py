@@ -206,14 +206,16 @@ def split_state_dict(sd, nb_block):
     return blocks, final
 
 
-def block_forward_backward(p, x, res_att, cheb, adj_pa, dims, g_out, g_re, hoist=True, relu_mask=None, pre_out=None):
+def block_forward_backward(p, x, res_att, cheb, adj_pa, dims, g_out, g_re, hoist=True, relu_mask=None, pre_out=None,
+                           train=False, drop_masks=None):
     """Forward + autograd backward of one block with upstream grads (g_out, g_re).
     Returns (out, re_at, grad_x, grad_res_att or None, {param_name: grad or None}).
-    relu_mask / pre_out: see cheb_conv_sat."""
+    relu_mask / pre_out: see cheb_conv_sat; train / drop_masks: see block_forward."""
     pp = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
     xx = x.detach().clone().requires_grad_(True)
     ra = res_att.detach().clone().requires_grad_(True) if torch.is_tensor(res_att) else res_att
-    out, re_at = block_forward(pp, xx, ra, cheb, adj_pa, dims, hoist=hoist, relu_mask=relu_mask, pre_out=pre_out)
+    out, re_at = block_forward(pp, xx, ra, cheb, adj_pa, dims, train=train, drop_masks=drop_masks, hoist=hoist,
+                               relu_mask=relu_mask, pre_out=pre_out)
     loss = (out * g_out).sum()
     if g_re is not None:
         loss = loss + (re_at * g_re).sum()

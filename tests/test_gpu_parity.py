@@ -310,9 +310,10 @@ CONFIGS = {
 RELU_EPS = 1e-5  # ReLU decisions may differ from the fp64 oracle's only where |z| <= RELU_EPS * max|z|
 
 
-def hip_cheb_relu_mask(blk, x, res):
+def hip_cheb_relu_mask(blk, x, res, train=False, seed=0):
     """(B,N,C,T) bool: the HIP forward's ReLU decisions at model/DSTAGNN_my.py:133 (X > 0 of
-    the Chebyshev output the forward keeps, dstagnn::block_cheb_out)."""
+    the Chebyshev output the forward keeps, dstagnn::block_cheb_out); train=True with the
+    dropout seed of the run under test (the EmbedS dropout feeds the spatial attention)."""
     from dstagnn_drought_amd import _lib, block_fn as bf
     names, ps, slots = blk._param_list()
     graph = blk._graph()
@@ -321,21 +322,22 @@ def hip_cheb_relu_mask(blk, x, res):
     if fl:
         graph = blk._flash_graph(graph)
     X = _lib.load().block_cheb_out(x.detach().float().contiguous(), bf.res_arg(res, x.shape[2]), list(ps), slots,
-                                   bf.graph_list(graph, sparse, fl), bf.cfg_of(blk.meta), 0.05, 0,
-                                   bf.flags_of(False, sparse, False, fl))
+                                   bf.graph_list(graph, sparse, fl), bf.cfg_of(blk.meta), 0.05, int(seed),
+                                   bf.flags_of(train, sparse, False, fl))
     return (X > 0).permute(0, 1, 3, 2).contiguous().cpu()
 
 
-def relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask_hip, what, eps=RELU_EPS):
+def relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask_hip, what, eps=RELU_EPS, drop_masks=None):
     """Check that the HIP's ReLU decisions differ from the fp64 oracle's only where the fp64
     pre-activation is within RELU_EPS * scale of 0; returns the number of such flips (the
     oracle then evaluates with the HIP's decisions, so a flip cannot fail the value checks
-    and a kernel bug cannot hide behind one)."""
+    and a kernel bug cannot hide behind one).  drop_masks: train mode with these masks."""
     d64 = lambda t: t.double() if torch.is_tensor(t) else t  # noqa: E731
     pre = {}
+    dm = None if drop_masks is None else tuple(d64(m) for m in drop_masks)
     with torch.no_grad():
         ref.block_forward({k: d64(v) for k, v in p.items()}, d64(x), d64(res), [d64(c) for c in cheb], d64(apa), dims,
-                          hoist=True, pre_out=pre)
+                          train=dm is not None, drop_masks=dm, hoist=True, pre_out=pre)
     z = pre["z"]
     flip = mask_hip != (z > 0)
     scale = float(z.abs().max())
@@ -345,8 +347,20 @@ def relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask_hip, what, eps=RELU_EP
     return int(flip.sum())
 
 
-def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=RELU_EPS, errs=None, normwise=False):
+TRAIN_SEED = 1234  # torch.manual_seed before a train-mode forward: the block draws its dropout seed from it
+
+
+def _train_seed():
+    """The dropout seed DSTAGNN_block.forward draws after torch.manual_seed(TRAIN_SEED)
+    (model.py: torch.randint(0, 2**62) from the global CPU generator)."""
+    torch.manual_seed(TRAIN_SEED)
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=RELU_EPS, errs=None, normwise=False,
+                          train=False):
     import dstagnn_drought_amd as D_
+    from dstagnn_drought_amd.block_fn import dropout_masks
     N, T, K, h, D, dk, C = CONFIGS[name]
     ref, p, x, res, cheb, apa, dims, gen = _oracle_case(B, N, T, K, h, D, dk, C, first, 0 if first else 1, seed=seed)
     g_out = torch.randn(B, N, C, T, generator=gen)
@@ -354,17 +368,27 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
     F = x.shape[2]
     blk = D_.DSTAGNN_block("cpu", F, F, K, C, C, 1, cheb, apa, apa, N, T, D, dk, dk, h)
     blk.load_state_dict(p)
-    blk = blk.cuda().eval()
+    blk = blk.cuda().train(train)
     blk.flash_cheb = flash
     xg = x.cuda().requires_grad_(True)
     rg = res.cuda().requires_grad_(True) if torch.is_tensor(res) else 0
-    mask = hip_cheb_relu_mask(blk, xg, rg)
-    flips = relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask, name, eps=relu_eps)
+    dseed = _train_seed() if train else 0
+    dm = None
+    if train:
+        # the exact keep-masks (0 or 1/(1-p)) the HIP forward draws for this seed, handed to
+        # the oracle: EmbedS (B,N,D) as drawn, fcmy (B,N,C,T) -> the oracle's (B,C,N,T)
+        m0, m1 = dropout_masks(blk.meta, x.shape, dseed)
+        keep = float((m0 > 0).float().mean())
+        assert 0.94 < keep < 0.96, keep  # p = 0.05 over B*N*D draws
+        dm = (m0.cpu(), m1.cpu().permute(0, 2, 1, 3).contiguous())
+    mask = hip_cheb_relu_mask(blk, xg, rg, train=train, seed=dseed)
+    flips = relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask, name, eps=relu_eps, drop_masks=dm)
     d64 = lambda t: t.double() if torch.is_tensor(t) else t  # noqa: E731
     out_r, re_r, gx_r, gra_r, grads_r = ref.block_forward_backward(
         {k: d64(v) for k, v in p.items()}, d64(x), d64(res), [d64(c) for c in cheb], d64(apa), dims, d64(g_out),
-        d64(g_re), relu_mask=mask)
-    o32 = ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, relu_mask=mask)
+        d64(g_re), relu_mask=mask, train=train, drop_masks=None if dm is None else tuple(d64(m) for m in dm))
+    o32 = ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, relu_mask=mask, train=train,
+                                     drop_masks=dm)
     ref32 = {"out": o32[0], "re_at": o32[1], "grad_x": o32[2], "grad_res_att": o32[3], **o32[4]}
 
     def close_cal(a, b, key):
@@ -385,6 +409,8 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
             errs[key] = err / scale
         assert err <= bound, f"{name} {key}: max err {err:.3e} > bound {bound:.3e} (fp32 reference's own {own:.3e})"
 
+    if train:
+        torch.manual_seed(TRAIN_SEED)  # the forward draws dseed again
     out, re_at = blk(xg, rg)
     close_cal(out, out_r, "out")
     close_cal(re_at, re_r, "re_at")
@@ -419,6 +445,20 @@ def test_block_vs_oracle_configs(name, first, B, flash):
     _need_gpu()
     flips = _run_config_vs_oracle(name, first, B, flash=flash)
     print(f"{name} B={B} flash={flash}: {flips} ReLU decision(s) within rounding of 0")
+
+
+@pytest.mark.parametrize("name,first,B,flash", [("pems08", False, 32, None), ("pems08", True, 32, None),
+                                                ("pems08", False, 4, True), ("pems07", False, 2, None)])
+def test_block_train_mode_vs_oracle_configs(name, first, B, flash):
+    """TRAIN mode at the bench's own size (PEMS08 inner block, B=32: the timed path of
+    bench.py, both Dropout(0.05) of model/DSTAGNN_my.py:218,221 active at :234,:243): the
+    fp64 oracle gets the exact keep-masks the HIP forward drew (dstagnn::dropout_masks for the
+    same seed), then out, re_At, grad_x, grad_res_att and every parameter gradient are held to
+    the same bound as the eval-mode cases above (1e-4 * max(1, max|ref|), or twice the fp32
+    reference's own error where larger).  Also the first block and the fused attention."""
+    _need_gpu()
+    flips = _run_config_vs_oracle(name, first, B, flash=flash, train=True)
+    print(f"train {name} first={first} B={B} flash={flash}: {flips} ReLU decision(s) within rounding of 0")
 
 
 BF16_TOL = 3e-2      # bf16-operand GEMM variant: normwise ||err||_2 / ||ref||_2 <= BF16_TOL per tensor
@@ -458,8 +498,8 @@ def test_bf16_gemm_variant(name, first, B):
 # x[b:b+1].  Reaches what the B<=2 oracle cases cannot: the bench batch, GAMBIA's row-chunked
 # fcmy GEMM (B*N*C > 2^28 / (3T-12) rows), SYN's (B,K,N,N) score tensor of > 2^31 elements.
 # ---------------------------------------------------------------------------------------
-@pytest.mark.parametrize("name,B,samples", [("pems08", 32, (0, 13, 31)), ("gambia", 12, (0, 10, 11)),
-                                            ("syn", 32, (0, 31))])
+@pytest.mark.parametrize("name,B,samples", [("pems08", 32, (0, 13, 31)), ("pems07", 12, (0, 7, 11)),
+                                            ("gambia", 12, (0, 10, 11)), ("syn", 32, (0, 31))])
 def test_batch_consistency(name, B, samples):
     """With split-K off (dstagnn::set_splitk_target(1): every reduction in one fixed order)
     the per-sample results (out, re_At, grad_x, grad_res_att) must be BIT-identical; with the
@@ -509,6 +549,56 @@ def test_batch_consistency(name, B, samples):
                         assert err <= TOL * scale, f"{name} B={B} sample {b} {what}: {err:.3e} > {TOL} * {scale:.3e}"
         finally:
             ops.set_splitk_target(prev)
+
+
+@pytest.mark.parametrize("name,B,samples", [("pems08", 32, (0, 13, 30)), ("pems07", 12, (0, 5, 10))])
+def test_batch_consistency_train(name, B, samples):
+    """Train mode (both dropouts on, one seed): the keep-mask of sample b depends only on
+    (seed, b, position), never on the batch size, and sample b's results do not depend on the
+    other samples.  So a run on the prefix x[:b+1] with the same seed must give sample b
+    BIT-identically to the full-batch run (split-K off: every reduction in one fixed order),
+    and its masks must equal the full batch's masks of sample b."""
+    _need_gpu()
+    import dstagnn_drought_amd as D_
+    from dstagnn_drought_amd import _lib
+    from dstagnn_drought_amd.block_fn import dropout_masks
+    ops = _lib.load()
+    N, T, K, h, D, dk, C = CONFIGS[name]
+    ref, p, x, res, cheb, apa, dims, gen = _oracle_case(B, N, T, K, h, D, dk, C, False, 1, seed=9)
+    g_out = torch.randn(B, N, C, T, generator=gen)
+    g_re = torch.randn(B, C, h, T, T, generator=gen)
+    blk = D_.DSTAGNN_block("cpu", C, C, K, C, C, 1, cheb, apa, apa, N, T, D, dk, dk, h)
+    blk.load_state_dict(p)
+    blk = blk.cuda().train()
+    dseed = _train_seed()
+    full_m = dropout_masks(blk.meta, x.shape, dseed)
+
+    def run(n):
+        xg = x[:n].cuda().requires_grad_(True)
+        rg = res[:n].cuda().requires_grad_(True)
+        torch.manual_seed(TRAIN_SEED)
+        out, re_at = blk(xg, rg)
+        ((out * g_out[:n].cuda()).sum() + (re_at * g_re[:n].cuda()).sum()).backward()
+        r = [t.detach() for t in (out, re_at, xg.grad, rg.grad)]
+        for prm in blk.parameters():
+            prm.grad = None
+        return r
+
+    prev = ops.set_splitk_target(1)
+    try:
+        full = run(B)
+        torch.cuda.synchronize()
+        assert all(bool(torch.isfinite(t).all()) for t in full), "non-finite values in the full-batch run"
+        for b in samples:
+            pre_m = dropout_masks(blk.meta, (b + 1,) + tuple(x.shape[1:]), dseed)
+            for a, o in zip(full_m, pre_m):
+                assert torch.equal(a[b], o[b]), f"{name}: dropout mask of sample {b} depends on the batch size"
+            one = run(b + 1)
+            for what, a, o in zip(("out", "re_at", "grad_x", "grad_res_att"), full, one):
+                assert torch.equal(a[b], o[b]), f"{name} train B={B} sample {b} {what}: not bit-identical " \
+                                                f"(max diff {float((a[b] - o[b]).abs().max()):.3e})"
+    finally:
+        ops.set_splitk_target(prev)
 
 
 # ---------------------------------------------------------------------------------------
