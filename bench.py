@@ -128,13 +128,18 @@ def extras(dev, steps, warmup):
 PMC_FILE = "profiles/block_pmc.json"
 
 
-def load_pmc():
-    """Counter summary of the same step (tools/pmc_step.sh -> tools/pmc_step_summary.py), or None."""
+def load_pmc(stamp):
+    """Counter summary of the same step (tools/pmc_step.sh -> tools/pmc_step_summary.py), or None;
+    `stale` is set unless it was measured on this very library build (same libdstagnn.so sha)
+    and workload."""
     try:
         with open(os.path.join(ROOT, PMC_FILE)) as f:
-            return json.load(f)
+            pmc = json.load(f)
     except (OSError, ValueError):
         return None
+    b = pmc.get("build") or {}
+    pmc["stale"] = b.get("lib_sha256") != stamp["lib_sha256"] or pmc.get("workload", "pems08") != "pems08"
+    return pmc
 
 
 def algorithmic_flops_per_sample(c=CFG):
@@ -347,12 +352,18 @@ def main():
         P = args.prof_steps
         fam = dict(launches=launches / P, flops=flops / P, bytes=gbytes / P, ms=gms / P, max_ms=gmax,
                    serial_step_ms=t_ser * 1e3, dropped=dropped)
-    pmc = load_pmc()
+    stamp = _lib.build_stamp()
+    pmc = load_pmc(stamp)
+    fresh = pmc is not None and not pmc["stale"]
     if fam is not None:
         achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                "traffic": pmc["gemm_family"]["bytes_corrected"] if pmc else None,
+                # bytes from the PMC summary only when it measured this build (else null + the
+                # stale figure for reference)
+                "traffic": pmc["gemm_family"]["bytes_corrected"] if fresh else None,
+                "traffic_source": None if pmc is None else {"file": PMC_FILE, "stale": pmc["stale"],
+                                                            "build": pmc.get("build")},
                 "kernel": "gemm_f32 family: every GEMM call of one step (kernel + split-K fold), summed",
                 "launches_per_step": round(fam["launches"], 1), "gflop_per_step": round(fam["flops"] / 1e9, 4),
                 "ms_per_step": round(fam["ms"], 4), "avg_launch_us": round(fam["ms"] / fam["launches"] * 1e3, 3),
@@ -409,7 +420,10 @@ def main():
         gbs = bps / (ms_per_step * 1e-3) / 1e9
         hbm_roof = {"bytes_per_step": bps, "achieved_GBs": round(gbs, 1), "peak_GBs": PEAK_HBM_GBS,
                     "frac": round(gbs / PEAK_HBM_GBS, 4), "mfma_busy_frac": pmc["step"]["mfma_busy_frac"],
-                    "gemm_mfma_busy_frac": pmc["gemm_family"]["mfma_busy_frac"], "source": PMC_FILE}
+                    "gemm_mfma_busy_frac": pmc["gemm_family"]["mfma_busy_frac"], "source": PMC_FILE,
+                    "stale": pmc["stale"], "pmc_build": pmc.get("build")}
+        if pmc["stale"]:  # counters of another build: no fraction is claimed from them
+            hbm_roof["frac"] = None
     f_alg = algorithmic_flops_per_sample()
     peak_sps = PEAK_FP32_TFLOPS * 1e12 / f_alg
     block_roof = {"bound": "mfma", "alg_flop_per_sample": round(f_alg / 1e6, 1), "unit_flop": "MFLOP",
@@ -432,6 +446,7 @@ def main():
             "block_roofline": block_roof,
             "hbm_roofline": hbm_roof,
             "cpu_baseline": cpu,
+            "build": stamp,
         }
         if bf16 is not None:
             line["variant_bf16_gemm"] = bf16

@@ -37,6 +37,21 @@ def load():
     return _ops
 
 
+def build_stamp():
+    """Identity of the native build in this tree: sha256 (first 16 hex digits) of
+    libdstagnn.so and of _C.so.  Profiles under profiles/ record the stamp of the build they
+    measured; bench.py marks a profile whose stamp differs from its own library as stale."""
+    import hashlib
+
+    def sha(path):
+        h = hashlib.sha256()
+        with open(path, "rb") as f:
+            for chunk in iter(lambda: f.read(1 << 20), b""):
+                h.update(chunk)
+        return h.hexdigest()[:16]
+    return {"lib_sha256": sha(LIB_PATH), "ext_sha256": sha(EXT_PATH)}
+
+
 def gemm_maps(*maps):
     """Flatten 9 (div, s0, s1) index maps (a_m a_k a_z b_k b_n b_z c_m c_n c_z) for
     dstagnn::gemm_f32; a missing map is (0, 0, 0)."""

@@ -93,7 +93,7 @@ struct BlockCall {
   int64_t flags = 0;
 };
 
-dstagnn_graph graph_of(at::TensorList graph, bool sparse);
+dstagnn_graph graph_of(at::TensorList graph, bool sparse, int64_t K, int64_t N);
 
 BlockCall make_call(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params, at::IntArrayRef slots,
                     at::TensorList graph, at::IntArrayRef cfg, double drop_p, int64_t seed, int64_t flags) {
@@ -124,7 +124,7 @@ BlockCall make_call(const Tensor& x, const c10::optional<Tensor>& res, at::Tenso
     check_dev(params[i], at::kFloat, "parameter");
     arr[slots[i]] = params[i].data_ptr<float>();
   }
-  c.g = graph_of(graph, d.cheb_sparse != 0);
+  c.g = graph_of(graph, d.cheb_sparse != 0, d.K, d.N);
   d.cheb_flash = (flags & kFlash) ? 1 : 0;
   TORCH_CHECK(!d.cheb_flash || graph.size() == 12, "flash Chebyshev path requested without its graph data");
   d.cheb_nnz = d.cheb_flash ? c.g.nnz : 0;
@@ -383,23 +383,35 @@ std::tuple<Tensor, Tensor> dropout_masks(const Tensor& like, at::IntArrayRef sha
 // -------------------------------------------------------------------------------------
 constexpr int64_t kGemmWsBytes = int64_t(8) << 22;  // the library's split-K slab (8M floats)
 
-dstagnn_graph graph_of(at::TensorList graph, bool sparse) {
+// every size a kernel indexes by is checked here: the kernels trust them (an undersized
+// support array would be an out-of-bounds device read)
+dstagnn_graph graph_of(at::TensorList graph, bool sparse, int64_t K, int64_t N) {
   TORCH_CHECK(graph.size() == 2 || graph.size() == 6 || graph.size() == 12, "graph: 2, 6 or 12 tensors");
   dstagnn_graph g{};
   check_dev(graph[0], at::kFloat, "cheb");
   check_dev(graph[1], at::kFloat, "adj_pa");
+  TORCH_CHECK(graph[0].numel() >= K * N * N, "cheb must hold K (N,N) polynomials: ", graph[0].sizes(), " for K=", K,
+              " N=", N);
+  TORCH_CHECK(graph[1].numel() == N * N, "adj_pa must be (N,N) for N=", N, ", got ", graph[1].sizes());
   g.cheb = graph[0].data_ptr<float>();
   g.adj_pa = graph[1].data_ptr<float>();
   if (graph.size() >= 6) {
     for (int i = 2; i < 6; ++i) check_dev(graph[i], at::kInt, "graph support");
     g.nnz = (int)graph[3].numel();
+    TORCH_CHECK(graph[2].numel() == N + 1 && graph[4].numel() == N + 1, "graph support: csc_ptr / csr_ptr must have N+1 entries");
+    TORCH_CHECK(graph[5].numel() == g.nnz, "graph support: csr_col and csc_row lengths differ");
     g.csc_ptr = graph[2].data_ptr<int>(); g.csc_row = graph[3].data_ptr<int>();
     g.csr_ptr = graph[4].data_ptr<int>(); g.csr_col = graph[5].data_ptr<int>();
   }
   if (graph.size() == 12) {  // csr2csc, apa_bits, apa_bits_t, apa_ptr, apa_row, tsupp
     for (int i = 6; i < 11; ++i) check_dev(graph[i], at::kInt, "flash graph data");
     check_dev(graph[11], at::kFloat, "tsupp");
-    TORCH_CHECK(graph[6].numel() == g.nnz && graph[11].numel() % std::max(1, g.nnz) == 0, "flash graph data: sizes");
+    const int64_t nw = (N + 31) / 32;
+    TORCH_CHECK(graph[6].numel() == g.nnz, "flash graph data: csr2csc must have nnz entries");
+    TORCH_CHECK(graph[7].numel() == N * nw && graph[8].numel() == N * nw,
+                "flash graph data: apa_bits / apa_bits_t must be (N, ceil(N/32)) words");
+    TORCH_CHECK(graph[9].numel() == N + 1, "flash graph data: apa_ptr must have N+1 entries");
+    TORCH_CHECK(graph[11].numel() == K * (int64_t)g.nnz, "flash graph data: tsupp must be (K, nnz) for K=", K);
     g.csr2csc = graph[6].data_ptr<int>();
     g.apa_bits = graph[7].data_ptr<int32_t>();
     g.apa_bits_t = graph[8].data_ptr<int32_t>();
@@ -424,7 +436,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> cheb_sat_fwd(const Tensor& x, const T
   TORCH_CHECK(theta_cat.sizes() == at::IntArrayRef({F, K * C}), "theta_cat must be (F,K*C)");
   TORCH_CHECK(mask_cat.sizes() == at::IntArrayRef({K, N, N}), "mask_cat must be (K,N,N)");
   c10::DeviceGuard guard(x.device());
-  dstagnn_graph g = graph_of(graph, sparse);
+  dstagnn_graph g = graph_of(graph, sparse, K, N);
   Tensor out = at::empty({B, N, C, T}, f32(x));
   Tensor P = at::empty({B, K, N, N}, f32(x));
   Tensor W = sparse ? at::empty({0}, f32(x)) : at::empty({B, K, N, N}, f32(x));
@@ -450,7 +462,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> cheb_sat_bwd(const Tensor& x, const T
     check_dev(t, at::kFloat, n);
   const int64_t B = x.size(0), N = x.size(1), F = x.size(2), T = x.size(3), K = P.size(1);
   c10::DeviceGuard guard(x.device());
-  dstagnn_graph g = graph_of(graph, sparse);
+  dstagnn_graph g = graph_of(graph, sparse, K, N);
   Tensor dx = at::empty_like(x), dsat = at::empty({B, K, N, N}, f32(x));
   Tensor dth = at::empty({F, K * C}, f32(x)), dmask = at::empty({K, N, N}, f32(x));
   const int64_t nbig = B * N * C * T, nxth = B * N * K * C * T;

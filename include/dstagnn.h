@@ -6,9 +6,10 @@
  * (model/DSTAGNN_my.py:199-253).  The reference is pure Python/PyTorch with no
  * FFI; its "operator API" is the nn.Module surface.  The Python package
  * dstagnn_drought_amd mirrors that surface (make_model / DSTAGNN_block with the
- * same signatures and state_dict keys) and binds the entry points below through
- * ctypes.  No torch types cross this boundary: plain device
- * pointers, sizes and a hipStream_t.
+ * same signatures and state_dict keys) and reaches the entry points below through
+ * the PyTorch-ROCm operator library _C.so (TORCH_LIBRARY(dstagnn, ...),
+ * csrc/torch_ops.cpp), which links this library.  No torch
+ * types cross this boundary: plain device pointers, sizes and a hipStream_t.
  *
  * Conventions
  *   - All tensors are fp32, contiguous, row-major, device resident (HBM).
@@ -305,7 +306,7 @@ int dstagnn_prof_start(int capacity);
 int dstagnn_prof_stop(dstagnn_prof_stats* stats);
 
 /* Split-K policy of the GEMMs: a GEMM with a grid below 128 workgroups splits its K range
- * over about `target` workgroups (default 512).  target = 1 never splits, so every reduction
+ * over about `target` workgroups (default 320).  target = 1 never splits, so every reduction
  * runs in one fixed order and a sample's results are bit-identical at any batch size (parity
  * tests).  Returns the previous target; target <= 0 only queries. */
 int dstagnn_set_splitk_target(int target);

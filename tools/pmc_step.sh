@@ -17,6 +17,7 @@ pass() {
   echo "== pmc $name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -5 $OUT/$name.log; exit $rc; fi
 }
+python3 -c "import json, sys; sys.path.insert(0, '.'); from dstagnn_drought_amd._lib import build_stamp; print(json.dumps(build_stamp()))" > $OUT/build.json
 pass calib_fetch FETCH_SIZE -- tools/fetch_calib
 pass calib_write WRITE_SIZE -- tools/fetch_calib
 pass fetch FETCH_SIZE -- $B

@@ -17,6 +17,7 @@ import glob
 import json
 import os
 import re
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -66,6 +67,25 @@ def calib(d, counter):
         if c.get(counter):
             f[k].append(CALIB_BYTES / (c[counter] * 1024.0))
     return {k: round(sum(v[1:] or v) / len(v[1:] or v), 3) for k, v in f.items()}
+
+
+def stamp(d):
+    """Build + workload the counters belong to: the library sha the run recorded
+    (pmc_step.sh writes build.json on the GPU box), else this tree's, and this tree's HEAD."""
+    st = {}
+    try:
+        with open(os.path.join(d, "build.json")) as fh:
+            st.update(json.load(fh))
+    except (OSError, ValueError):
+        sys.path.insert(0, ROOT)
+        from dstagnn_drought_amd._lib import build_stamp
+        st.update(build_stamp())
+    try:
+        st["git_head"] = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"],
+                                                 text=True).strip()
+    except (OSError, subprocess.CalledProcessError):
+        st["git_head"] = None
+    return st
 
 
 def main():
@@ -124,6 +144,7 @@ def main():
                      "(DSTAGNN_SIDE_STREAM=0); one step = the kernels between the 2nd and 3rd param_prep dispatch",
            "calibration": {"fetch_bytes_per_counted_byte": fx, "write_bytes_per_counted_byte": wx,
                            "applied": {"gemm_fetch": f_g, "other_fetch": f_o, "write": w_o}},
+           "build": stamp(d), "workload": os.environ.get("PMC_WORKLOAD", "pems08"),
            "step": allk, "gemm_family": gem, "per_kernel": table}
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as fh:
