@@ -52,7 +52,7 @@ def res_arg(res_att, F):
     return res_att.float().contiguous()
 
 
-FLASH_KEYS = ("csr2csc", "apa_bits", "apa_bits_t", "apa_ptr", "apa_row", "tsupp")
+FLASH_KEYS = ("csr2csc", "apa_bits", "apa_bits_t", "apa_ptr", "apa_row", "tsupp", "csc2csr", "apa_idx", "apa2t")
 
 
 def graph_list(graph, sparse, flash=False):
@@ -75,11 +75,16 @@ def use_sparse(graph, meta, T):
     return graph["csc_row"].numel() * 4 <= N * N and meta["C"] * T <= (1 << 20)
 
 
+FLASH_SMALL_N = 512  # cheb_flash.hip kSmallN: graphs up to this size take the LDS-staged kernels
+
+
 def use_flash(graph, meta, T, force=None, B=0):
     """Fused (flash-style) Chebyshev attention (cheb_flash.hip): the (B,K,N,N) scores, softmax
     and score gradient are never written; on the sparse path with d_k == 32 (the MFMA tile),
-    automatically from N >= 1024 (DSTAGNN_FLASH=0/1 overrides), or when forced; batches up to
-    128 per call (the mask-gradient kernel's lanes)."""
+    automatically for small graphs (N <= 512: one workgroup per 32-column strip, operands
+    staged once) and large ones (N >= 1024: one wave per strip, streamed tiles);
+    DSTAGNN_FLASH=0/1 overrides, as does `force`; batches up to 128 per call (the
+    mask-gradient kernel's lanes)."""
     if not use_sparse(graph, meta, T) or meta["d_k"] != 32 or B > 128:
         return False
     if force is not None:
@@ -87,7 +92,8 @@ def use_flash(graph, meta, T, force=None, B=0):
     env = os.environ.get("DSTAGNN_FLASH")
     if env is not None:
         return env == "1"
-    return graph["adj_pa"].shape[0] >= 1024
+    N = graph["adj_pa"].shape[0]
+    return N <= FLASH_SMALL_N or N >= 1024
 
 
 def cfg_of(meta):

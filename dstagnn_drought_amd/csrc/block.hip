@@ -46,7 +46,9 @@ struct Dims {
   int64_t FT, BFT, BN, NN, HQ, HV, QW, KD, KC, CT, KCT, S;
   int Tg[3], Lp[3], ks[3];
   bool first, sparse, flash;
-  int64_t nnz;  // flash: union-support entries
+  bool fsmall;      // flash on a small graph (flash_small): the LDS-staged kernels
+  int64_t nnz;      // flash: union-support entries
+  int64_t apa_nnz;  // small-graph flash: A_pa support entries
 };
 
 Dims mkdims(const dstagnn_block_dims& d) {
@@ -61,6 +63,8 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.sparse = d.cheb_sparse != 0;
   m.flash = m.sparse && d.cheb_flash != 0;
   m.nnz = m.flash ? d.cheb_nnz : 0;
+  m.fsmall = m.flash && flash_small(m.N);
+  m.apa_nnz = m.fsmall ? std::max(d.cheb_apa_nnz, 0) : 0;
   return m;
 }
 
@@ -71,6 +75,7 @@ struct SaveBufs {
   float *Wqkv, *Wqk, *Wp, *thcat, *Wgf[3], *Wgb[3];
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float *lse, *psupp, *wsupp;  // flash path: column log-sum-exp (B,K,N), P and T o P on the support (B,K,nnz)
+  float *am, *papa;            // small-graph flash: A_pa o M_k (K,N,N), P on the A_pa support (B,K,apa_nnz)
   float* conv[3];
   float *G, *tco, *r, *mu_c, *rs_c, *u_et, *mu_et, *rs_et;
 };
@@ -101,6 +106,8 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   s.lse = m.flash ? a.take((int64_t)m.B * m.K * m.N) : nullptr;
   s.psupp = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.wsupp = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
+  s.am = m.fsmall ? a.take((int64_t)m.K * m.NN) : nullptr;
+  s.papa = m.fsmall ? a.take(std::max<int64_t>(1, (int64_t)m.B * m.K * m.apa_nnz)) : nullptr;
   s.xth = a.take(m.BN * m.KCT);
   s.X = a.take(m.BN * m.CT);
   for (int g = 0; g < 3; ++g) s.conv[g] = a.take(m.BN * 2 * m.C * std::max(m.Tg[g], 0));
@@ -129,7 +136,7 @@ struct Scratch {
   float *gemm_ws_side, *part_side, *dWqkv, *dWqk;
   float *dtc, *dX, *gpre, *gcon_t, *bcon_t, *dres_t, *gcon_s, *bcon_s, *gcon_a, *gcon_e, *dconv[3], *dW, *dxth,
       *dthcat, *dqk, *dZd, *dY, *dWp, *dO, *dU, *dE, *dctx, *dqkv, *dscore, *du_et, *dGt;
-  float *dws, *dzs, *cc;  // flash path: dW and P o dP on the support (B,K,nnz), c (B,K,N)
+  float *dzs, *dzs_r, *cc;  // flash path: P o dP on the support (B,K,nnz; dzs_r in CSR order), c (B,K,N)
 };
 
 Scratch plan_scratch(const Dims& m, Arena& a) {
@@ -152,8 +159,8 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.gcon_e = m.first ? a.take((int64_t)m.B * m.T * m.N) : nullptr;
   for (int g = 0; g < 3; ++g) s.dconv[g] = a.take(m.BN * 2 * m.C * m.Lp[g]);
   s.dW = m.flash ? nullptr : a.take((int64_t)m.B * m.K * m.NN);
-  s.dws = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.dzs = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
+  s.dzs_r = m.fsmall ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.cc = m.flash ? a.take((int64_t)m.B * m.K * m.N) : nullptr;
   s.dxth = a.take(m.BN * m.KCT);
   s.dthcat = a.take((int64_t)m.F * m.KC);
@@ -368,6 +375,9 @@ ChebFl make_fl(const Dims& m, const dstagnn_block_params& p, const dstagnn_graph
   f.csc_ptr = g.csc_ptr; f.csc_row = g.csc_row; f.csr_ptr = g.csr_ptr; f.csr_col = g.csr_col; f.csr2csc = g.csr2csc;
   f.apa_ptr = g.apa_ptr; f.apa_row = g.apa_row; f.tsupp = g.tsupp;
   f.lse = s.lse; f.psupp = s.psupp; f.wsupp = s.wsupp;
+  if (m.fsmall) {
+    f.am = s.am; f.papa = s.papa; f.apa_nnz = (int)m.apa_nnz; f.apa_idx = g.apa_idx; f.apa2t = g.apa2t;
+  }
   return f;
 }
 
@@ -574,6 +584,11 @@ struct Fwd {
       add(3, p.gtu_w[g], s.Wgf[g], n, m.C, m.ks[g]);
       add(4, p.gtu_w[g], s.Wgb[g], n, m.C, m.ks[g]);
     }
+    if (m.fsmall)  // the dense A_pa o M_k of the small-graph attention kernels (:122)
+      for (int k = 0; k < m.K; ++k) {
+        add(5, p.mask[k], s.am + (int64_t)k * m.NN, m.NN);
+        pp.seg[pp.nseg - 1].src2 = gr.adj_pa;
+      }
     DS_TRY(op_param_prep(pp, q));
     return 0;
   }
@@ -714,7 +729,7 @@ struct Bwd {
   ChebFl fl;
   ChebFl flash_args() {
     ChebFl f = make_fl(m, p, gr, s);
-    f.dws = w.dws; f.dzs = w.dzs; f.cc = w.cc; f.dqk = w.dqk;
+    f.dzs = w.dzs; f.dzs_r = w.dzs_r; f.cc = w.cc; f.dqk = w.dqk;
     for (int k = 0; k < m.K; ++k) f.dmask[k] = gd.mask[k];
     return f;
   }
@@ -838,8 +853,10 @@ struct Bwd {
       // T_k != 0 (no memset)
       ChebSp sp = make_sp(B, N, K, C, m.T, &gr);
       sp.P = s.P; sp.xth = s.xth; sp.g = w.gpre; sp.dW = w.dW; sp.dxth = w.dxth;
-      if (m.flash) {  // T o P and dW compact on the support
-        sp.nnz = (int)m.nnz; sp.wsupp = s.wsupp; sp.dws = w.dws; sp.csr2csc = gr.csr2csc;
+      if (m.flash) {  // T o P compact on the support; the SDDMM writes dzs = P o T o dW and c
+        sp.nnz = (int)m.nnz; sp.wsupp = s.wsupp; sp.csr2csc = gr.csr2csc;
+        sp.psupp = s.psupp; sp.tsupp = gr.tsupp; sp.dzs = w.dzs; sp.cc = w.cc;
+        if (m.fsmall) { sp.csc2csr = gr.csc2csr; sp.dzs_r = w.dzs_r; }
       }
       // dxth = W^T g on the side stream (only the Theta / x gradients, also on the side,
       // read it), dW = (x Theta) g^T on the support on the main chain: independent products
@@ -872,8 +889,7 @@ struct Bwd {
     sm.dW = w.dW; sm.dz = w.dW;
     for (int k = 0; k < K; ++k) sm.dmask[k] = gd.mask[k];
     if (m.flash) {
-      fl = flash_args();
-      DS_TRY(op_flash_colc(fl, st));
+      fl = flash_args();  // c and dzs came with the SDDMM
     } else {
       DS_TRY(op_cheb_softmax_bwd(sm, st));
     }
@@ -1146,6 +1162,10 @@ int check_graph(const Dims& m, const dstagnn_graph* g) {
   if (m.flash && (g->nnz != m.nnz || !g->csr2csc || !g->apa_bits || !g->apa_bits_t || !g->apa_ptr || !g->apa_row ||
                   !g->tsupp)) {
     set_last_error("cheb_flash set but the graph lacks the flash data (or its nnz differs from cheb_nnz)");
+    return DSTAGNN_E_ARG;
+  }
+  if (m.fsmall && (!g->csc2csr || !g->apa_idx || !g->apa2t || g->apa_nnz != m.apa_nnz)) {
+    set_last_error("cheb_flash on a small graph needs csc2csr / apa_idx / apa2t (and apa_nnz == cheb_apa_nnz)");
     return DSTAGNN_E_ARG;
   }
   return 0;

@@ -344,10 +344,350 @@ __global__ __launch_bounds__(256) void flash_zero_kernel(ChebFl a) {
 
 unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
 
+// ---------------------------------------------------------------------------------------
+// Small graphs (N <= kSmallN: PEMS08 170, PEMS04 307).  The kernels above give one wave a
+// whole 32-column strip and walk its row tiles with a global round trip per tile (Q' rows,
+// bit words, the A_pa term) behind a serial MFMA chain: at N = 170 that is ~6 latency-bound
+// iterations on < 1 wave per SIMD.  Here a 4-wave workgroup owns the strip, each wave takes
+// every 4th tile, and every operand is fetched in ONE round at kernel entry: the score
+// operands, the dense A_pa o M_k strip (AM, formed once per forward by param_prep: no bit
+// tests and no dependent loads; AM = 0 off the support, and z + 0 = z exactly), and the
+// strip's support pointers.  The forward also keeps P on the A_pa support (papa), so the mask
+// gradient needs no score recomputation at all.
+// ---------------------------------------------------------------------------------------
+constexpr int kSmallN = 512;         // <= 16 tiles: <= kSmallTPW per wave
+constexpr int kSmallTPW = 4;         // tiles per wave at most (kernels templated on 1..4)
+constexpr int kXs = 36;              // LDS row stride (floats) of a staged (N, 32) operand: 16-B rows
+
+// forward: lse_j, P and W = T o P on the T support, P on the A_pa support, for one
+// (b, k, 32-column strip).  The strip's P tile goes through LDS ((32 nt) x 33 floats, dynamic).
+template <int kSmallTiles>
+__global__ __launch_bounds__(256) void flash_small_fwd_kernel(ChebFl a) {
+  extern __shared__ float Pt[];  // [(32 nt)][33]
+  __shared__ float red_m[4][32], red_l[4][32];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int nt = (a.N + 31) >> 5;
+  const int jt = (int)(blockIdx.x % nt), bk = (int)(blockIdx.x / nt), k = bk % a.K, b = bk / a.K;
+  const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+  const float* Kp = Q + a.kd;
+  const float* AM = a.am + (int64_t)k * a.N * a.N;
+  const int j = jt * 32 + l32, jc = min(j, a.N - 1);
+  // the strip's support walk (8 threads per column): pointers now, first entries below
+  const int jl = threadIdx.x >> 3, sub = threadIdx.x & 7, jj = min(jt * 32 + jl, a.N - 1);
+  const bool jok = jt * 32 + jl < a.N;
+  const int p0 = a.csc_ptr[jj], p1 = a.csc_ptr[jj + 1], q0 = a.apa_ptr[jj], q1 = a.apa_ptr[jj + 1];
+  // every operand of this wave's tiles in the same round
+  float bkv[16], aq[kSmallTiles][16], am[kSmallTiles][16];
+  load16(Kp + (int64_t)jc * a.ld + h * 16, bkv);
+#pragma unroll
+  for (int q = 0; q < kSmallTiles; ++q) {
+    const int it = w + 4 * q;
+    if (it < nt) {
+      load16(Q + (int64_t)min(it * 32 + l32, a.N - 1) * a.ld + h * 16, aq[q]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) am[q][r] = AM[(int64_t)min(it * 32 + frag_row(r, h), a.N - 1) * a.N + jc];
+    }
+  }
+  const int pf = p0 + sub, qf = q0 + sub;  // first support entries of this thread
+  const int row_p = pf < p1 ? a.csc_row[pf] : 0, row_q = qf < q1 ? a.apa_row[qf] : 0;
+  const float t_p = pf < p1 ? a.tsupp[(int64_t)k * a.nnz + pf] : 0.f;
+  float z[kSmallTiles][16];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < kSmallTiles; ++q) {
+    const int it = w + 4 * q;
+    if (it >= nt) break;
+    floatx16 acc = zero16();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[q][s], bkv[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = it * 32 + frag_row(r, h) < a.N ? acc[r] * a.scale + am[q][r] : -INFINITY;
+      z[q][r] = v;
+      mx = fmaxf(mx, v);
+    }
+  }
+  // column max, then column sum of exp over the four waves (two-pass softmax statistics)
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  if (h == 0) red_m[w][l32] = mx;
+  __syncthreads();
+  const float M = fmaxf(fmaxf(red_m[0][l32], red_m[1][l32]), fmaxf(red_m[2][l32], red_m[3][l32]));
+  float l = 0.f;
+#pragma unroll
+  for (int q = 0; q < kSmallTiles; ++q) {
+    if (w + 4 * q >= nt) break;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) l += __expf(z[q][r] - M);
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (h == 0) red_l[w][l32] = l;
+  __syncthreads();
+  const float lse = M + __logf((red_l[0][l32] + red_l[1][l32]) + (red_l[2][l32] + red_l[3][l32]));
+  if (w == 0 && h == 0 && j < a.N) a.lse[(int64_t)bk * a.N + j] = lse;
+#pragma unroll
+  for (int q = 0; q < kSmallTiles; ++q) {
+    const int it = w + 4 * q;
+    if (it >= nt) break;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Pt[(it * 32 + frag_row(r, h)) * 33 + l32] = __expf(z[q][r] - lse);
+  }
+  __syncthreads();
+  if (!jok) return;
+  const int64_t base = (int64_t)bk * a.nnz;
+  for (int p = pf; p < p1; p += 8) {
+    const int i = p == pf ? row_p : a.csc_row[p];
+    const float P = Pt[i * 33 + jl];
+    a.psupp[base + p] = P;
+    a.wsupp[base + p] = (p == pf ? t_p : a.tsupp[(int64_t)k * a.nnz + p]) * P;
+  }
+  const int64_t abase = (int64_t)bk * a.apa_nnz;
+  for (int q = qf; q < q1; q += 8) a.papa[abase + q] = Pt[(q == qf ? row_q : a.apa_row[q]) * 33 + jl];
+}
+
+// stage rows [0, N) of one (b, k) 32-float block of qk (Q' or K') into LDS X[(32 nt)][kXs]
+// (rows past N zero) — one cooperative round of 16-B loads
+__device__ __forceinline__ void stage_rows(const float* src, int64_t ld, int N, int NP, float* X) {
+  for (int e = threadIdx.x; e < NP * 8; e += 256) {
+    const int row = e >> 3, c4 = (e & 7) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < N) v = *reinterpret_cast<const float4*>(src + (int64_t)row * ld + c4);
+    *reinterpret_cast<float4*>(X + row * kXs + c4) = v;
+  }
+}
+
+__device__ __forceinline__ void lds16(const float* p, float (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+  }
+}
+
+// backward: dK' (workgroups [0, B K nt): one 32-column strip each) and dQ' (the next B K nt:
+// one 32-row strip each) in one launch.  The strip's own operand sits in registers, the other
+// (all N rows of Q' resp. K') is staged in LDS once; the waves split the contraction's tiles
+// and their 32 x 32 partial products are summed through LDS.  The sparse terms walk the
+// strip's support (CSC for dK', CSR with the CSR-ordered dzs_r for dQ').
+//   dK'_j = s (sum_{i in supp(j)} dzs_ij Q'_i - c_j sum_i P_ij Q'_i)
+//   dQ'_i = s (sum_{j in supp_row(i)} dzs_ij K'_j - sum_j P_ij c_j K'_j)
+template <int kSmallTiles>
+__global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
+  extern __shared__ float X[];  // [(32 nt)][kXs] operand rows, then lse [32 nt], c [32 nt] (dQ)
+  __shared__ float red[4][32][33];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int nt = (a.N + 31) >> 5, NP = nt * 32;
+  const int64_t half = (int64_t)a.B * a.K * nt;
+  const bool dq = blockIdx.x >= half;
+  const int64_t wg = dq ? blockIdx.x - half : blockIdx.x;
+  const int st = (int)(wg % nt), bk = (int)(wg / nt), k = bk % a.K, b = bk / a.K;
+  const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+  const float* Kp = Q + a.kd;
+  const float* AM = a.am + (int64_t)k * a.N * a.N;
+  const float* lseb = a.lse + (int64_t)bk * a.N;
+  const float* cb = a.cc + (int64_t)bk * a.N;
+  const int64_t zb = (int64_t)bk * a.nnz;
+  float* Ls = X + NP * kXs;
+  float* Cs = Ls + NP;
+  const int own = min(st * 32 + l32, a.N - 1);  // this lane's row (dQ) / column (dK) of the strip
+  // final phase: thread -> (4 strip rows, d); their support pointers fetched now
+  const int d = threadIdx.x & 31;
+  const int* ptr = dq ? a.csr_ptr : a.csc_ptr;
+  int pb[4], pe[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = min(st * 32 + (threadIdx.x >> 5) + 8 * u, a.N - 1);
+    pb[u] = ptr[row];
+    pe[u] = ptr[row + 1];
+  }
+  float bv[16], am[kSmallTiles][16];
+  float lse_own = 0.f, c_own = 0.f;
+  if (dq) {
+    load16(Q + (int64_t)own * a.ld + h * 16, bv);
+#pragma unroll
+    for (int q = 0; q < kSmallTiles; ++q)
+      if (w + 4 * q < nt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) am[q][r] = AM[(int64_t)own * a.N + min((w + 4 * q) * 32 + frag_row(r, h), a.N - 1)];
+    stage_rows(Kp, a.ld, a.N, NP, X);
+    for (int e = threadIdx.x; e < NP; e += 256) {
+      Ls[e] = e < a.N ? lseb[e] : INFINITY;
+      Cs[e] = e < a.N ? cb[e] : 0.f;
+    }
+  } else {
+    load16(Kp + (int64_t)own * a.ld + h * 16, bv);
+#pragma unroll
+    for (int q = 0; q < kSmallTiles; ++q)
+      if (w + 4 * q < nt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) am[q][r] = AM[(int64_t)min((w + 4 * q) * 32 + frag_row(r, h), a.N - 1) * a.N + own];
+    lse_own = lseb[own];
+    stage_rows(Q, a.ld, a.N, NP, X);
+  }
+  (void)c_own;
+  __syncthreads();
+  floatx16 O = zero16();
+#pragma unroll
+  for (int q = 0; q < kSmallTiles; ++q) {
+    const int tt = w + 4 * q;  // the contraction's tile: columns j (dQ) / rows i (dK)
+    if (tt >= nt) break;
+    float av[16];
+    lds16(X + (tt * 32 + l32) * kXs + h * 16, av);
+    floatx16 S = zero16();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], S, 0, 0, 0);
+    float pv[16];
+    if (dq) {  // S^T tile D[m = j][n = i]: lane (i = l32) holds P_ij c_j for j = frag_row(r, h)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int jj = tt * 32 + frag_row(r, h);
+        pv[r] = __expf(S[r] * a.scale + am[q][r] - Ls[jj]) * Cs[jj];  // 0 past N (lse = +inf, c = 0)
+      }
+    } else {   // S tile D[m = i][n = j]: lane (j = l32) holds P_ij for i = frag_row(r, h)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        pv[r] = tt * 32 + frag_row(r, h) < a.N ? __expf(S[r] * a.scale + am[q][r] - lse_own) : 0.f;
+    }
+    // O[m = strip row][n = d] += sum over the tile's 32 entries of pv x (staged row)[d]
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      O = __builtin_amdgcn_mfma_f32_32x32x2f32(pv[s], X[(tt * 32 + frag_row(s, h)) * kXs + l32], O, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[w][frag_row(r, h)][l32] = O[r];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int rl = (threadIdx.x >> 5) + 8 * u, row = st * 32 + rl;
+    if (row >= a.N) continue;
+    const float dense = (red[0][rl][d] + red[1][rl][d]) + (red[2][rl][d] + red[3][rl][d]);
+    float sp = 0.f;
+    if (dq) {
+      for (int p = pb[u]; p < pe[u]; ++p) sp = fmaf(a.dzs_r[zb + p], X[a.csr_col[p] * kXs + d], sp);
+      a.dqk[((int64_t)b * a.N + row) * a.ld + k * 32 + d] = (sp - dense) * a.scale;
+    } else {
+      for (int p = pb[u]; p < pe[u]; ++p) sp = fmaf(a.dzs[zb + p], X[a.csc_row[p] * kXs + d], sp);
+      a.dqk[((int64_t)b * a.N + row) * a.ld + a.kd + k * 32 + d] = (sp - cb[row] * dense) * a.scale;
+    }
+  }
+}
+
+// backward, small graphs: dM_k[i,j] = A_pa[i,j] sum_b (dzs_b[i,j] - P_b[i,j] c_b[j]), every
+// element of the K (N,N) gradients written by one thread (0 off the A_pa support), P on the
+// support kept by the forward (papa), the T-support position of the entry from apa2t.
+__global__ __launch_bounds__(256) void flash_small_mask_kernel(ChebFl a) {
+  const int64_t NN = (int64_t)a.N * a.N;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)a.K * NN) return;
+  const int k = (int)(e / NN);
+  const int64_t o = e - (int64_t)k * NN;
+  float* dM = a.dmask[k];
+  if (!dM) return;
+  const int q = a.apa_idx[o];
+  if (q < 0) {
+    dM[o] = 0.f;
+    return;
+  }
+  const int j = (int)(o % a.N), pt = a.apa2t[q];
+  float s = 0.f;
+  for (int b = 0; b < a.B; ++b) {
+    const int64_t bk = (int64_t)b * a.K + k;
+    s += (pt >= 0 ? a.dzs[bk * a.nnz + pt] : 0.f) - a.papa[bk * a.apa_nnz + q] * a.cc[bk * a.N + j];
+  }
+  dM[o] = a.apa[o] * s;
+}
+
+// backward: dM_k[i, :] for one (k, row i) per wave, every N entries written: zeros off the A_pa
+// support (coalesced row stores — no separate zeroing pass), A_pa[i,j] sum_b dz_b[i,j] on it.
+// Lanes over the batch (B <= 128); P recomputed by a 32-long dot product per (b, j); the
+// T-support position of (i, j) from the CSR row (no search over a CSC column).
+__global__ __launch_bounds__(256) void flash_mask_grad_rows_kernel(ChebFl a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= (int64_t)a.K * a.N) return;
+  const int i = (int)(wid % a.N), k = (int)(wid / a.N);
+  float* dM = a.dmask[k];
+  if (!dM) return;
+  const float* Mk = a.mask[k];
+  const int32_t* br = a.bits + (int64_t)i * a.nw;
+  float* drow = dM + (int64_t)i * a.N;
+  for (int j = lane; j < a.N; j += 64)
+    if (!((br[j >> 5] >> (j & 31)) & 1)) drow[j] = 0.f;
+  constexpr int kMaxBB = 2;
+  const int nb = min(kMaxBB, (a.B + 63) / 64);
+  float qv[kMaxBB][32];
+#pragma unroll
+  for (int bb = 0; bb < kMaxBB; ++bb) {
+    const int b = min(lane + 64 * bb, a.B - 1);
+    const float* qr = a.qk + ((int64_t)b * a.N + i) * a.ld + k * 32;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float4 v = *reinterpret_cast<const float4*>(qr + 4 * u);
+      qv[bb][4 * u] = v.x; qv[bb][4 * u + 1] = v.y; qv[bb][4 * u + 2] = v.z; qv[bb][4 * u + 3] = v.w;
+    }
+  }
+  const int q0 = a.csr_ptr[i], q1 = a.csr_ptr[i + 1];
+  for (int w0 = 0; w0 < a.nw; w0 += 64) {
+    const uint32_t wl = w0 + lane < a.nw ? (uint32_t)br[w0 + lane] : 0u;
+    const int nwc = min(64, a.nw - w0);
+    for (int wi = 0; wi < nwc; ++wi) {
+      uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)wl, wi);
+      while (word) {
+        const int bit = __builtin_ctz(word);
+        word &= word - 1u;
+        const int j = (w0 + wi) * 32 + bit;
+        const float av = a.apa[(int64_t)i * a.N + j];
+        const float mterm = av * Mk[(int64_t)i * a.N + j];
+        int pt = -1;  // the T-support entry (i, j), if any (CSC position)
+        for (int q = q0; q < q1; ++q)
+          if (a.csr_col[q] == j) pt = a.csr2csc[q];
+        float s = 0.f;
+        for (int bb = 0; bb < nb; ++bb) {
+          const int b = lane + 64 * bb;
+          if (b >= a.B) break;
+          const int bk = b * a.K + k;
+          const float* kr = a.qk + ((int64_t)b * a.N + j) * a.ld + a.kd + k * 32;
+          const float z = dot32(kr, qv[bb]) * a.scale + mterm;
+          const float P = __expf(z - a.lse[(int64_t)bk * a.N + j]);
+          const float dzs = pt >= 0 ? a.dzs[(int64_t)bk * a.nnz + pt] : 0.f;
+          s += dzs - P * a.cc[(int64_t)bk * a.N + j];
+        }
+        s = wave_sum(s);
+        if (lane == 0) drow[j] = av * s;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool flash_small(int N) { return N <= kSmallN; }
+
+namespace {
+// dynamic LDS beyond the default 64 KB needs the kernel's limit raised once
+template <typename Kern>
+int allow_lds(Kern k, size_t bytes) {
+  if (bytes <= (64u << 10)) return 0;
+  const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) { set_last_error(std::string("flash: LDS attribute: ") + hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
 }  // namespace
 
 int op_flash_forward(const ChebFl& a, hipStream_t st) {
   const int nt = (a.N + 31) >> 5;
+  if (a.am) {  // small graphs (flash_small): statistics and the support P from the same score tiles
+    const size_t lds = (size_t)nt * 32 * 33 * sizeof(float);
+    const dim3 grid((unsigned)((int64_t)a.B * a.K * nt));
+    switch ((nt + 3) / 4) {  // tiles per wave
+#define DS_FWD(T) case T: DS_TRY(allow_lds(flash_small_fwd_kernel<T>, lds)); \
+      hipLaunchKernelGGL(flash_small_fwd_kernel<T>, grid, dim3(256), lds, st, a); break;
+      DS_FWD(1) DS_FWD(2) DS_FWD(3) DS_FWD(4)
+#undef DS_FWD
+      default: set_last_error("flash: graph too large for the small-graph kernels"); return DSTAGNN_E_SHAPE;
+    }
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(flash_stats_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   hipLaunchKernelGGL(flash_psupp_kernel, dim3((unsigned)cdiv64((int64_t)a.B * a.K * a.N, 256)), dim3(256), 0, st, a);
@@ -363,6 +703,19 @@ int op_flash_colc(const ChebFl& a, hipStream_t st) {
 
 int op_flash_dqk(const ChebFl& a, hipStream_t st) {
   const int nt = (a.N + 31) >> 5;
+  if (a.am) {  // small graphs (flash_small): dK' and dQ' strips in one launch
+    const size_t lds = ((size_t)nt * 32 * kXs + 2 * (size_t)nt * 32) * sizeof(float);
+    const dim3 grid((unsigned)(2 * (int64_t)a.B * a.K * nt));
+    switch ((nt + 3) / 4) {  // tiles per wave
+#define DS_DQK(T) case T: DS_TRY(allow_lds(flash_small_dqk_kernel<T>, lds)); \
+      hipLaunchKernelGGL(flash_small_dqk_kernel<T>, grid, dim3(256), lds, st, a); break;
+      DS_DQK(1) DS_DQK(2) DS_DQK(3) DS_DQK(4)
+#undef DS_DQK
+      default: set_last_error("flash: graph too large for the small-graph kernels"); return DSTAGNN_E_SHAPE;
+    }
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(flash_dq_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
   hipLaunchKernelGGL(flash_dk_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
@@ -371,6 +724,20 @@ int op_flash_dqk(const ChebFl& a, hipStream_t st) {
 }
 
 int op_flash_mask_grad(const ChebFl& a, hipStream_t st) {
+  // row-wise: every row of dM_k written by one wave (zeros off the A_pa support included);
+  // DSTAGNN_FLASH_MASK_COLS=1 keeps the column-wise kernel + zeroing pass (A/B)
+  static const bool cols = getenv("DSTAGNN_FLASH_MASK_COLS") && atoi(getenv("DSTAGNN_FLASH_MASK_COLS")) != 0;
+  if (a.papa && a.apa_idx && !cols) {  // small graphs: one thread per element, P from the forward
+    hipLaunchKernelGGL(flash_small_mask_kernel, dim3((unsigned)cdiv64((int64_t)a.K * a.N * a.N, 256)), dim3(256), 0,
+                       st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
+  if (!cols) {
+    hipLaunchKernelGGL(flash_mask_grad_rows_kernel, dim3(grid_waves((int64_t)a.K * a.N)), dim3(256), 0, st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   const int64_t NN = (int64_t)a.N * a.N;
   hipLaunchKernelGGL(flash_zero_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(NN, 256), 4096), (unsigned)a.K),
                      dim3(256), 0, st, a);

@@ -95,6 +95,18 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   }
 }
 
+// the flash path's softmax-backward column terms at the SDDMM (was a separate pass over the
+// compact dW): dzs_ij = P_ij T_ij dW_ij (stored by lane 0), returned for c_j = sum_i dzs_ij
+__device__ __forceinline__ float sddmm_dzs(const ChebSp& a, int b, int k, int p, float dw) {
+  const int64_t o = ((int64_t)b * a.K + k) * a.nnz + p;
+  const float d = a.psupp[o] * (a.tsupp[(int64_t)k * a.nnz + p] * dw);
+  if ((threadIdx.x & 63) == 0) {
+    a.dzs[o] = d;
+    if (a.dzs_r) a.dzs_r[((int64_t)b * a.K + k) * a.nnz + a.csc2csr[p]] = d;
+  }
+  return d;
+}
+
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
@@ -117,6 +129,7 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
     for (int k = 0; k < a.K; ++k) {
       float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
       float* dSk = a.dws ? a.dws + ((int64_t)b * a.K + k) * a.nnz : nullptr;
+      float csum = 0.f;
       for (int p = p0; p < p1; ++p) {
         const int i = a.csc_row[p];
         const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
@@ -124,17 +137,20 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
 #pragma unroll
         for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], xr[xo[q]], s);
         s = wave_sum(s);
-        if (lane == 0) {
+        if (a.dzs) csum += sddmm_dzs(a, b, k, p, s);
+        else if (lane == 0) {
           if (dSk) dSk[p] = s;
           else dWk[(int64_t)i * a.N + j] = s;
         }
       }
+      if (a.dzs && lane == 0) a.cc[((int64_t)b * a.K + k) * a.N + j] = csum;
     }
     return;
   }
   for (int k = 0; k < a.K; ++k) {  // long rows: the dot product walks the chunks
     float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
     float* dSk = a.dws ? a.dws + ((int64_t)b * a.K + k) * a.nnz : nullptr;
+    float csum = 0.f;
     for (int p = p0; p < p1; ++p) {
       const int i = a.csc_row[p];
       const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
@@ -149,11 +165,13 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
         }
       }
       s = wave_sum(s);
-      if (lane == 0) {
+      if (a.dzs) csum += sddmm_dzs(a, b, k, p, s);
+      else if (lane == 0) {
         if (dSk) dSk[p] = s;
         else dWk[(int64_t)i * a.N + j] = s;
       }
     }
+    if (a.dzs && lane == 0) a.cc[((int64_t)b * a.K + k) * a.N + j] = csum;
   }
 }
 

@@ -1129,11 +1129,14 @@ __global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
         o = (oc * g.p1 + j) * g.p0 + c;
         break;
       }
-      default: {  // src (o, c, j) -> dst (ks-1-j, o, c)
+      case 4: {  // src (o, c, j) -> dst (ks-1-j, o, c)
         const int64_t j = i % g.p1, r = i / g.p1, c = r % g.p0, oc = r / g.p0;
         o = ((g.p1 - 1 - j) * 2 * g.p0 + oc) * g.p0 + c;
         break;
       }
+      default:  // elementwise product (A_pa o M_k: the reference's adj_pa.mul(mask[k]), :122)
+        g.dst[i] = v * g.src2[i];
+        continue;
     }
     g.dst[o] = v;
   }
@@ -1402,7 +1405,7 @@ int op_cheb_mask_grad(const ChebSm& a, hipStream_t st) {
 
 int op_param_prep(const ParamPrep& a, hipStream_t st) {
   if (a.nseg <= 0) return 0;
-  if (a.nseg > 24) { set_last_error("param_prep: too many segments"); return DSTAGNN_E_ARG; }
+  if (a.nseg > kPrepSegs) { set_last_error("param_prep: too many segments"); return DSTAGNN_E_ARG; }
   int64_t mx = 1;
   for (int q = 0; q < a.nseg; ++q) mx = std::max<int64_t>(mx, a.seg[q].n);
   hipLaunchKernelGGL(param_prep_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(mx, 256), 256), (unsigned)a.nseg),

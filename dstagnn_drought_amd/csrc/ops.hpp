@@ -78,16 +78,19 @@ struct PackRows {
 //   2 theta          thcat[f][k*C + c] = theta_k[f][c]  p0 = C, p1 = K*C, p2 = k
 //   3 gtu fwd        perm[o][j][c] = w[o][c][j]         p0 = C, p1 = ks
 //   4 gtu bwd        perm[j'][o][c] = w[o][c][ks-1-j']  p0 = C, p1 = ks
+//   5 product        dst[i] = src[i] * src2[i]                          (A_pa o M_k)
 struct PrepSeg {
   int kind = 0, p0 = 0, p1 = 0, p2 = 0;
   int64_t n = 0;        // source elements
   int64_t dst_off = 0;  // kind 0: element offset into dst
   const float* src = nullptr;
+  const float* src2 = nullptr;  // kind 5
   float* dst = nullptr;
 };
+constexpr int kPrepSegs = 32;
 struct ParamPrep {
   int nseg = 0;
-  PrepSeg seg[24];
+  PrepSeg seg[kPrepSegs];
 };
 
 // fused per-node GTU gates + fcmy + dropout + residual + LayerNorm (gtu_tail.hip)
@@ -141,6 +144,14 @@ struct ChebSp {
   int nnz = 0;
   const float* wsupp = nullptr;  // fwd / spmm_t: replaces T_k[i,j] P[b,k,i,j]
   float* dws = nullptr;          // sddmm: written instead of dW
+  // sddmm with the softmax-backward column terms fused (flash path): with dzs set, instead
+  // of dW it writes dzs = P o T o dW on the support and cc[b,k,j] = sum_i dzs_ij
+  const float* psupp = nullptr;  // (B,K,nnz) P on the support
+  const float* tsupp = nullptr;  // (K,nnz) T_k on the support
+  float* dzs = nullptr;          // (B,K,nnz)
+  float* cc = nullptr;           // (B,K,N)
+  const int* csc2csr = nullptr;  // with dzs_r: dzs also stored in CSR order (small-graph flash)
+  float* dzs_r = nullptr;        // (B,K,nnz)
   const int* csr2csc = nullptr;  // CSR position -> CSC position
   int xcd_order = 0;             // set by the launcher: XCD-aware row-block order (cheb_sparse.hip)
 };
@@ -163,7 +174,14 @@ struct ChebFl {
   const float* dws = nullptr; float* dzs = nullptr; float* cc = nullptr;  // (B,K,nnz) x2, (B,K,N)
   float* dqk = nullptr;                    // (B*N, ld) dQ' | dK'
   float* dmask[DSTAGNN_MAX_K] = {};        // (N,N) each, fully written
+  // small graphs (flash_small(N)): the dense A_pa o M_k, P on the A_pa support, the index maps
+  const float* am = nullptr;               // (K,N,N) A_pa o M_k (param_prep, every forward)
+  float* papa = nullptr; int apa_nnz = 0;  // (B,K,apa_nnz) P on the A_pa support (A_pa CSC order)
+  const int* apa_idx = nullptr;            // (N,N) A_pa-CSC index or -1
+  const int* apa2t = nullptr;              // (apa_nnz) union-support CSC position or -1
+  float* dzs_r = nullptr;                  // (B,K,nnz) dzs in CSR order (the SDDMM writes it)
 };
+bool flash_small(int N);  // the LDS-staged small-graph kernels (N <= 512)
 int op_flash_forward(const ChebFl& a, hipStream_t st);   // lse, psupp, wsupp
 int op_flash_colc(const ChebFl& a, hipStream_t st);      // cc, dzs
 int op_flash_dqk(const ChebFl& a, hipStream_t st);       // dqk

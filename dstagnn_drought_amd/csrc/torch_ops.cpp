@@ -101,9 +101,9 @@ BlockCall make_call(const Tensor& x, const c10::optional<Tensor>& res, at::Tenso
   TORCH_CHECK(x.dim() == 4, "x must be (B,N,F,T), got ", x.sizes());
   TORCH_CHECK(cfg.size() == 6, "cfg must be [n_heads, d_k, d_v, d_model, K, C]");
   TORCH_CHECK(params.size() == slots.size(), "params / slots length mismatch");
-  TORCH_CHECK(graph.size() == 2 || graph.size() == 6 || graph.size() == 12,
+  TORCH_CHECK(graph.size() == 2 || graph.size() == 6 || graph.size() == 15,
               "graph = [cheb, adj_pa] (+ csc_ptr, csc_row, csr_ptr, csr_col (+ csr2csc, apa_bits, apa_bits_t, "
-              "apa_ptr, apa_row, tsupp))");
+              "apa_ptr, apa_row, tsupp, csc2csr, apa_idx, apa2t))");
   BlockCall c;
   c.flags = flags;
   c.mode = res_mode_of(res, x.size(2));
@@ -126,8 +126,9 @@ BlockCall make_call(const Tensor& x, const c10::optional<Tensor>& res, at::Tenso
   }
   c.g = graph_of(graph, d.cheb_sparse != 0, d.K, d.N);
   d.cheb_flash = (flags & kFlash) ? 1 : 0;
-  TORCH_CHECK(!d.cheb_flash || graph.size() == 12, "flash Chebyshev path requested without its graph data");
+  TORCH_CHECK(!d.cheb_flash || graph.size() == 15, "flash Chebyshev path requested without its graph data");
   d.cheb_nnz = d.cheb_flash ? c.g.nnz : 0;
+  d.cheb_apa_nnz = d.cheb_flash ? c.g.apa_nnz : 0;
   return c;
 }
 
@@ -386,7 +387,7 @@ constexpr int64_t kGemmWsBytes = int64_t(8) << 22;  // the library's split-K sla
 // every size a kernel indexes by is checked here: the kernels trust them (an undersized
 // support array would be an out-of-bounds device read)
 dstagnn_graph graph_of(at::TensorList graph, bool sparse, int64_t K, int64_t N) {
-  TORCH_CHECK(graph.size() == 2 || graph.size() == 6 || graph.size() == 12, "graph: 2, 6 or 12 tensors");
+  TORCH_CHECK(graph.size() == 2 || graph.size() == 6 || graph.size() == 15, "graph: 2, 6 or 15 tensors");
   dstagnn_graph g{};
   check_dev(graph[0], at::kFloat, "cheb");
   check_dev(graph[1], at::kFloat, "adj_pa");
@@ -403,8 +404,9 @@ dstagnn_graph graph_of(at::TensorList graph, bool sparse, int64_t K, int64_t N) 
     g.csc_ptr = graph[2].data_ptr<int>(); g.csc_row = graph[3].data_ptr<int>();
     g.csr_ptr = graph[4].data_ptr<int>(); g.csr_col = graph[5].data_ptr<int>();
   }
-  if (graph.size() == 12) {  // csr2csc, apa_bits, apa_bits_t, apa_ptr, apa_row, tsupp
+  if (graph.size() == 15) {  // csr2csc, apa_bits, apa_bits_t, apa_ptr, apa_row, tsupp, csc2csr, apa_idx, apa2t
     for (int i = 6; i < 11; ++i) check_dev(graph[i], at::kInt, "flash graph data");
+    for (int i = 12; i < 15; ++i) check_dev(graph[i], at::kInt, "flash graph data");
     check_dev(graph[11], at::kFloat, "tsupp");
     const int64_t nw = (N + 31) / 32;
     TORCH_CHECK(graph[6].numel() == g.nnz, "flash graph data: csr2csc must have nnz entries");
@@ -419,6 +421,15 @@ dstagnn_graph graph_of(at::TensorList graph, bool sparse, int64_t K, int64_t N) 
     g.apa_row = graph[10].data_ptr<int>();
     g.apa_nnz = (int)graph[10].numel();
     g.tsupp = graph[11].data_ptr<float>();
+    // the small-graph arrays (empty for larger graphs: the library then takes the streamed kernels)
+    const bool small = graph[13].numel() > 0;
+    if (small) {
+      TORCH_CHECK(graph[12].numel() == g.nnz && graph[13].numel() == N * N && graph[14].numel() == g.apa_nnz,
+                  "flash graph data: csc2csr (nnz), apa_idx (N,N), apa2t (apa_nnz)");
+      g.csc2csr = graph[12].data_ptr<int>();
+      g.apa_idx = graph[13].data_ptr<int>();
+      g.apa2t = graph[14].data_ptr<int>();
+    }
   }
   TORCH_CHECK(!sparse || g.nnz > 0, "sparse path requested without a CSC/CSR support");
   return g;

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .block_fn import block_call, slots_of, use_flash
+from .block_fn import FLASH_SMALL_N, block_call, slots_of, use_flash
 from .head_fn import DSTAGNNHeadFunction
 from .graph import cheb_polynomial, scaled_Laplacian
 
@@ -127,8 +127,11 @@ def flash_support(cheb_stack, csc_ptr, csc_row, csr_ptr, csr_col, adj_pa):
     """Index data of the fused (flash-style) Chebyshev attention (cheb_flash.hip): csr2csc
     (the CSC position of every CSR entry of the T_k union support), tsupp (K, nnz) = T_k on
     that support in CSC order, the A_pa support as bit rows (apa_bits: row i, bit j) and bit
-    columns (apa_bits_t: column j, bit i), and its CSC (apa_ptr, apa_row).  Built on
-    adj_pa's device."""
+    columns (apa_bits_t: column j, bit i), and its CSC (apa_ptr, apa_row).  For the
+    small-graph kernels (N <= FLASH_SMALL_N) also csc2csr (the inverse of csr2csc), apa_idx
+    (N, N): the A_pa-CSC index of (i, j) or -1, and apa2t (apa_nnz): the union-support CSC
+    position of every A_pa entry or -1 (empty tensors for larger graphs).  Built on adj_pa's
+    device."""
     dev = adj_pa.device
     N = adj_pa.shape[0]
     cp, cr = csc_ptr.to(dev).long(), csc_row.to(dev).long()
@@ -140,8 +143,26 @@ def flash_support(cheb_stack, csc_ptr, csc_row, csr_ptr, csr_col, adj_pa):
     tsupp = cheb_stack.to(dev)[:, cr, ccol].contiguous()
     nz = adj_pa != 0
     apa_ptr, apa_row, _, _ = support_index(nz.unsqueeze(0).cpu())
-    return {"csr2csc": csr2csc, "tsupp": tsupp, "apa_bits": _bits(nz), "apa_bits_t": _bits(nz.t()),
-            "apa_ptr": apa_ptr.to(dev), "apa_row": apa_row.to(dev)}
+    apa_ptr, apa_row = apa_ptr.to(dev), apa_row.to(dev)
+    out = {"csr2csc": csr2csc, "tsupp": tsupp, "apa_bits": _bits(nz), "apa_bits_t": _bits(nz.t()),
+           "apa_ptr": apa_ptr, "apa_row": apa_row}
+    empty = torch.zeros(0, dtype=torch.int32, device=dev)
+    if N <= FLASH_SMALL_N:
+        nnz = cr.numel()
+        csc2csr = torch.empty(nnz, dtype=torch.int64, device=dev)
+        csc2csr[csr2csc.long()] = torch.arange(nnz, device=dev)
+        ap, ar = apa_ptr.long(), apa_row.long()
+        acol = torch.repeat_interleave(torch.arange(N, device=dev), ap[1:] - ap[:-1])
+        apa_idx = torch.full((N, N), -1, dtype=torch.int32, device=dev)
+        apa_idx[ar, acol] = torch.arange(ar.numel(), device=dev, dtype=torch.int32)
+        key = acol * N + ar
+        pos = torch.searchsorted(csc_key, key).clamp(max=max(nnz - 1, 0))
+        hit = (csc_key[pos] == key) if nnz else torch.zeros_like(key, dtype=torch.bool)
+        apa2t = torch.where(hit, pos, torch.full_like(pos, -1)).to(torch.int32)
+        out.update({"csc2csr": csc2csr.to(torch.int32), "apa_idx": apa_idx.contiguous(), "apa2t": apa2t})
+    else:
+        out.update({"csc2csr": empty, "apa_idx": empty, "apa2t": empty})
+    return out
 
 
 class cheb_conv(nn.Module):

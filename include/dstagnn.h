@@ -69,6 +69,7 @@ typedef struct dstagnn_block_dims {
                               scores / softmax / score gradient are never materialised;
                               S tiles are recomputed from Q', K' on the matrix cores    */
   int cheb_nnz;            /* flash path: entries of the union support (== graph nnz)   */
+  int cheb_apa_nnz;        /* flash path, N <= 512: entries of the adj_pa support (== graph apa_nnz) */
 } dstagnn_block_dims;
 
 /* Parameter pointers in state_dict order.  For the first block
@@ -137,6 +138,10 @@ typedef struct dstagnn_graph {
   const int* apa_ptr;          /* (N+1)  CSC of the adj_pa support: per column j ...            */
   const int* apa_row;          /* (apa_nnz) ... the rows i                                     */
   const float* tsupp;          /* (K, nnz) T_k on the union support, CSC order                  */
+  /* flash path on small graphs (N <= 512), else NULL: */
+  const int* csc2csr;          /* (nnz)  CSR position of every CSC entry (inverse of csr2csc)   */
+  const int* apa_idx;          /* (N, N) index of (i, j) in the adj_pa CSC, -1 off the support  */
+  const int* apa2t;            /* (apa_nnz) union-support CSC position of adj_pa entry q, or -1 */
 } dstagnn_graph;
 
 /* Bytes needed for the forward->backward `save` buffer and the per-call scratch. */

@@ -429,10 +429,12 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
 @pytest.mark.parametrize("name,first,B,flash", [
     ("pems04", False, 1, None), ("pems07", False, 1, None), ("gambia", True, 1, None), ("gambia", False, 1, None),
     ("syn", False, 1, None), ("t24", True, 1, None), ("t24", False, 1, None), ("pems08", False, 32, None),
-    # the fused (flash) Chebyshev attention is automatic from N = 1024 (gambia, syn above); forced on
-    # at small N and forced off at a large one, so both paths are held to the oracle everywhere
-    ("pems08", False, 4, True), ("pems08", True, 2, True), ("pems07", False, 2, True), ("t24", False, 2, True),
-    ("gambia", False, 1, False)])
+    # the fused (flash) Chebyshev attention is automatic for N <= 512 (the LDS-staged small-graph
+    # kernels: pems08, pems04, t24 above) and N >= 1024 (gambia, syn: the streamed kernels);
+    # forced on at PEMS07 (N = 883, streamed) and forced off at small and large N, so both
+    # paths are held to the oracle everywhere
+    ("pems07", False, 2, True), ("pems08", False, 4, False), ("pems08", True, 2, False), ("pems04", False, 2, False),
+    ("t24", False, 2, False), ("gambia", False, 1, False)])
 def test_block_vs_oracle_configs(name, first, B, flash):
     """Held against the oracle evaluated in float64 (pems08 at B=32: the bench configuration
     itself).  Bound per tensor: the stated 1e-4 (scaled by max(1, max|ref|)), or twice the
@@ -448,7 +450,7 @@ def test_block_vs_oracle_configs(name, first, B, flash):
 
 
 @pytest.mark.parametrize("name,first,B,flash", [("pems08", False, 32, None), ("pems08", True, 32, None),
-                                                ("pems08", False, 4, True), ("pems07", False, 2, None)])
+                                                ("pems08", False, 4, False), ("pems07", False, 2, None)])
 def test_block_train_mode_vs_oracle_configs(name, first, B, flash):
     """TRAIN mode at the bench's own size (PEMS08 inner block, B=32: the timed path of
     bench.py, both Dropout(0.05) of model/DSTAGNN_my.py:218,221 active at :234,:243): the
@@ -459,6 +461,19 @@ def test_block_train_mode_vs_oracle_configs(name, first, B, flash):
     _need_gpu()
     flips = _run_config_vs_oracle(name, first, B, flash=flash, train=True)
     print(f"train {name} first={first} B={B} flash={flash}: {flips} ReLU decision(s) within rounding of 0")
+
+
+@pytest.mark.parametrize("name,B,flash", [("pems08", 96, True), ("pems07", 66, True)])
+def test_flash_large_batch_vs_oracle(name, B, flash):
+    """The fused Chebyshev attention at a batch in (64, 128] against the fp64 oracle: the
+    large-graph mask-gradient kernel gives every lane two batch elements there (b and b + 64),
+    a lane group no B <= 64 case reaches, and the small-graph kernels sum the batch in one
+    thread.  (A direct flash-vs-unfused comparison is not a sound test: the two paths round
+    the Chebyshev pre-activation differently, so a ReLU decision within rounding of 0 may
+    differ between them — the oracle comparison is ReLU-aware.)"""
+    _need_gpu()
+    flips = _run_config_vs_oracle(name, False, B, flash=flash)
+    print(f"{name} B={B} flash={flash}: {flips} ReLU decision(s) within rounding of 0")
 
 
 BF16_TOL = 3e-2      # bf16-operand GEMM variant: normwise ||err||_2 / ||ref||_2 <= BF16_TOL per tensor
