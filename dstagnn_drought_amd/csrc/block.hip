@@ -75,7 +75,7 @@ struct SaveBufs {
   float *Wqkv, *Wqk, *Wp, *thcat, *Wgf[3], *Wgb[3];
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float *lse, *psupp, *wsupp;  // flash path: column log-sum-exp (B,K,N), P and T o P on the support (B,K,nnz)
-  float *am, *papa;            // small-graph flash: A_pa o M_k (K,N,N), P on the A_pa support (B,K,apa_nnz)
+  float *am, *amt, *papa;      // small-graph flash: A_pa o M_k (K,N,N) and its transpose, P on the A_pa support
   float* conv[3];
   float *G, *tco, *r, *mu_c, *rs_c, *u_et, *mu_et, *rs_et;
 };
@@ -107,6 +107,7 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   s.psupp = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.wsupp = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.am = m.fsmall ? a.take((int64_t)m.K * m.NN) : nullptr;
+  s.amt = m.fsmall ? a.take((int64_t)m.K * m.NN) : nullptr;
   s.papa = m.fsmall ? a.take(std::max<int64_t>(1, (int64_t)m.B * m.K * m.apa_nnz)) : nullptr;
   s.xth = a.take(m.BN * m.KCT);
   s.X = a.take(m.BN * m.CT);
@@ -376,7 +377,7 @@ ChebFl make_fl(const Dims& m, const dstagnn_block_params& p, const dstagnn_graph
   f.apa_ptr = g.apa_ptr; f.apa_row = g.apa_row; f.tsupp = g.tsupp;
   f.lse = s.lse; f.psupp = s.psupp; f.wsupp = s.wsupp;
   if (m.fsmall) {
-    f.am = s.am; f.papa = s.papa; f.apa_nnz = (int)m.apa_nnz; f.apa_idx = g.apa_idx; f.apa2t = g.apa2t;
+    f.am = s.am; f.amt = s.amt; f.papa = s.papa; f.apa_nnz = (int)m.apa_nnz; f.apa_idx = g.apa_idx; f.apa2t = g.apa2t;
   }
   return f;
 }
@@ -587,6 +588,8 @@ struct Fwd {
     if (m.fsmall)  // the dense A_pa o M_k of the small-graph attention kernels (:122)
       for (int k = 0; k < m.K; ++k) {
         add(5, p.mask[k], s.am + (int64_t)k * m.NN, m.NN);
+        pp.seg[pp.nseg - 1].src2 = gr.adj_pa;
+        add(6, p.mask[k], s.amt + (int64_t)k * m.NN, m.NN, m.N);
         pp.seg[pp.nseg - 1].src2 = gr.adj_pa;
       }
     DS_TRY(op_param_prep(pp, q));

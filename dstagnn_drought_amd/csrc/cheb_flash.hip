@@ -358,6 +358,7 @@ unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
 constexpr int kSmallN = 512;         // <= 16 tiles: <= kSmallTPW per wave
 constexpr int kSmallTPW = 4;         // tiles per wave at most (kernels templated on 1..4)
 constexpr int kXs = 36;              // LDS row stride (floats) of a staged (N, 32) operand: 16-B rows
+constexpr int kStripE = 1024;        // sparse entries of one strip staged in LDS (else read from HBM)
 
 // forward: lse_j, P and W = T o P on the T support, P on the A_pa support, for one
 // (b, k, 32-column strip).  The strip's P tile goes through LDS ((32 nt) x 33 floats, dynamic).
@@ -483,21 +484,39 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
   const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
   const float* Kp = Q + a.kd;
   const float* AM = a.am + (int64_t)k * a.N * a.N;
+  const float* AMT = a.amt + (int64_t)k * a.N * a.N;  // transposed: the dQ role's strip is a row strip
   const float* lseb = a.lse + (int64_t)bk * a.N;
   const float* cb = a.cc + (int64_t)bk * a.N;
   const int64_t zb = (int64_t)bk * a.nnz;
   float* Ls = X + NP * kXs;
   float* Cs = Ls + NP;
+  float* Ed = Cs + NP;                            // the strip's sparse entries: dzs values ...
+  int* Ec = reinterpret_cast<int*>(Ed + kStripE);  // ... and their staged-row indices
   const int own = min(st * 32 + l32, a.N - 1);  // this lane's row (dQ) / column (dK) of the strip
-  // final phase: thread -> (4 strip rows, d); their support pointers fetched now
+  // final phase: thread -> (4 strip rows, d); their support pointers fetched now.  The strip's
+  // entries are contiguous in CSR (dQ) / CSC (dK) order: staged in LDS when they fit
   const int d = threadIdx.x & 31;
   const int* ptr = dq ? a.csr_ptr : a.csc_ptr;
+  const int* eidx = dq ? a.csr_col : a.csc_row;
+  const float* edz = (dq ? a.dzs_r : a.dzs) + zb;
   int pb[4], pe[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int row = min(st * 32 + (threadIdx.x >> 5) + 8 * u, a.N - 1);
     pb[u] = ptr[row];
     pe[u] = ptr[row + 1];
+  }
+  const int sbeg = ptr[st * 32], send = ptr[min(st * 32 + 32, a.N)];
+  const bool staged = send - sbeg <= kStripE;
+  int ec[kStripE / 256] = {};
+  float ed[kStripE / 256] = {};
+  if (staged && send > sbeg) {
+#pragma unroll
+    for (int u = 0; u < kStripE / 256; ++u) {
+      const int p = min(sbeg + (int)threadIdx.x + 256 * u, send - 1);
+      ec[u] = eidx[p];
+      ed[u] = edz[p];
+    }
   }
   float bv[16], am[kSmallTiles][16];
   float lse_own = 0.f, c_own = 0.f;
@@ -507,7 +526,7 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
     for (int q = 0; q < kSmallTiles; ++q)
       if (w + 4 * q < nt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) am[q][r] = AM[(int64_t)own * a.N + min((w + 4 * q) * 32 + frag_row(r, h), a.N - 1)];
+        for (int r = 0; r < 16; ++r) am[q][r] = AMT[(int64_t)min((w + 4 * q) * 32 + frag_row(r, h), a.N - 1) * a.N + own];
     stage_rows(Kp, a.ld, a.N, NP, X);
     for (int e = threadIdx.x; e < NP; e += 256) {
       Ls[e] = e < a.N ? lseb[e] : INFINITY;
@@ -524,6 +543,13 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
     stage_rows(Q, a.ld, a.N, NP, X);
   }
   (void)c_own;
+  if (staged) {
+#pragma unroll
+    for (int u = 0; u < kStripE / 256; ++u) {
+      const int p = sbeg + (int)threadIdx.x + 256 * u;
+      if (p < send) { Ec[p - sbeg] = ec[u]; Ed[p - sbeg] = ed[u]; }
+    }
+  }
   __syncthreads();
   floatx16 O = zero16();
 #pragma unroll
@@ -561,13 +587,13 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
     if (row >= a.N) continue;
     const float dense = (red[0][rl][d] + red[1][rl][d]) + (red[2][rl][d] + red[3][rl][d]);
     float sp = 0.f;
-    if (dq) {
-      for (int p = pb[u]; p < pe[u]; ++p) sp = fmaf(a.dzs_r[zb + p], X[a.csr_col[p] * kXs + d], sp);
-      a.dqk[((int64_t)b * a.N + row) * a.ld + k * 32 + d] = (sp - dense) * a.scale;
+    if (staged) {
+      for (int p = pb[u] - sbeg; p < pe[u] - sbeg; ++p) sp = fmaf(Ed[p], X[Ec[p] * kXs + d], sp);
     } else {
-      for (int p = pb[u]; p < pe[u]; ++p) sp = fmaf(a.dzs[zb + p], X[a.csc_row[p] * kXs + d], sp);
-      a.dqk[((int64_t)b * a.N + row) * a.ld + a.kd + k * 32 + d] = (sp - cb[row] * dense) * a.scale;
+      for (int p = pb[u]; p < pe[u]; ++p) sp = fmaf(edz[p], X[eidx[p] * kXs + d], sp);
     }
+    if (dq) a.dqk[((int64_t)b * a.N + row) * a.ld + k * 32 + d] = (sp - dense) * a.scale;
+    else a.dqk[((int64_t)b * a.N + row) * a.ld + a.kd + k * 32 + d] = (sp - cb[row] * dense) * a.scale;
   }
 }
 
@@ -589,9 +615,19 @@ __global__ __launch_bounds__(256) void flash_small_mask_kernel(ChebFl a) {
   }
   const int j = (int)(o % a.N), pt = a.apa2t[q];
   float s = 0.f;
-  for (int b = 0; b < a.B; ++b) {
-    const int64_t bk = (int64_t)b * a.K + k;
-    s += (pt >= 0 ? a.dzs[bk * a.nnz + pt] : 0.f) - a.papa[bk * a.apa_nnz + q] * a.cc[bk * a.N + j];
+  constexpr int kBB = 8;  // batch elements per round of loads (fixed summation order)
+  for (int b0 = 0; b0 < a.B; b0 += kBB) {
+    float dz[kBB], pp[kBB], cv[kBB];
+#pragma unroll
+    for (int u = 0; u < kBB; ++u) {
+      const int64_t bk = (int64_t)min(b0 + u, a.B - 1) * a.K + k;
+      dz[u] = pt >= 0 ? a.dzs[bk * a.nnz + pt] : 0.f;
+      pp[u] = a.papa[bk * a.apa_nnz + q];
+      cv[u] = a.cc[bk * a.N + j];
+    }
+#pragma unroll
+    for (int u = 0; u < kBB; ++u)
+      if (b0 + u < a.B) s += dz[u] - pp[u] * cv[u];
   }
   dM[o] = a.apa[o] * s;
 }
@@ -704,7 +740,7 @@ int op_flash_colc(const ChebFl& a, hipStream_t st) {
 int op_flash_dqk(const ChebFl& a, hipStream_t st) {
   const int nt = (a.N + 31) >> 5;
   if (a.am) {  // small graphs (flash_small): dK' and dQ' strips in one launch
-    const size_t lds = ((size_t)nt * 32 * kXs + 2 * (size_t)nt * 32) * sizeof(float);
+    const size_t lds = ((size_t)nt * 32 * kXs + 2 * (size_t)nt * 32 + 2 * (size_t)kStripE) * sizeof(float);
     const dim3 grid((unsigned)(2 * (int64_t)a.B * a.K * nt));
     switch ((nt + 3) / 4) {  // tiles per wave
 #define DS_DQK(T) case T: DS_TRY(allow_lds(flash_small_dqk_kernel<T>, lds)); \

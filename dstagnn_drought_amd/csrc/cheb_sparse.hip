@@ -59,6 +59,12 @@ __device__ __forceinline__ int64_t xcd_row_block(int on) {
   return (p & 7) * per + (p >> 3);
 }
 
+// The support walks below go kE entries at a time: the batch's row indices in one memory
+// round, then every gathered element of the batch in the next (one round trip per batch and
+// k instead of two per entry — at ~3.6 entries per column the per-entry chain was the cost).
+// Entries past the end of the support repeat the batch's last valid one with weight 0.
+constexpr int kE = 4;
+
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
@@ -74,17 +80,28 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   xth_offsets<kNQ>(a, e0, lane, xo);
   const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csc_ptr[j], p1 = a.csc_ptr[j + 1];
-  for (int k = 0; k < a.K; ++k) {
-    const float* Pk = a.P + ((int64_t)b * a.K + k) * NN;
-    const float* Tk = a.cheb + (int64_t)k * NN;
-    const float* Wk = a.wsupp ? a.wsupp + ((int64_t)b * a.K + k) * a.nnz : nullptr;
-    for (int p = p0; p < p1; ++p) {
-      const int i = a.csc_row[p];
-      const int64_t o = (int64_t)i * a.N + j;
-      const float w = Wk ? Wk[p] : Tk[o] * Pk[o];
-      const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
+  for (int pb = p0; pb < p1; pb += kE) {
+    int rows[kE];
 #pragma unroll
-      for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, xr[xo[q]], acc[q]);
+    for (int e = 0; e < kE; ++e) rows[e] = a.csc_row[min(pb + e, p1 - 1)];
+    for (int k = 0; k < a.K; ++k) {
+      const float* Pk = a.P + ((int64_t)b * a.K + k) * NN;
+      const float* Tk = a.cheb + (int64_t)k * NN;
+      const float* Wk = a.wsupp ? a.wsupp + ((int64_t)b * a.K + k) * a.nnz : nullptr;
+      float w[kE], v[kE][kNQ];
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const int64_t o = (int64_t)rows[e] * a.N + j;
+        const float wv = Wk ? Wk[min(pb + e, p1 - 1)] : Tk[o] * Pk[o];
+        w[e] = pb + e < p1 ? wv : 0.f;
+        const float* xr = a.xth + ((int64_t)b * a.N + rows[e]) * KCT + k * a.C;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) v[e][q] = xr[xo[q]];
+      }
+#pragma unroll
+      for (int e = 0; e < kE; ++e)
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w[e], v[e][q], acc[q]);
     }
   }
   float* orow = a.out + ((int64_t)b * a.N + j) * a.CT;
@@ -95,18 +112,9 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
   }
 }
 
-// the flash path's softmax-backward column terms at the SDDMM (was a separate pass over the
-// compact dW): dzs_ij = P_ij T_ij dW_ij (stored by lane 0), returned for c_j = sum_i dzs_ij
-__device__ __forceinline__ float sddmm_dzs(const ChebSp& a, int b, int k, int p, float dw) {
-  const int64_t o = ((int64_t)b * a.K + k) * a.nnz + p;
-  const float d = a.psupp[o] * (a.tsupp[(int64_t)k * a.nnz + p] * dw);
-  if ((threadIdx.x & 63) == 0) {
-    a.dzs[o] = d;
-    if (a.dzs_r) a.dzs_r[((int64_t)b * a.K + k) * a.nnz + a.csc2csr[p]] = d;
-  }
-  return d;
-}
-
+// SDDMM dW_ij = <xth_i, g_j> on the support.  On the flash path the softmax backward's
+// support terms ride along: dzs_ij = P_ij T_ij dW_ij (also in CSR order for the small-graph
+// kernels) and c_j = sum_i dzs_ij, instead of dW.
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
@@ -129,18 +137,50 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
     for (int k = 0; k < a.K; ++k) {
       float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
       float* dSk = a.dws ? a.dws + ((int64_t)b * a.K + k) * a.nnz : nullptr;
+      const int64_t zk = ((int64_t)b * a.K + k) * a.nnz;
       float csum = 0.f;
-      for (int p = p0; p < p1; ++p) {
-        const int i = a.csc_row[p];
-        const float* xr = a.xth + ((int64_t)b * a.N + i) * KCT + k * a.C;
-        float s = 0.f;
+      for (int pb = p0; pb < p1; pb += kE) {
+        int rows[kE];
 #pragma unroll
-        for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], xr[xo[q]], s);
-        s = wave_sum(s);
-        if (a.dzs) csum += sddmm_dzs(a, b, k, p, s);
-        else if (lane == 0) {
-          if (dSk) dSk[p] = s;
-          else dWk[(int64_t)i * a.N + j] = s;
+        for (int e = 0; e < kE; ++e) rows[e] = a.csc_row[min(pb + e, p1 - 1)];
+        // the flash path's softmax-backward operands of the batch, in the same round
+        float pv[kE] = {}, tv[kE] = {};
+        int rp[kE] = {};
+        if (a.dzs) {
+#pragma unroll
+          for (int e = 0; e < kE; ++e) {
+            const int p = min(pb + e, p1 - 1);
+            pv[e] = a.psupp[zk + p];
+            tv[e] = a.tsupp[(int64_t)k * a.nnz + p];
+            rp[e] = a.dzs_r ? a.csc2csr[p] : 0;
+          }
+        }
+        float v[kE][kNQ];
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          const float* xr = a.xth + ((int64_t)b * a.N + rows[e]) * KCT + k * a.C;
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) v[e][q] = xr[xo[q]];
+        }
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) s = fmaf(g[q], v[e][q], s);
+          s = wave_sum(s);
+          const int p = pb + e;
+          if (p >= p1) break;
+          if (a.dzs) {
+            const float d = pv[e] * (tv[e] * s);
+            csum += d;
+            if (lane == 0) {
+              a.dzs[zk + p] = d;
+              if (a.dzs_r) a.dzs_r[zk + rp[e]] = d;
+            }
+          } else if (lane == 0) {
+            if (dSk) dSk[p] = s;
+            else dWk[(int64_t)rows[e] * a.N + j] = s;
+          }
         }
       }
       if (a.dzs && lane == 0) a.cc[((int64_t)b * a.K + k) * a.N + j] = csum;
@@ -150,6 +190,7 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   for (int k = 0; k < a.K; ++k) {  // long rows: the dot product walks the chunks
     float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
     float* dSk = a.dws ? a.dws + ((int64_t)b * a.K + k) * a.nnz : nullptr;
+    const int64_t zk = ((int64_t)b * a.K + k) * a.nnz;
     float csum = 0.f;
     for (int p = p0; p < p1; ++p) {
       const int i = a.csc_row[p];
@@ -165,8 +206,14 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
         }
       }
       s = wave_sum(s);
-      if (a.dzs) csum += sddmm_dzs(a, b, k, p, s);
-      else if (lane == 0) {
+      if (a.dzs) {
+        const float d = a.psupp[zk + p] * (a.tsupp[(int64_t)k * a.nnz + p] * s);
+        csum += d;
+        if (lane == 0) {
+          a.dzs[zk + p] = d;
+          if (a.dzs_r) a.dzs_r[zk + a.csc2csr[p]] = d;
+        }
+      } else if (lane == 0) {
         if (dSk) dSk[p] = s;
         else dWk[(int64_t)i * a.N + j] = s;
       }
@@ -194,13 +241,28 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
     float acc[kNQ];
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) acc[q] = 0.f;
-    for (int p = p0; p < p1; ++p) {
-      const int j = a.csr_col[p];
-      const int64_t o = (int64_t)i * a.N + j;
-      const float w = Wk ? Wk[a.csr2csc[p]] : Tk[o] * Pk[o];
-      const float* gr = a.g + ((int64_t)b * a.N + j) * a.CT;
+    for (int pb = p0; pb < p1; pb += kE) {
+      int cols[kE], ci[kE];
 #pragma unroll
-      for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w, gr[min(e0 + lane + 64 * q, a.CT - 1)], acc[q]);
+      for (int e = 0; e < kE; ++e) {
+        const int p = min(pb + e, p1 - 1);
+        cols[e] = a.csr_col[p];
+        ci[e] = Wk ? a.csr2csc[p] : 0;
+      }
+      float w[kE], v[kE][kNQ];
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const int64_t o = (int64_t)i * a.N + cols[e];
+        const float wv = Wk ? Wk[ci[e]] : Tk[o] * Pk[o];
+        w[e] = pb + e < p1 ? wv : 0.f;
+        const float* gr = a.g + ((int64_t)b * a.N + cols[e]) * a.CT;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) v[e][q] = gr[min(e0 + lane + 64 * q, a.CT - 1)];
+      }
+#pragma unroll
+      for (int e = 0; e < kE; ++e)
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) acc[q] = fmaf(w[e], v[e][q], acc[q]);
     }
     float* dr = a.dxth + ((int64_t)b * a.N + i) * KCT + k * a.C;
 #pragma unroll

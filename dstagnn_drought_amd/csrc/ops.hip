@@ -1134,8 +1134,12 @@ __global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
         o = ((g.p1 - 1 - j) * 2 * g.p0 + oc) * g.p0 + c;
         break;
       }
-      default:  // elementwise product (A_pa o M_k: the reference's adj_pa.mul(mask[k]), :122)
+      case 5:  // elementwise product (A_pa o M_k: the reference's adj_pa.mul(mask[k]), :122)
         g.dst[i] = v * g.src2[i];
+        continue;
+      default:  // its transpose: (i, j) -> (j, i), N = p0
+        o = (i % g.p0) * g.p0 + i / g.p0;
+        g.dst[o] = v * g.src2[i];
         continue;
     }
     g.dst[o] = v;

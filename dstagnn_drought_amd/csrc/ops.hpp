@@ -79,6 +79,7 @@ struct PackRows {
 //   3 gtu fwd        perm[o][j][c] = w[o][c][j]         p0 = C, p1 = ks
 //   4 gtu bwd        perm[j'][o][c] = w[o][c][ks-1-j']  p0 = C, p1 = ks
 //   5 product        dst[i] = src[i] * src2[i]                          (A_pa o M_k)
+//   6 product^T      dst[(i % p0) * p0 + i / p0] = src[i] * src2[i]     (its transpose, N = p0)
 struct PrepSeg {
   int kind = 0, p0 = 0, p1 = 0, p2 = 0;
   int64_t n = 0;        // source elements
@@ -176,6 +177,7 @@ struct ChebFl {
   float* dmask[DSTAGNN_MAX_K] = {};        // (N,N) each, fully written
   // small graphs (flash_small(N)): the dense A_pa o M_k, P on the A_pa support, the index maps
   const float* am = nullptr;               // (K,N,N) A_pa o M_k (param_prep, every forward)
+  const float* amt = nullptr;              // (K,N,N) its transpose (the dQ' kernel's row strips)
   float* papa = nullptr; int apa_nnz = 0;  // (B,K,apa_nnz) P on the A_pa support (A_pa CSC order)
   const int* apa_idx = nullptr;            // (N,N) A_pa-CSC index or -1
   const int* apa2t = nullptr;              // (apa_nnz) union-support CSC position or -1

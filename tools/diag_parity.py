@@ -1,0 +1,26 @@
+"""Diagnostic: every tensor's error against the fp64 oracle (err / max(1, max|ref|)) for a few
+block configurations, without asserting — for reading how an error scales with the batch and
+which path (fused / unfused Chebyshev attention) carries it.
+usage: python tools/diag_parity.py name:B:flash [...]     e.g. pems07:2:1 pems07:66:0"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import test_gpu_parity as T  # noqa: E402
+
+
+def main():
+    for spec in sys.argv[1:]:
+        name, B, fl = spec.split(":")
+        flash = None if fl == "auto" else bool(int(fl))
+        errs = {}
+        T._run_config_vs_oracle(name, False, int(B), flash=flash, tol=1.0, errs=errs)
+        worst = sorted(errs.items(), key=lambda kv: -kv[1])[:8]
+        print(f"{spec}: " + " ".join(f"{k}={v:.2e}" for k, v in worst), flush=True)
+
+
+if __name__ == "__main__":
+    main()
