@@ -446,13 +446,21 @@ __global__ __launch_bounds__(256) void flash_small_fwd_kernel(ChebFl a) {
 }
 
 // stage rows [0, N) of one (b, k) 32-float block of qk (Q' or K') into LDS X[(32 nt)][kXs]
-// (rows past N zero) — one cooperative round of 16-B loads
+// (rows past N zero) — one cooperative round of 16-B loads: every load is issued before the
+// first LDS store (a load-store loop would wait out one memory round trip per iteration)
+template <int kIt>  // >= NP * 8 / 256
 __device__ __forceinline__ void stage_rows(const float* src, int64_t ld, int N, int NP, float* X) {
-  for (int e = threadIdx.x; e < NP * 8; e += 256) {
-    const int row = e >> 3, c4 = (e & 7) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < N) v = *reinterpret_cast<const float4*>(src + (int64_t)row * ld + c4);
-    *reinterpret_cast<float4*>(X + row * kXs + c4) = v;
+  float4 v[kIt];
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int e = threadIdx.x + 256 * u, row = e >> 3, c4 = (e & 7) * 4;
+    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < N) v[u] = *reinterpret_cast<const float4*>(src + (int64_t)row * ld + c4);
+  }
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int e = threadIdx.x + 256 * u, row = e >> 3, c4 = (e & 7) * 4;
+    if (row < NP) *reinterpret_cast<float4*>(X + row * kXs + c4) = v[u];
   }
 }
 
@@ -527,10 +535,18 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
       if (w + 4 * q < nt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) am[q][r] = AMT[(int64_t)min((w + 4 * q) * 32 + frag_row(r, h), a.N - 1) * a.N + own];
-    stage_rows(Kp, a.ld, a.N, NP, X);
-    for (int e = threadIdx.x; e < NP; e += 256) {
-      Ls[e] = e < a.N ? lseb[e] : INFINITY;
-      Cs[e] = e < a.N ? cb[e] : 0.f;
+    stage_rows<kSmallTiles * 4>(Kp, a.ld, a.N, NP, X);
+    float lv[kSmallTiles / 2 + 1], cv[kSmallTiles / 2 + 1];  // NP <= 128 kSmallTiles
+#pragma unroll
+    for (int u = 0; u <= kSmallTiles / 2; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      lv[u] = e < a.N ? lseb[e] : INFINITY;
+      cv[u] = e < a.N ? cb[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u <= kSmallTiles / 2; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < NP) { Ls[e] = lv[u]; Cs[e] = cv[u]; }
     }
   } else {
     load16(Kp + (int64_t)own * a.ld + h * 16, bv);
@@ -540,7 +556,7 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) am[q][r] = AM[(int64_t)min((w + 4 * q) * 32 + frag_row(r, h), a.N - 1) * a.N + own];
     lse_own = lseb[own];
-    stage_rows(Q, a.ld, a.N, NP, X);
+    stage_rows<kSmallTiles * 4>(Q, a.ld, a.N, NP, X);
   }
   (void)c_own;
   if (staged) {

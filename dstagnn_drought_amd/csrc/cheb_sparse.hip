@@ -115,11 +115,16 @@ __global__ __launch_bounds__(256) void cheb_spmm_fwd_kernel(ChebSp a) {
 // SDDMM dW_ij = <xth_i, g_j> on the support.  On the flash path the softmax backward's
 // support terms ride along: dzs_ij = P_ij T_ij dW_ij (also in CSR order for the small-graph
 // kernels) and c_j = sum_i dzs_ij, instead of dW.
+// One wave per (b, j, k) on the one-pass path (K x the waves of a (b, j) walk: the walk is a
+// latency chain, so more, shorter chains in flight); per (b, j) on the chunked path.
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = xcd_row_block(a.xcd_order) * 4 + (threadIdx.x >> 6);
-  if (wv >= (int64_t)a.B * a.N) return;
+  const int64_t wv0 = xcd_row_block(a.xcd_order) * 4 + (threadIdx.x >> 6);
+  const bool per_k = a.CT <= kChunk;
+  if (wv0 >= (int64_t)a.B * a.N * (per_k ? a.K : 1)) return;
+  const int kk = per_k ? (int)(wv0 % a.K) : 0;
+  const int64_t wv = per_k ? wv0 / a.K : wv0;
   const int b = (int)(wv / a.N), j = (int)(wv % a.N);
   const int64_t NN = (int64_t)a.N * a.N;
   const float* grow = a.g + ((int64_t)b * a.N + j) * a.CT;
@@ -134,7 +139,8 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
     }
     int xo[kNQ];
     xth_offsets<kNQ>(a, 0, lane, xo);
-    for (int k = 0; k < a.K; ++k) {
+    {
+      const int k = kk;
       float* dWk = a.dW + ((int64_t)b * a.K + k) * NN;
       float* dSk = a.dws ? a.dws + ((int64_t)b * a.K + k) * a.nnz : nullptr;
       const int64_t zk = ((int64_t)b * a.K + k) * a.nnz;
@@ -222,11 +228,14 @@ __global__ __launch_bounds__(256) void cheb_sddmm_bwd_kernel(ChebSp a) {
   }
 }
 
+// one wave per (b, i, k): every k writes its own slice of dxth
 template <int kNQ>
 __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wv = xcd_row_block(a.xcd_order) * 4 + (threadIdx.x >> 6);
-  if (wv >= (int64_t)a.B * a.N) return;
+  const int64_t wv0 = xcd_row_block(a.xcd_order) * 4 + (threadIdx.x >> 6);
+  if (wv0 >= (int64_t)a.B * a.N * a.K) return;
+  const int kk = (int)(wv0 % a.K);
+  const int64_t wv = wv0 / a.K;
   const int b = (int)(wv / a.N), i = (int)(wv % a.N);
   const int e0 = blockIdx.y * kChunk;
   const int64_t NN = (int64_t)a.N * a.N;
@@ -234,7 +243,8 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
   xth_offsets<kNQ>(a, e0, lane, xo);
   const int64_t KCT = (int64_t)a.K * a.CT;
   const int p0 = a.csr_ptr[i], p1 = a.csr_ptr[i + 1];
-  for (int k = 0; k < a.K; ++k) {
+  {
+    const int k = kk;
     const float* Pk = a.P + ((int64_t)b * a.K + k) * NN;
     const float* Tk = a.cheb + (int64_t)k * NN;
     const float* Wk = a.wsupp ? a.wsupp + ((int64_t)b * a.K + k) * a.nnz : nullptr;
@@ -278,10 +288,10 @@ __global__ __launch_bounds__(256) void cheb_spmm_t_bwd_kernel(ChebSp a) {
 bool cheb_sparse_ok(int CT) { return CT > 0 && CT <= (1 << 20); }
 
 namespace {
-#define DS_NQ_DISPATCH(KER, a, st, CHUNKED)                                                        \
+#define DS_NQ_DISPATCH(KER, a, st, CHUNKED, WPR)                                                   \
   do {                                                                                             \
     const int nq = (int)cdiv64(std::min((a).CT, kChunk), 64);                                      \
-    const dim3 grid((unsigned)(cdiv64(cdiv64((int64_t)(a).B * (a).N, 4), 8) * 8),                   \
+    const dim3 grid((unsigned)(cdiv64(cdiv64((int64_t)(a).B * (a).N * (WPR), 4), 8) * 8),           \
                     (CHUNKED) ? (unsigned)cdiv64((a).CT, kChunk) : 1u);                            \
     if (nq <= 1) hipLaunchKernelGGL(KER<1>, grid, dim3(256), 0, st, a);                            \
     else if (nq <= 2) hipLaunchKernelGGL(KER<2>, grid, dim3(256), 0, st, a);                       \
@@ -303,19 +313,19 @@ ChebSp with_xcd_order(const ChebSp& a0) {
 
 int op_cheb_spmm_fwd(const ChebSp& a0, hipStream_t st) {
   const ChebSp a = with_xcd_order(a0);
-  DS_NQ_DISPATCH(cheb_spmm_fwd_kernel, a, st, true);
+  DS_NQ_DISPATCH(cheb_spmm_fwd_kernel, a, st, true, 1);
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_cheb_sddmm_bwd(const ChebSp& a0, hipStream_t st) {
   const ChebSp a = with_xcd_order(a0);
-  DS_NQ_DISPATCH(cheb_sddmm_bwd_kernel, a, st, false);
+  DS_NQ_DISPATCH(cheb_sddmm_bwd_kernel, a, st, false, (a.CT <= kChunk ? a.K : 1));
   DS_CHECK_LAUNCH();
   return 0;
 }
 int op_cheb_spmm_t_bwd(const ChebSp& a0, hipStream_t st) {
   const ChebSp a = with_xcd_order(a0);
-  DS_NQ_DISPATCH(cheb_spmm_t_bwd_kernel, a, st, true);
+  DS_NQ_DISPATCH(cheb_spmm_t_bwd_kernel, a, st, true, a.K);
   DS_CHECK_LAUNCH();
   return 0;
 }

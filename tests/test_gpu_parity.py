@@ -358,7 +358,7 @@ def _train_seed():
 
 
 def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=RELU_EPS, errs=None, normwise=False,
-                          train=False):
+                          train=False, owns=None):
     import dstagnn_drought_amd as D_
     from dstagnn_drought_amd.block_fn import dropout_masks
     N, T, K, h, D, dk, C = CONFIGS[name]
@@ -407,6 +407,8 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
         err = float(d.abs().max())
         if errs is not None:
             errs[key] = err / scale
+        if owns is not None:
+            owns[key] = own / scale
         assert err <= bound, f"{name} {key}: max err {err:.3e} > bound {bound:.3e} (fp32 reference's own {own:.3e})"
 
     if train:

@@ -16,10 +16,10 @@ def main():
     for spec in sys.argv[1:]:
         name, B, fl = spec.split(":")
         flash = None if fl == "auto" else bool(int(fl))
-        errs = {}
-        T._run_config_vs_oracle(name, False, int(B), flash=flash, tol=1.0, errs=errs)
+        errs, owns = {}, {}
+        T._run_config_vs_oracle(name, False, int(B), flash=flash, tol=1.0, errs=errs, owns=owns)
         worst = sorted(errs.items(), key=lambda kv: -kv[1])[:8]
-        print(f"{spec}: " + " ".join(f"{k}={v:.2e}" for k, v in worst), flush=True)
+        print(f"{spec}: " + " ".join(f"{k}={v:.2e}(own {owns.get(k, 0):.1e})" for k, v in worst), flush=True)
 
 
 if __name__ == "__main__":
