@@ -185,14 +185,21 @@ bool gemm_log_on() {
 
 struct Plan {
   GemmK k;
-  char log[200];
+  char log[220];
   int best, va, vb, ns;
-  bool akc, bnc, ktwo, hot;
+  bool akc, bnc, ktwo, hot, acc2;
   bool same_kernel(const Plan& o) const {
     return best == o.best && va == o.va && vb == o.vb && ns == o.ns && akc == o.akc && bnc == o.bnc &&
-           ktwo == o.ktwo && hot == o.hot;
+           ktwo == o.ktwo && hot == o.hot && acc2 == o.acc2;
   }
 };
+
+// a workgroup reducing more than this many k in one fp32 chain takes the two-level
+// accumulation (gemm_kern.hpp ACC2); DSTAGNN_GEMM_ACC2_MINK overrides
+int acc2_min_k() {
+  static const int v = getenv("DSTAGNN_GEMM_ACC2_MINK") ? atoi(getenv("DSTAGNN_GEMM_ACC2_MINK")) : 1024;
+  return v;
+}
 
 // Plan one problem (tile shape, split-K, DMA widths, stages); ws: its split-K slab space.
 int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
@@ -273,6 +280,7 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   while (k.red_g < 64 && k.red_g * 8 < splitk) k.red_g *= 2;
 
   pl.best = best;
+  pl.acc2 = !g_bf16 && (best == 0 || best == 2) && kchunk > acc2_min_k();
   pl.akc = !g.ak.two && g.ak.s0 == 1;
   pl.bnc = !g.bn.two && g.bn.s0 == 1;
   pl.ktwo = g.ak.two || g.bk.two;
@@ -286,9 +294,9 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   k.nstage = pl.ns;
   if (gemm_log_on()) {
     // one "[gemm]" line per kernel launch (run_gemm_group joins a group's problems with " | ")
-    snprintf(pl.log, sizeof(pl.log), "M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d bf=%d ones=%d",
+    snprintf(pl.log, sizeof(pl.log), "M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d bf=%d ones=%d acc2=%d",
              g.M, Nk, g.K, g.batch, best, splitk, (int)pl.akc, (int)pl.bnc, (int)pl.ktwo, (long long)blocks * splitk,
-             pl.ns, pl.va, pl.vb, g_bf16, g.ones_out ? 1 : 0);
+             pl.ns, pl.va, pl.vb, g_bf16, g.ones_out ? 1 : 0, (int)pl.acc2);
   }
   return 0;
 }
@@ -313,11 +321,13 @@ void launch_plans(Plan* const* ps, int n, hipStream_t st) {
   GemmG gg;
   const uint32_t grid = make_group(ks, counts, n, &gg);
   using Unit = void (*)(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
-  static const Unit units[2][3][2] = {
+  static const Unit units[3][3][2] = {
       {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}},
-      {{gemm_c0_k0_bf, gemm_c0_k1_bf}, {gemm_c1_k0_bf, gemm_c1_k1_bf}, {gemm_c2_k0_bf, gemm_c2_k1_bf}}};
+      {{gemm_c0_k0_bf, gemm_c0_k1_bf}, {gemm_c1_k0_bf, gemm_c1_k1_bf}, {gemm_c2_k0_bf, gemm_c2_k1_bf}},
+      {{gemm_c0_k0_a2, gemm_c0_k1_a2}, {nullptr, nullptr}, {gemm_c2_k0_a2, gemm_c2_k1_a2}}};
   const Plan& pl = *ps[0];
-  units[g_bf16 ? 1 : 0][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, pl.hot, st);
+  const int var = pl.acc2 ? 2 : (g_bf16 ? 1 : 0);
+  units[var][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, pl.hot, st);
 }
 
 }  // namespace

@@ -58,6 +58,13 @@ namespace {
 
 constexpr int BKMAX = 32;  // k-tile depth
 
+__device__ __forceinline__ floatx16 zero_acc() {
+  floatx16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
 // The problem of this workgroup and its descriptor, in one memory round: every lane loads
 // dwords lane, lane+64, ... of the whole group argument, the slice starts come back by
 // readlane, and the selected problem's dwords by readlane from compile-time positions (one
@@ -323,7 +330,12 @@ __device__ __forceinline__ void img_rk(int p, int& row, int& k) {
   }
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
+// ACC2: two-level fp32 accumulation for long reductions — each k-tile's 32 products go into a
+// fresh tile accumulator, which is then added to the running one, so no fp32 chain is longer
+// than 32 + K/32 additions (a single MFMA chain over K = 5.8K lost 1e-3 of a cancelling weight
+// gradient against the fp64 oracle).  +16 VGPRs per accumulator: only for long K per workgroup.
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false,
+          bool ACC2 = false>
 __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   constexpr int BK = 32;
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
@@ -522,6 +534,23 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
 #pragma unroll
         for (int j = 0; j < WN; ++j) read_b(j, q, bv[q][j]);
       }
+      if constexpr (ACC2) {
+        floatx16 tacc[WM][WN];
+#pragma unroll
+        for (int q = 0; q < BK / 8; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+              for (int j = 0; j < WN; ++j)
+                tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q][i][c], bv[q][j][c],
+                                                                 (q | c) ? tacc[i][j] : zero_acc(), 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) acc[i][j] += tacc[i][j];
+      } else {
 #pragma unroll
       for (int q = 0; q < BK / 8; ++q)
 #pragma unroll
@@ -531,6 +560,7 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
 #pragma unroll
             for (int j = 0; j < WN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q][i][c], bv[q][j][c], acc[i][j], 0, 0, 0);
+      }
       // software-pipeline the k-tile by one step: the reads of steps 0 and 1, then the MFMAs of
       // step q beside the reads of step q + 2 (DS reads per step: b128 per row-major operand,
       // two read2 pairs per column-major one)
@@ -560,9 +590,10 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false,
+          bool ACC2 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void gemm_f32_kernel(GemmG g) {
-  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
+  gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT, ACC2>(g);
 }
 // same code under a second name: the GEMM a profile reports as "the hot kernel" (Gemm::hot)
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
@@ -571,11 +602,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
 }
 }  // namespace
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false,
+          bool ACC2 = false>
 void launch_one(const GemmG& k, dim3 grid, bool hot, hipStream_t st) {
   // the "hot" name exists for the one GEMM it tags (pre_conv forward: 64x64, single-level k, fp32)
-  constexpr bool HOT_OK = WGM == 2 && WGN == 2 && WM == 1 && WN == 1 && !KTWO && !BF && !KCAT;
-  auto ker = gemm_f32_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>;
+  constexpr bool HOT_OK = WGM == 2 && WGN == 2 && WM == 1 && WN == 1 && !KTWO && !BF && !KCAT && !ACC2;
+  auto ker = gemm_f32_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT, ACC2>;
   if constexpr (HOT_OK) {
     if (hot) ker = gemm_f32_hot_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>;
   }
@@ -587,18 +619,18 @@ void launch_one(const GemmG& k, dim3 grid, bool hot, hipStream_t st) {
 constexpr bool kcat_supported(int wgm, int wgn, int wm, int wn, bool ktwo) {
   return wgm == 4 && wgn == 1 && wm == 1 && wn == 1 && !ktwo;
 }
-template <int WGM, int WGN, int WM, int WN, bool KTWO, bool BF>
+template <int WGM, int WGN, int WM, int WN, bool KTWO, bool BF, bool ACC2 = false>
 void launch_cfg(const GemmG& kk, dim3 grid, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {
   if (kk.start[0] > 0) {  // K-concatenated (run_gemm_kcat checked kcat_ok)
-    if constexpr (kcat_supported(WGM, WGN, WM, WN, KTWO))
+    if constexpr (kcat_supported(WGM, WGN, WM, WN, KTWO) && !ACC2)
       launch_one<WGM, WGN, WM, WN, true, true, KTWO, 4, 4, BF, true>(kk, grid, false, st);
     return;
   }
 #define DS_V(AK, BN_)                                                                                        \
-  if (va == 4 && vb == 4)  launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4, BF>(kk, grid, hot, st);              \
-  else if (va == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1, BF>(kk, grid, hot, st);              \
-  else if (vb == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 4, BF>(kk, grid, hot, st);              \
-  else                     launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 1, BF>(kk, grid, hot, st);
+  if (va == 4 && vb == 4)  launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4, BF, false, ACC2>(kk, grid, hot, st); \
+  else if (va == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1, BF, false, ACC2>(kk, grid, hot, st); \
+  else if (vb == 4)        launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 4, BF, false, ACC2>(kk, grid, hot, st); \
+  else                     launch_one<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 1, BF, false, ACC2>(kk, grid, hot, st);
   if (akc && bnc) { DS_V(true, true) }
   else if (akc)   { DS_V(true, false) }
   else if (bnc)   { DS_V(false, true) }
@@ -610,6 +642,11 @@ void launch_cfg(const GemmG& kk, dim3 grid, bool akc, bool bnc, int va, int vb, 
 #define DS_GEMM_UNIT(NAME, WGM, WGN, WM, WN, KTWO, BF)                                                   \
   void NAME(const GemmG& k, dim3 grid, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {  \
     launch_cfg<WGM, WGN, WM, WN, KTWO, BF>(k, grid, akc, bnc, va, vb, hot, st);                          \
+  }
+// the two-level-accumulation variants (fp32, the tiles split-K uses: 64x64 and 128x32)
+#define DS_GEMM_UNIT_ACC2(NAME, WGM, WGN, WM, WN, KTWO)                                                  \
+  void NAME(const GemmG& k, dim3 grid, bool akc, bool bnc, int va, int vb, bool hot, hipStream_t st) {  \
+    launch_cfg<WGM, WGN, WM, WN, KTWO, false, true>(k, grid, akc, bnc, va, vb, hot, st);                 \
   }
 void gemm_c0_k0(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 void gemm_c0_k1(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
@@ -623,5 +660,9 @@ void gemm_c1_k0_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 void gemm_c1_k1_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 void gemm_c2_k0_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 void gemm_c2_k1_bf(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k0_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c0_k1_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k0_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_c2_k1_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 
 }  // namespace dsgemm
