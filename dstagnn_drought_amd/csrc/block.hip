@@ -1199,11 +1199,12 @@ int dstagnn_block_sizes(const dstagnn_block_dims* d, size_t* save_bytes, size_t*
 
 int dstagnn_block_save_offset(const dstagnn_block_dims* d, int which, size_t* offset_bytes, size_t* count) {
   DS_TRY(check_dims(d));
-  if (!offset_bytes || !count || which != 0) return DSTAGNN_E_ARG;
+  if (!offset_bytes || !count || which < 0 || which > 2) return DSTAGNN_E_ARG;
   const Dims m = mkdims(*d);
   Arena a((void*)(uintptr_t)256);  // the forward carves the 256-aligned save buffer the same way
   SaveBufs s = plan_save(m, a);
-  *offset_bytes = (size_t)((char*)s.X - (char*)(uintptr_t)256);
+  const float* t = which == 0 ? s.X : (which == 1 ? s.tco : s.r);
+  *offset_bytes = (size_t)((const char*)t - (char*)(uintptr_t)256);
   *count = (size_t)(m.BN * m.CT);
   return 0;
 }

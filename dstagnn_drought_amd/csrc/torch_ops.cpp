@@ -326,16 +326,23 @@ std::tuple<Tensor, Tensor, Tensor> block_bwd(const Tensor& x, const c10::optiona
   return {r.dx, r.dres.defined() ? r.dres : at::empty({0}, f32(x)), r.flat};
 }
 
-// the Chebyshev output X (B,N,T,C) the forward keeps in `save` (parity tests: its sign
-// pattern is the ReLU decision of model/DSTAGNN_my.py:133)
-Tensor block_cheb_out(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params, at::IntArrayRef slots,
-                      at::TensorList graph, at::IntArrayRef cfg, double drop_p, int64_t seed, int64_t flags) {
+// a ReLU output the forward keeps in `save` (parity tests: its sign pattern is that ReLU's
+// decision): which 0 = the Chebyshev output X (B,N,T,C) (model/DSTAGNN_my.py:133), 1 = tco
+// (B,N,C,T) (:245/:247), 2 = ReLU(residual + tco) (B,N,C,T) (:252)
+Tensor block_relu_out(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params, at::IntArrayRef slots,
+                      at::TensorList graph, at::IntArrayRef cfg, double drop_p, int64_t seed, int64_t flags,
+                      int64_t which) {
   BlockCall c = make_call(x, res, params, slots, graph, cfg, drop_p, seed, flags);
   auto [out, re_at, save] = run_forward(c, x, res);
   size_t off = 0, n = 0;
-  check_rc(dstagnn_block_save_offset(&c.d, 0, &off, &n), "dstagnn_block_save_offset");
+  check_rc(dstagnn_block_save_offset(&c.d, (int)which, &off, &n), "dstagnn_block_save_offset");
   const int64_t base = (int64_t)((256 - ((uintptr_t)save.data_ptr() & 255)) & 255);  // the library's align256
-  return save.narrow(0, base + (int64_t)off, (int64_t)n * 4).view(at::kFloat).view({c.d.B, c.d.N, c.d.T, c.d.C}).clone();
+  Tensor t = save.narrow(0, base + (int64_t)off, (int64_t)n * 4).view(at::kFloat);
+  return (which == 0 ? t.view({c.d.B, c.d.N, c.d.T, c.d.C}) : t.view({c.d.B, c.d.N, c.d.C, c.d.T})).clone();
+}
+Tensor block_cheb_out(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params, at::IntArrayRef slots,
+                      at::TensorList graph, at::IntArrayRef cfg, double drop_p, int64_t seed, int64_t flags) {
+  return block_relu_out(x, res, params, slots, graph, cfg, drop_p, seed, flags, 0);
 }
 
 // HIP-event timing of one block stage (dstagnn_block_time_stage) after one forward:
@@ -702,6 +709,7 @@ TORCH_LIBRARY(dstagnn, m) {
         "int[] slots, Tensor[] graph, int[] cfg, float drop_p, int seed, int flags) -> (Tensor, Tensor, Tensor)");
   m.def("block_time_stage(" DSTAGNN_BLK_ARGS ", int stage, int iters) -> float");
   m.def("block_cheb_out(" DSTAGNN_BLK_ARGS ") -> Tensor");
+  m.def("block_relu_out(" DSTAGNN_BLK_ARGS ", int which) -> Tensor");
 #undef DSTAGNN_BLK_ARGS
   m.def("dropout_masks(Tensor like, int[] shape, int[] cfg, float drop_p, int seed) -> (Tensor, Tensor)");
   m.def("cheb_sat_fwd(Tensor x, Tensor sat, Tensor theta_cat, Tensor mask_cat, Tensor[] graph, int C, bool sparse) "
@@ -734,6 +742,7 @@ TORCH_LIBRARY_IMPL(dstagnn, CUDA, m) {
   m.impl("block_time_stage", block_time_stage);
   m.impl("dropout_masks", dropout_masks);
   m.impl("block_cheb_out", block_cheb_out);
+  m.impl("block_relu_out", block_relu_out);
   m.impl("cheb_sat_fwd", cheb_sat_fwd);
   m.impl("cheb_sat_bwd", cheb_sat_bwd);
   m.impl("gemm_f32", gemm_f32);

@@ -156,10 +156,11 @@ int dstagnn_block_forward(const dstagnn_block_dims* d, const dstagnn_block_param
                           dstagnn_stream_t stream);
 
 /* Introspection for parity tests: byte offset (from the 256-aligned start of `save`) and
- * element count of a tensor the forward keeps in `save`.  which = 0: the Chebyshev output
- * X = ReLU(cheb_conv_withSAt pre-activation), layout (B,N,T,C) — its sign pattern is the
- * ReLU decision of :133, which an fp64 oracle can adopt where the pre-activation is within
- * rounding of 0. */
+ * element count of a tensor the forward keeps in `save`; the sign pattern of each is one of
+ * the block's ReLU decisions, which an fp64 oracle can adopt where the pre-activation is
+ * within rounding of 0.  which = 0: the Chebyshev output X = ReLU(cheb_conv_withSAt
+ * pre-activation), layout (B,N,T,C) (:133); 1: tco = ReLU(X + tc) (first block ReLU(tc)),
+ * layout (B,N,C,T) (:245/:247); 2: ReLU(residual + tco), layout (B,N,C,T) (:252). */
 int dstagnn_block_save_offset(const dstagnn_block_dims* d, int which, size_t* offset_bytes, size_t* count);
 
 /* Autograd backward of the block (replaces torch autograd over :225-253).

@@ -139,12 +139,15 @@ def gtu(p, name, X, k):
 
 
 def block_forward(p, x, res_att, cheb, adj_pa, dims, train=False, drop_masks=None, hoist=False, relu_mask=None,
-                  pre_out=None):
+                  pre_out=None, tail_masks=None):
     """DSTAGNN_block.forward (:225-253).  Returns (x_out (B,N,C,T), re_At (B,F,h,T,T)).
 
     dims: dict(n_heads, d_k, d_v, K).  train=True applies the two Dropout(0.05)
     (:218,:221) using drop_masks=(mask_S (B,N,D), mask_T (B,C,N,T)) already scaled by
-    1/(1-p), so a test can inject the exact masks the HIP path drew."""
+    1/(1-p), so a test can inject the exact masks the HIP path drew.
+    relu_mask / tail_masks (parity tests): the decisions of the ReLUs at :133 (see
+    cheb_conv_sat) and at :245/:247 and :252 ((B,C,N,T) each) taken from the implementation
+    under test instead of z > 0; pre_out also receives their pre-activations "z_tco", "z_r"."""
     B, N, Fd, T = x.shape
     h, dk, dv, K = dims["n_heads"], dims["d_k"], dims["d_v"], dims["K"]
     if Fd == 1:
@@ -166,13 +169,19 @@ def block_forward(p, x, res_att, cheb, adj_pa, dims, train=False, drop_masks=Non
     tc = tc @ p["fcmy.0.weight"].t() + p["fcmy.0.bias"]                 # :243
     if train and drop_masks is not None:
         tc = tc * drop_masks[1]
+    relu = (lambda z, m: z * m.to(z.dtype)) if tail_masks is not None else (lambda z, m: F.relu(z))  # noqa: E731
     if Fd == 1:
-        tco = F.relu(tc)                                                # :245
+        z_tco = tc                                                      # :245
         xres = F.conv2d(x.permute(0, 2, 1, 3), p["residual_conv.weight"], p["residual_conv.bias"])  # :249
     else:
-        tco = F.relu(X + tc)                                            # :247
+        z_tco = X + tc                                                  # :247
         xres = x.permute(0, 2, 1, 3)                                    # :251
-    out = layer_norm(F.relu(xres + tco).permute(0, 3, 2, 1), p["ln.weight"], p["ln.bias"]).permute(0, 2, 3, 1)  # :252
+    tco = relu(z_tco, tail_masks[0] if tail_masks is not None else None)
+    z_r = xres + tco
+    if pre_out is not None:
+        pre_out["z_tco"], pre_out["z_r"] = z_tco.detach(), z_r.detach()
+    out = layer_norm(relu(z_r, tail_masks[1] if tail_masks is not None else None).permute(0, 3, 2, 1),
+                     p["ln.weight"], p["ln.bias"]).permute(0, 2, 3, 1)  # :252
     return out, re_at
 
 
@@ -207,15 +216,15 @@ def split_state_dict(sd, nb_block):
 
 
 def block_forward_backward(p, x, res_att, cheb, adj_pa, dims, g_out, g_re, hoist=True, relu_mask=None, pre_out=None,
-                           train=False, drop_masks=None):
+                           train=False, drop_masks=None, tail_masks=None):
     """Forward + autograd backward of one block with upstream grads (g_out, g_re).
     Returns (out, re_at, grad_x, grad_res_att or None, {param_name: grad or None}).
-    relu_mask / pre_out: see cheb_conv_sat; train / drop_masks: see block_forward."""
+    relu_mask / pre_out: see cheb_conv_sat; train / drop_masks / tail_masks: see block_forward."""
     pp = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
     xx = x.detach().clone().requires_grad_(True)
     ra = res_att.detach().clone().requires_grad_(True) if torch.is_tensor(res_att) else res_att
     out, re_at = block_forward(pp, xx, ra, cheb, adj_pa, dims, train=train, drop_masks=drop_masks, hoist=hoist,
-                               relu_mask=relu_mask, pre_out=pre_out)
+                               relu_mask=relu_mask, pre_out=pre_out, tail_masks=tail_masks)
     loss = (out * g_out).sum()
     if g_re is not None:
         loss = loss + (re_at * g_re).sum()

@@ -44,7 +44,7 @@ def test_library_exports_header_symbols():
 
 OPS = ["block", "block_fwd", "block_bwd", "block_time_stage", "dropout_masks", "cheb_sat_fwd", "cheb_sat_bwd",
        "gemm_f32", "head_fwd", "head_bwd", "stag_prep", "stag_emd_pairs", "stag_emd_lds_bytes", "emd_dense",
-       "fast_stag_distances", "graph_topk", "version", "block_cheb_out", "prof_start", "prof_stop",
+       "fast_stag_distances", "graph_topk", "version", "block_cheb_out", "block_relu_out", "prof_start", "prof_stop",
        "set_splitk_target", "set_gemm_bf16"]
 
 

@@ -245,10 +245,10 @@ def test_block_vs_oracle_pems08_geometry(first, res_kind, sparse):
     blk.sparse_cheb = sparse
     xg = x.cuda().requires_grad_(True)
     rg = res.cuda().requires_grad_(True) if torch.is_tensor(res) else 0
-    mask = hip_cheb_relu_mask(blk, xg, rg)
-    relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask, "pems08-geometry")
+    masks = hip_relu_masks(blk, xg, rg)
+    relu_aware_mask(ref, p, x, res, cheb, apa, dims, masks, "pems08-geometry")
     out_r, re_r, gx_r, gra_r, grads_r = ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re,
-                                                                   relu_mask=mask)
+                                                                   relu_mask=masks[0], tail_masks=masks[1:])
     out, re_at = blk(xg, rg)
     close(out, out_r, what="out")
     close(re_at, re_r, what="re_at")
@@ -310,10 +310,11 @@ CONFIGS = {
 RELU_EPS = 1e-5  # ReLU decisions may differ from the fp64 oracle's only where |z| <= RELU_EPS * max|z|
 
 
-def hip_cheb_relu_mask(blk, x, res, train=False, seed=0):
-    """(B,N,C,T) bool: the HIP forward's ReLU decisions at model/DSTAGNN_my.py:133 (X > 0 of
-    the Chebyshev output the forward keeps, dstagnn::block_cheb_out); train=True with the
-    dropout seed of the run under test (the EmbedS dropout feeds the spatial attention)."""
+def hip_relu_masks(blk, x, res, train=False, seed=0):
+    """The HIP forward's decisions at the block's three ReLUs (dstagnn::block_relu_out: the
+    sign patterns of the ReLU outputs the forward keeps): model/DSTAGNN_my.py:133 (the
+    Chebyshev output, (B,N,C,T) like the oracle's z), :245/:247 and :252 ((B,C,N,T), the
+    oracle's tail layout).  train=True with the dropout seed of the run under test."""
     from dstagnn_drought_amd import _lib, block_fn as bf
     names, ps, slots = blk._param_list()
     graph = blk._graph()
@@ -321,30 +322,53 @@ def hip_cheb_relu_mask(blk, x, res, train=False, seed=0):
     fl = bf.use_flash(graph, blk.meta, x.shape[3], blk.flash_cheb, x.shape[0])
     if fl:
         graph = blk._flash_graph(graph)
-    X = _lib.load().block_cheb_out(x.detach().float().contiguous(), bf.res_arg(res, x.shape[2]), list(ps), slots,
-                                   bf.graph_list(graph, sparse, fl), bf.cfg_of(blk.meta), 0.05, int(seed),
-                                   bf.flags_of(train, sparse, False, fl))
-    return (X > 0).permute(0, 1, 3, 2).contiguous().cpu()
+    args = (x.detach().float().contiguous(), bf.res_arg(res, x.shape[2]), list(ps), slots,
+            bf.graph_list(graph, sparse, fl), bf.cfg_of(blk.meta), 0.05, int(seed), bf.flags_of(train, sparse, False, fl))
+    ops = _lib.load()
+    X = ops.block_relu_out(*args, 0)
+    tco = ops.block_relu_out(*args, 1)
+    r = ops.block_relu_out(*args, 2)
+    return ((X > 0).permute(0, 1, 3, 2).contiguous().cpu(), (tco > 0).permute(0, 2, 1, 3).contiguous().cpu(),
+            (r > 0).permute(0, 2, 1, 3).contiguous().cpu())
+
+
+def hip_cheb_relu_mask(blk, x, res, train=False, seed=0):
+    """(B,N,C,T) bool: the HIP forward's ReLU decisions at model/DSTAGNN_my.py:133."""
+    return hip_relu_masks(blk, x, res, train, seed)[0]
 
 
 def relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask_hip, what, eps=RELU_EPS, drop_masks=None):
     """Check that the HIP's ReLU decisions differ from the fp64 oracle's only where the fp64
     pre-activation is within RELU_EPS * scale of 0; returns the number of such flips (the
     oracle then evaluates with the HIP's decisions, so a flip cannot fail the value checks
-    and a kernel bug cannot hide behind one).  drop_masks: train mode with these masks."""
+    and a kernel bug cannot hide behind one).  mask_hip: the :133 decisions, or the triple of
+    hip_relu_masks (then the tail ReLUs :245/:247 and :252 are checked the same way, each
+    given the HIP's earlier decisions).  drop_masks: train mode with these masks."""
     d64 = lambda t: t.double() if torch.is_tensor(t) else t  # noqa: E731
-    pre = {}
+    masks = mask_hip if isinstance(mask_hip, tuple) else (mask_hip,)
     dm = None if drop_masks is None else tuple(d64(m) for m in drop_masks)
-    with torch.no_grad():
-        ref.block_forward({k: d64(v) for k, v in p.items()}, d64(x), d64(res), [d64(c) for c in cheb], d64(apa), dims,
-                          train=dm is not None, drop_masks=dm, hoist=True, pre_out=pre)
-    z = pre["z"]
-    flip = mask_hip != (z > 0)
-    scale = float(z.abs().max())
-    if bool(flip.any()):
-        worst = float(z[flip].abs().max())
-        assert worst <= eps * scale, f"{what}: ReLU decision differs at |z| = {worst:.3e} > {eps} * {scale:.3e}"
-    return int(flip.sum())
+    flips = 0
+    names = ("z", "z_tco", "z_r")
+    for q, m in enumerate(masks):
+        # each ReLU's fp64 pre-activation given the HIP's decisions at the ReLUs before it
+        kw = {}
+        if q >= 1:
+            kw["relu_mask"] = masks[0]
+        if q >= 2:
+            kw["tail_masks"] = (masks[1], torch.ones_like(masks[1]))  # z_r is recorded before its own ReLU
+        pre = {}
+        with torch.no_grad():
+            ref.block_forward({k: d64(v) for k, v in p.items()}, d64(x), d64(res), [d64(c) for c in cheb], d64(apa),
+                              dims, train=dm is not None, drop_masks=dm, hoist=True, pre_out=pre, **kw)
+        z = pre[names[q]]
+        flip = m != (z > 0)
+        scale = float(z.abs().max())
+        if bool(flip.any()):
+            worst = float(z[flip].abs().max())
+            assert worst <= eps * scale, \
+                f"{what}: ReLU decision ({names[q]}) differs at |z| = {worst:.3e} > {eps} * {scale:.3e}"
+        flips += int(flip.sum())
+    return flips
 
 
 TRAIN_SEED = 1234  # torch.manual_seed before a train-mode forward: the block draws its dropout seed from it
@@ -381,14 +405,15 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
         keep = float((m0 > 0).float().mean())
         assert 0.94 < keep < 0.96, keep  # p = 0.05 over B*N*D draws
         dm = (m0.cpu(), m1.cpu().permute(0, 2, 1, 3).contiguous())
-    mask = hip_cheb_relu_mask(blk, xg, rg, train=train, seed=dseed)
-    flips = relu_aware_mask(ref, p, x, res, cheb, apa, dims, mask, name, eps=relu_eps, drop_masks=dm)
+    masks = hip_relu_masks(blk, xg, rg, train=train, seed=dseed)  # all three ReLUs (:133, :247, :252)
+    flips = relu_aware_mask(ref, p, x, res, cheb, apa, dims, masks, name, eps=relu_eps, drop_masks=dm)
     d64 = lambda t: t.double() if torch.is_tensor(t) else t  # noqa: E731
     out_r, re_r, gx_r, gra_r, grads_r = ref.block_forward_backward(
         {k: d64(v) for k, v in p.items()}, d64(x), d64(res), [d64(c) for c in cheb], d64(apa), dims, d64(g_out),
-        d64(g_re), relu_mask=mask, train=train, drop_masks=None if dm is None else tuple(d64(m) for m in dm))
-    o32 = ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, relu_mask=mask, train=train,
-                                     drop_masks=dm)
+        d64(g_re), relu_mask=masks[0], tail_masks=masks[1:], train=train,
+        drop_masks=None if dm is None else tuple(d64(m) for m in dm))
+    o32 = ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, relu_mask=masks[0], tail_masks=masks[1:],
+                                     train=train, drop_masks=dm)
     ref32 = {"out": o32[0], "re_at": o32[1], "grad_x": o32[2], "grad_res_att": o32[3], **o32[4]}
 
     def close_cal(a, b, key):
