@@ -105,14 +105,28 @@ def flags_of(train, sparse, direct, flash=False):
             | (_lib.F_POISON if _POISON else 0) | (_lib.F_FLASH if flash else 0))
 
 
-def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False, flash=None):
-    """(out, re_at) = dstagnn::block(...) — autograd-tracked."""
+def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False, flash=None, plan_cache=None):
+    """(out, re_at) = dstagnn::block(...) — autograd-tracked.  In direct-gradient mode with a
+    plan_cache dict (the module's), the block's constant arguments go to the library once, as a
+    cached BlockPlan (dstagnn::block_planned): same kernels, less host work per call."""
     ops = _lib.load()
     x = x.float().contiguous()
     sparse = use_sparse(graph, meta, x.shape[3])
     fl = use_flash(graph, meta, x.shape[3], flash, x.shape[0])
+    flags = flags_of(train, sparse, direct, fl)
+    if direct and plan_cache is not None:
+        key = (id(params), id(graph), sparse, fl)
+        ent = plan_cache.get("plan")
+        if ent is None or ent[0] != key:
+            plist = list(params)
+            plan = torch.classes.dstagnn.BlockPlan(plist, list(slots), graph_list(graph, sparse, fl), cfg_of(meta))
+            anchor = next((p for p in plist if p.requires_grad), plist[0])
+            ent = (key, plan, anchor, params, graph)  # params / graph kept alive: the key holds their ids
+            plan_cache["plan"] = ent
+        return ops.block_planned(x, res_arg(res_att, x.shape[2]), ent[1], ent[2], float(meta.get("drop_p", 0.05)),
+                                 int(seed), flags)
     return ops.block(x, res_arg(res_att, x.shape[2]), list(params), slots, graph_list(graph, sparse, fl),
-                     cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed), flags_of(train, sparse, direct, fl))
+                     cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed), flags)
 
 
 def dropout_masks(meta, x_shape, seed):

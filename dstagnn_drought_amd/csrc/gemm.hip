@@ -194,7 +194,7 @@ struct Plan {
   }
 };
 
-// a workgroup reducing more than this many k in one fp32 chain takes the two-level
+// a split-K workgroup reducing more than this many k in one fp32 chain takes the two-level
 // accumulation (gemm_kern.hpp ACC2); DSTAGNN_GEMM_ACC2_MINK overrides
 int acc2_min_k() {
   static const int v = getenv("DSTAGNN_GEMM_ACC2_MINK") ? atoi(getenv("DSTAGNN_GEMM_ACC2_MINK")) : 1024;
@@ -280,7 +280,10 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   while (k.red_g < 64 && k.red_g * 8 < splitk) k.red_g *= 2;
 
   pl.best = best;
-  pl.acc2 = !g_bf16 && (best == 0 || best == 2) && kchunk > acc2_min_k();
+  // split-K launches only: their K slices are the long chains (weight gradients), and a GEMM
+  // that does not split keeps one summation order under every tile configuration (a B=1 and a
+  // B=32 call may pick different tiles: per-sample results stay bit-identical, test_batch_consistency)
+  pl.acc2 = !g_bf16 && (best == 0 || best == 2) && splitk > 1 && kchunk > acc2_min_k();
   pl.akc = !g.ak.two && g.ak.s0 == 1;
   pl.bnc = !g.bn.two && g.bn.s0 == 1;
   pl.ktwo = g.ak.two || g.bk.two;

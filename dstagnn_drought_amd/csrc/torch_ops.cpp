@@ -292,6 +292,85 @@ class BlockFunction : public torch::autograd::Function<BlockFunction> {
   }
 };
 
+// -------------------------------------------------------------------------------------
+// dstagnn::block_planned — the same node for direct-gradient mode with the block's constant
+// arguments (parameters, slots, graph, cfg) held in ONE cached BlockPlan object instead of
+// being boxed, edge-linked and saved per call: the parameters are not autograd inputs (their
+// gradients are written by the backward itself), so the node has three inputs (x, res_att and
+// an anchor parameter that keeps the node in the graph when x needs no gradient) instead of
+// ~50.  Host cost, not arithmetic: the kernels and their results are the same as dstagnn::block.
+// -------------------------------------------------------------------------------------
+struct BlockPlan : torch::CustomClassHolder {
+  std::vector<Tensor> params, graph;
+  std::vector<int64_t> slots, cfg;
+  BlockPlan(std::vector<Tensor> p, std::vector<int64_t> s, std::vector<Tensor> g, std::vector<int64_t> c)
+      : params(std::move(p)), graph(std::move(g)), slots(std::move(s)), cfg(std::move(c)) {
+    TORCH_CHECK(params.size() == slots.size(), "BlockPlan: params / slots length mismatch");
+  }
+};
+
+class BlockPlanFunction : public torch::autograd::Function<BlockPlanFunction> {
+ public:
+  static variable_list forward(AutogradContext* ctx, const Tensor& x, const c10::optional<Tensor>& res,
+                               const c10::intrusive_ptr<BlockPlan>& plan, const Tensor& anchor, double drop_p,
+                               int64_t seed, int64_t flags) {
+    (void)anchor;
+    ctx->set_materialize_grads(false);
+    TORCH_CHECK(flags & kDirect, "block_planned: direct-gradient mode only");
+    BlockCall c = make_call(x, res, plan->params, plan->slots, plan->graph, plan->cfg, drop_p, seed, flags);
+    auto [out, re_at, save] = run_forward(c, x, res);
+    ctx->save_for_backward({x, c.mode != DSTAGNN_RES_NONE ? *res : Tensor()});
+    ctx->saved_data["plan"] = plan;
+    ctx->saved_data["drop_p"] = drop_p;
+    ctx->saved_data["seed"] = seed;
+    ctx->saved_data["flags"] = flags;
+    ctx->saved_data["save"] = save;
+    return {out, re_at};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list gout) {
+    auto saved = ctx->get_saved_variables();
+    const Tensor x = saved[0];
+    c10::optional<Tensor> res;
+    if (saved[1].defined()) res = saved[1];
+    auto plan = ctx->saved_data["plan"].toCustomClass<BlockPlan>();
+    const int64_t flags = ctx->saved_data["flags"].toInt();
+    BlockCall c = make_call(x, res, plan->params, plan->slots, plan->graph, plan->cfg, ctx->saved_data["drop_p"].toDouble(),
+                            ctx->saved_data["seed"].toInt(), flags);
+    Tensor save = ctx->saved_data["save"].toTensor();
+    ctx->saved_data["save"] = Tensor();  // release the forward state with the backward
+    c10::optional<Tensor> dre;
+    if (gout.size() > 1 && gout[1].defined()) dre = gout[1];
+    BwdResult r = run_backward(c, x, res, gout[0], dre, save, plan->params, plan->slots);
+    for (size_t i = 0; i < plan->params.size(); ++i) {
+      Tensor p = plan->params[i];
+      if (r.grads[i].defined() && p.requires_grad()) {
+        Tensor& pg = p.mutable_grad();
+        if (!pg.defined()) pg = r.grads[i];
+        else pg.add_(r.grads[i]);
+      }
+    }
+    // gradient list: x, res_att, plan, anchor, drop_p, seed, flags
+    return {r.dx, r.dres, Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+  }
+};
+
+std::tuple<Tensor, Tensor> block_planned_autograd(const Tensor& x, const c10::optional<Tensor>& res,
+                                                  const c10::intrusive_ptr<BlockPlan>& plan, const Tensor& anchor,
+                                                  double drop_p, int64_t seed, int64_t flags) {
+  auto o = BlockPlanFunction::apply(x, res, plan, anchor, drop_p, seed, flags);
+  return {o[0], o[1]};
+}
+
+std::tuple<Tensor, Tensor> block_planned_infer(const Tensor& x, const c10::optional<Tensor>& res,
+                                               const c10::intrusive_ptr<BlockPlan>& plan, const Tensor& anchor,
+                                               double drop_p, int64_t seed, int64_t flags) {
+  (void)anchor;
+  BlockCall c = make_call(x, res, plan->params, plan->slots, plan->graph, plan->cfg, drop_p, seed, flags);
+  auto [out, re_at, save] = run_forward(c, x, res);
+  return {out, re_at};
+}
+
 std::tuple<Tensor, Tensor> block_autograd(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params,
                                           at::IntArrayRef slots, at::TensorList graph, at::IntArrayRef cfg,
                                           double drop_p, int64_t seed, int64_t flags) {
@@ -701,6 +780,10 @@ std::vector<double> prof_stop() {
 }  // namespace
 
 TORCH_LIBRARY(dstagnn, m) {
+  m.class_<BlockPlan>("BlockPlan")
+      .def(torch::init<std::vector<Tensor>, std::vector<int64_t>, std::vector<Tensor>, std::vector<int64_t>>());
+  m.def("block_planned(Tensor x, Tensor? res_att, __torch__.torch.classes.dstagnn.BlockPlan plan, Tensor anchor, "
+        "float drop_p, int seed, int flags) -> (Tensor, Tensor)");
 #define DSTAGNN_BLK_ARGS \
   "Tensor x, Tensor? res_att, Tensor[] params, int[] slots, Tensor[] graph, int[] cfg, float drop_p, int seed, int flags"
   m.def("block(" DSTAGNN_BLK_ARGS ") -> (Tensor, Tensor)");
@@ -737,6 +820,7 @@ TORCH_LIBRARY(dstagnn, m) {
 // PyTorch-ROCm dispatches HIP device tensors under the CUDA key
 TORCH_LIBRARY_IMPL(dstagnn, CUDA, m) {
   m.impl("block", block_infer);
+  m.impl("block_planned", block_planned_infer);
   m.impl("block_fwd", block_fwd);
   m.impl("block_bwd", block_bwd);
   m.impl("block_time_stage", block_time_stage);
@@ -756,4 +840,7 @@ TORCH_LIBRARY_IMPL(dstagnn, CUDA, m) {
   m.impl("graph_topk", graph_topk);
 }
 
-TORCH_LIBRARY_IMPL(dstagnn, Autograd, m) { m.impl("block", block_autograd); }
+TORCH_LIBRARY_IMPL(dstagnn, Autograd, m) {
+  m.impl("block", block_autograd);
+  m.impl("block_planned", block_planned_autograd);
+}

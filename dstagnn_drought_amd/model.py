@@ -266,7 +266,7 @@ class DSTAGNN_block(nn.Module):
         if use_flash(graph, meta, T, self.flash_cheb, B):
             graph = self._flash_graph(graph)
         out, re_at = block_call(x, res_att, params, slots, graph, meta, meta["train"], meta["seed"],
-                                self.direct_grads, flash=self.flash_cheb)
+                                self.direct_grads, flash=self.flash_cheb, plan_cache=self.__dict__.setdefault("_pcache", {}))
         if self.grads_ready is not None and out.requires_grad:
             # DP overlap (dp.GradAllReducer.attach): once this block's backward node has run,
             # its parameter gradients are final — hand them over from a post-hook on the node
