@@ -47,6 +47,7 @@ struct Dims {
   int Tg[3], Lp[3], ks[3];
   bool first, sparse, flash;
   bool fsmall;      // flash on a small graph (flash_small): the LDS-staged kernels
+  bool agg;         // sparse path in aggregate-first order (cheb_agg.hip): no x Theta GEMM
   int64_t nnz;      // flash: union-support entries
   int64_t apa_nnz;  // small-graph flash: A_pa support entries
 };
@@ -64,6 +65,8 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.flash = m.sparse && d.cheb_flash != 0;
   m.nnz = m.flash ? d.cheb_nnz : 0;
   m.fsmall = m.flash && flash_small(m.N);
+  static const bool agg_env = !getenv("DSTAGNN_CHEB_AGG") || atoi(getenv("DSTAGNN_CHEB_AGG")) != 0;
+  m.agg = agg_env && m.sparse && cheb_agg_ok(m.F, m.C);
   m.apa_nnz = m.fsmall ? std::max(d.cheb_apa_nnz, 0) : 0;
   return m;
 }
@@ -163,7 +166,7 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.dzs = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.dzs_r = m.fsmall ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.cc = m.flash ? a.take((int64_t)m.B * m.K * m.N) : nullptr;
-  s.dxth = a.take(m.BN * m.KCT);
+  s.dxth = m.agg ? nullptr : a.take(m.BN * m.KCT);
   s.dthcat = a.take((int64_t)m.F * m.KC);
   s.dqk = a.take(m.BN * 2 * m.KD);
   s.dZd = a.take(m.BN * m.D);
@@ -228,6 +231,7 @@ struct ChebIO {
   const float* thcat;      // (F, K*C)
   float *P, *W, *xth, *X;  // W unused (null) on the sparse path; xth (B,N,T,K,C), X (B,N,T,C)
   const ChebFl* fl = nullptr;  // fused (flash) attention: softmax statistics + support P, no dense P
+  bool agg = false;            // aggregate-first order (cheb_agg.hip): xth holds the aggregates (B,N,K,F,T)
 };
 
 ChebSp make_sp(int B, int N, int K, int C, int T, const dstagnn_graph* g) {
@@ -258,9 +262,24 @@ int cheb_xtheta(const ChebIO& c, float* ws, hipStream_t st) {
   return run_gemm(g, ws, kGemmWs, st);
 }
 
+ChebAg make_ag(int B, int N, int K, int F, int C, int T, const dstagnn_graph* g) {
+  ChebAg a;
+  a.B = B; a.N = N; a.K = K; a.F = F; a.C = C; a.T = T; a.KC = K * C;
+  a.csc_ptr = g->csc_ptr; a.csc_row = g->csc_row; a.csr_ptr = g->csr_ptr; a.csr_col = g->csr_col;
+  a.csr2csc = g->csr2csc; a.cheb = g->cheb;
+  return a;
+}
+
 // X[b,j,(t,c)] = relu( sum_{k,i} W[b,k,i,j] xth[b,i,t,k,c] )
+// (aggregate-first: X = relu( sum_k (sum_i W[b,k,i,j] x_i)^T Theta_k ), xth holding the aggregates)
 int cheb_aggregate(const ChebIO& c, float* ws, hipStream_t st) {
   const int64_t NN = (int64_t)c.N * c.N, KC = (int64_t)c.K * c.C, T = c.T, CT = (int64_t)c.C * T, KCT = KC * T;
+  if (c.agg) {
+    ChebAg a = make_ag(c.B, c.N, c.K, c.F, c.C, c.T, c.g);
+    a.x = c.x; a.thcat = c.thcat; a.P = c.P; a.agg = c.xth; a.X = c.X;
+    if (c.fl) { a.wsupp = c.fl->wsupp; a.nnz = c.fl->nnz; }
+    return op_cheb_agg_fwd(a, st);
+  }
   if (c.sparse) {
     ChebSp sp = make_sp(c.B, c.N, c.K, c.C, c.T, c.g);
     sp.P = c.P; sp.xth = c.xth; sp.out = c.X;
@@ -278,7 +297,7 @@ int cheb_aggregate(const ChebIO& c, float* ws, hipStream_t st) {
 
 int cheb_forward(const ChebIO& c, float* ws, hipStream_t st) {
   DS_TRY(cheb_softmax(c, st));
-  DS_TRY(cheb_xtheta(c, ws, st));
+  if (!c.agg) DS_TRY(cheb_xtheta(c, ws, st));
   return cheb_aggregate(c, ws, st);
 }
 
@@ -634,6 +653,7 @@ struct Fwd {
     c.B = m.B; c.N = m.N; c.F = m.F; c.T = m.T; c.K = m.K; c.C = m.C;
     c.x = x; c.S = s.P; c.mask = p.mask; c.g = &gr; c.sparse = m.sparse; c.thcat = s.thcat;
     c.P = s.P; c.W = s.W; c.xth = s.xth; c.X = s.X;
+    c.agg = m.agg;
     if (m.flash) {
       fl = make_fl(m, p, gr, s);
       c.fl = &fl;
@@ -688,7 +708,7 @@ struct Fwd {
         if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
         e_side = true;
       }
-      DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
+      if (!m.agg) DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
     }
     DS_TRY(stage_tat());
     ht.lap("tat");
@@ -851,7 +871,36 @@ struct Bwd {
     // gpre = dX * (X > 0) was written by the last transposed-conv GEMM's epilogue
     const int64_t NN = m.NN, KC = m.KC, T = m.T, CT = m.CT, KCT = m.KCT, FT = m.FT;
     const int B = m.B, N = m.N, K = m.K, C = m.C, F = m.F;
-    if (m.sparse) {
+    if (m.agg) {
+      // aggregate-first (cheb_agg.hip).  Side stream: dx += the Chebyshev path's gradient
+      // (transposed SpMM of g, Theta on the matrix cores) and dTheta_k = agg_k^T g, both from g
+      // alone; main: the SDDMM dW = <x_i, Theta_k g_j^T> (flash: dzs and c) for the softmax backward
+      ChebAg a = make_ag(B, N, K, F, C, m.T, &gr);
+      a.x = x; a.thcat = s.thcat; a.P = s.P; a.agg = s.xth; a.g = w.gpre; a.dW = w.dW; a.dx = dx; a.dx_beta = 1.f;
+      if (m.flash) {
+        a.nnz = (int)m.nnz; a.wsupp = s.wsupp; a.psupp = s.psupp; a.tsupp = gr.tsupp; a.dzs = w.dzs; a.cc = w.cc;
+        if (m.fsmall) { a.csc2csr = gr.csc2csr; a.dzs_r = w.dzs_r; }
+      }
+      DS_TRY(fork());
+      DS_TRY(op_cheb_agg_spmm_t(a, sd));
+      DS_TRY(mark_side(&dx_ready));
+      {
+        Gemm g;  // dTheta[(k,f), c] = sum_{b,j,t} agg[b,j,k,f,t] g[b,j,t,c]
+        g.M = K * F; g.N = C; g.K = B * N * m.T;
+        g.A = s.xth; g.am = idx1(T); g.ak = idx2(T, 1, (int64_t)K * FT);
+        g.B = w.gpre; g.bk = idx1(C); g.bn = idx1(1);
+        bool adjacent = gd.theta[0] != nullptr;
+        for (int k = 1; k < K && adjacent; ++k) adjacent = gd.theta[k] == gd.theta[0] + (int64_t)k * F * C;
+        if (adjacent) {  // [k][f][c]: the parameters' own layout in the flat gradient buffer
+          g.C = gd.theta[0]; g.cm = idx1(C); g.cn = idx1(1);
+        } else {         // (F, K*C), unpacked below
+          g.C = w.dthcat; g.cm = idx2(F, KC, C); g.cn = idx1(1);
+        }
+        DS_TRY(sgemm(g));
+        if (!adjacent) DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sd));
+      }
+      DS_TRY(op_cheb_agg_sddmm(a, st));
+    } else if (m.sparse) {
       // dW is written on the support only; the softmax backward reads it only where
       // T_k != 0 (no memset)
       ChebSp sp = make_sp(B, N, K, C, m.T, &gr);
@@ -900,6 +949,7 @@ struct Bwd {
     DS_TRY(fork());
     if (m.flash) DS_TRY(op_flash_mask_grad(fl, sd));
     else DS_TRY(op_cheb_mask_grad(sm, sd));
+    if (m.agg) return 0;  // Theta and x gradients came with the aggregate-first kernels above
     {
       Gemm g;  // dTheta_cat[f,(k,c)] = sum_{b,i,t} x[b,i,f,t] dxth[b,i,t,k,c]
       g.M = F; g.N = (int)KC; g.K = B * N * m.T;

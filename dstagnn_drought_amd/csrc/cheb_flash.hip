@@ -356,7 +356,6 @@ unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
 // gradient needs no score recomputation at all.
 // ---------------------------------------------------------------------------------------
 constexpr int kSmallN = 512;         // <= 16 tiles: <= kSmallTPW per wave
-constexpr int kSmallTPW = 4;         // tiles per wave at most (kernels templated on 1..4)
 constexpr int kXs = 36;              // LDS row stride (floats) of a staged (N, 32) operand: 16-B rows
 constexpr int kStripE = 1024;        // sparse entries of one strip staged in LDS (else read from HBM)
 

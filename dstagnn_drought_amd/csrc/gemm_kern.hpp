@@ -352,7 +352,14 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   if (idle) return;  // uniform over the workgroup, before any barrier
   // two LDS stages, compile-time (static LDS: the stage addresses fold into the ds_read /
   // M0 immediates; a runtime stage count cost ~10 % of the GEMM family, measured)
-  constexpr int NS = 2;
+#ifndef DSTAGNN_GEMM_NS
+#define DSTAGNN_GEMM_NS 2
+#endif
+  // LDS stages (compile-time: the stage addresses fold into immediates); deeper rings for the
+  // tiles whose ring still fits 64 KB
+  constexpr int NS = (BM + BN) * BK * 4 * DSTAGNN_GEMM_NS <= 65536 ? DSTAGNN_GEMM_NS : 2;
+  constexpr int FT = NA + NB, PT = LA1 + LB1;  // DMA instructions of a full / the partial k-tile
+  static_assert(NS >= 2 && NS <= 4, "LDS ring of 2..4 stages");
   __shared__ __attribute__((aligned(16))) float Asm[NS * BM * BK];
   __shared__ __attribute__((aligned(16))) float Bsm[NS * BN * BK];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -458,8 +465,23 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
     if (s0 < ntiles) issue(kbeg + s0 * BK, s0);
   int st = 0;
   for (int t = 0; t < ntiles; ++t) {
-    // retire tile t: with two stages nothing younger is in flight
-    wait_vm_barrier<0>();
+    // retire tile t: the DMAs of the (up to NS - 2) younger tiles issued so far stay in flight
+    if constexpr (NS == 2) {
+      wait_vm_barrier<0>();
+    } else {
+      const int young = min(NS - 2, ntiles - 1 - t);
+      const bool lastp = (kend - kbeg) % BK != 0;  // the last k-tile is the partial one
+      if (young <= 0) wait_vm_barrier<0>();
+      else if (young == 1) {
+        if (t + 1 == ntiles - 1 && lastp) wait_vm_barrier<PT>();
+        else wait_vm_barrier<FT>();
+      } else {
+        if constexpr (NS >= 4) {
+          if (t + 2 == ntiles - 1 && lastp) wait_vm_barrier<FT + PT>();
+          else wait_vm_barrier<2 * FT>();
+        }
+      }
+    }
     if (ones_tile) {
       // column-sum column: B = 1 in this stage's image (A is 0 past K); written after the
       // DMA landed, read after one more barrier (only the tile column that holds it pays)
@@ -590,14 +612,18 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
 }
 
+// occupancy target (waves per SIMD) the register allocator works to
+#ifndef DSTAGNN_GEMM_WPE
+#define DSTAGNN_GEMM_WPE 4
+#endif
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false,
           bool ACC2 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void gemm_f32_kernel(GemmG g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, DSTAGNN_GEMM_WPE))) void gemm_f32_kernel(GemmG g) {
   gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT, ACC2>(g);
 }
 // same code under a second name: the GEMM a profile reports as "the hot kernel" (Gemm::hot)
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void gemm_f32_hot_kernel(GemmG g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, DSTAGNN_GEMM_WPE))) void gemm_f32_hot_kernel(GemmG g) {
   gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
 }
 }  // namespace

@@ -158,6 +158,30 @@ struct ChebSp {
 };
 bool cheb_sparse_ok(int CT);
 
+// the block's sparse Chebyshev convolution in aggregate-first order (cheb_agg.hip): the
+// support gather runs on x (F*T per node) and the Theta products on each wave's matrix cores
+struct ChebAg {
+  int B = 0, N = 0, K = 0, F = 0, C = 0, T = 0, KC = 0, nnz = 0;
+  const float* x = nullptr;        // (B,N,F,T)
+  const float* thcat = nullptr;    // (F, K*C)
+  const int *csc_ptr = nullptr, *csc_row = nullptr, *csr_ptr = nullptr, *csr_col = nullptr, *csr2csc = nullptr;
+  const float* cheb = nullptr;     // (K,N,N)   } unfused path: W = T o P
+  const float* P = nullptr;        // (B,K,N,N) }
+  const float* wsupp = nullptr;    // (B,K,nnz) flash path: W on the support (CSC order)
+  float* agg = nullptr;            // (B,N,K,F,T) fwd output, saved for dTheta
+  float* X = nullptr;              // (B,N,T,C) fwd output (ReLU applied)
+  const float* g = nullptr;        // (B,N,T,C) bwd: d(pre-ReLU X)
+  float* dW = nullptr;             // (B,K,N,N) sddmm, unfused path (support entries only)
+  const float* psupp = nullptr; const float* tsupp = nullptr;  // flash path: the softmax backward's
+  float* dzs = nullptr; float* dzs_r = nullptr; const int* csc2csr = nullptr; float* cc = nullptr;  // support terms
+  float* dx = nullptr; float dx_beta = 1.f;  // spmm_t: dx = dx_beta dx + (the Chebyshev path's gradient)
+  int xcd_order = 0;
+};
+bool cheb_agg_ok(int F, int C);
+int op_cheb_agg_fwd(const ChebAg& a, hipStream_t st);
+int op_cheb_agg_sddmm(const ChebAg& a, hipStream_t st);
+int op_cheb_agg_spmm_t(const ChebAg& a, hipStream_t st);
+
 // fused (flash-style) Chebyshev attention (cheb_flash.hip); dk == 32
 struct ChebFl {
   int B = 0, N = 0, K = 0, nnz = 0, nw = 0;  // nw = 32-bit words per A_pa bit row
