@@ -61,13 +61,18 @@ __device__ __forceinline__ int64_t xcd_block(int on) {
 }
 
 constexpr int kE = 4;      // support entries per batch (one memory round per batch)
+// occupancy the register allocator targets (waves per SIMD): these kernels are chains of
+// dependent gathers, so resident waves hide the latency
+#ifndef DSTAGNN_AGG_WPE
+#define DSTAGNN_AGG_WPE 4
+#endif
 constexpr int kAs = 33;    // LDS row stride of a 32 x 32 operand tile
 
 // ---------------------------------------------------------------------------------------
 // forward: one wave per (b, j, time chunk)
 // ---------------------------------------------------------------------------------------
 template <int kNQ, int KM>  // kNQ >= F * Tc / 64, KM >= K
-__global__ __launch_bounds__(256) void cheb_agg_fwd_kernel(ChebAg a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <= 24 ? DSTAGNN_AGG_WPE : 2, 8))) void cheb_agg_fwd_kernel(ChebAg a) {
   __shared__ float As[4][32 * kAs];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
@@ -165,7 +170,7 @@ __global__ __launch_bounds__(256) void cheb_agg_fwd_kernel(ChebAg a) {
 // dzs = P T dW and c_j instead, as cheb_sparse.hip).
 // ---------------------------------------------------------------------------------------
 template <int kNQ, int KM>  // kNQ >= min(F*T, 1024) / 64
-__global__ __launch_bounds__(256) void cheb_agg_sddmm_kernel(ChebAg a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <= 24 ? DSTAGNN_AGG_WPE : 2, 8))) void cheb_agg_sddmm_kernel(ChebAg a) {
   extern __shared__ float Dg[];  // [waves][K][F * T]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(256) void cheb_agg_sddmm_kernel(ChebAg a) {
 // dx_i[f, t'] += sum_k sum_c Theta_k[f][c] h_k[t'][c] on the matrix cores.
 // ---------------------------------------------------------------------------------------
 template <int kNQ, int KM>  // kNQ >= Tc * C / 64
-__global__ __launch_bounds__(256) void cheb_agg_spmm_t_kernel(ChebAg a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <= 24 ? DSTAGNN_AGG_WPE : 2, 8))) void cheb_agg_spmm_t_kernel(ChebAg a) {
   __shared__ float Hs[4][32 * kAs];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;

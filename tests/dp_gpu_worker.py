@@ -2,7 +2,7 @@
 ranks on cuda:0, gloo over device tensors): a real DSTAGNN_block forward + backward in
 direct-gradient mode with GradAllReducer.attach — the overlap path of dp.py that the
 driver's RCCL scaling bench runs — against the same gradients reduced without attach.
-Prints one JSON line per rank."""
+Writes one JSON record per rank into $DSTAGNN_DP_OUT."""
 import json
 import os
 import sys
@@ -68,8 +68,10 @@ def main():
     allp = [torch.zeros_like(probe) for _ in range(world)]
     dist.all_gather(allp, probe)
     ranks_agree = all(torch.equal(allp[0], a) for a in allp)
-    print(json.dumps({"rank": rank, "inflight_with_attach": n_on, "inflight_without": n_off, "flat": flat_on,
-                      "max_err": err, "same_keys": same_keys, "ranks_agree": ranks_agree}), flush=True)
+    rec = {"rank": rank, "inflight_with_attach": n_on, "inflight_without": n_off, "flat": flat_on,
+           "max_err": err, "same_keys": same_keys, "ranks_agree": ranks_agree}
+    with open(os.path.join(os.environ["DSTAGNN_DP_OUT"], f"rank{rank}.json"), "w") as f:
+        json.dump(rec, f)
     dist.barrier()
     dist.destroy_process_group()
 

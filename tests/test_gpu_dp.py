@@ -19,21 +19,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-def test_dp_overlap_on_hip_blocks():
+def test_dp_overlap_on_hip_blocks(tmp_path):
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", DSTAGNN_DP_OUT=str(tmp_path))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "dp_gpu_worker.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
-    recs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert sorted(x["rank"] for x in recs) == [0, 1], r.stdout
+    recs = [json.loads((tmp_path / f"rank{r_}.json").read_text()) for r_ in (0, 1)]
+    assert sorted(x["rank"] for x in recs) == [0, 1], recs
     for x in recs:
         assert x["flat"], x                         # the backward packed one flat gradient buffer
         assert x["inflight_with_attach"] == 1, x    # ... whose all-reduce the node's post-hook issued
