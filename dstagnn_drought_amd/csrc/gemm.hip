@@ -17,8 +17,10 @@
 // slabs summed by a deterministic second pass (no float atomics).
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "common.hpp"
+#include "ops.hpp"
 
 #include "gemm_kern.hpp"
 
@@ -68,6 +70,179 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmG gin) {
     const int64_t mn = idx % MN;
     epilogue_store(g, zb, (int)(mn / g.N), (int)(mn % g.N), red[threadIdx.x]);
   }
+}
+
+// ---------------------------------------------------------------------------------
+// Skinny long reductions: M and the kernel's N (with the column-sum column) <= 32, batch 1,
+// K >= kSkinnyMinK — the fcmy weight gradient (12 x 25 over B*N*C = 174K rows at PEMS08).
+// The tiled kernel's 128x32 tile wastes 90 % of its loads and MFMAs on clamped rows and
+// spends its time in per-k-tile DMA round trips.  Here every wave owns kpw consecutive k and
+// loads a round of kSkU k-quads at once (v_mfma_f32_16x16x4_f32, lane (q = l>>4, i = l&15):
+// A[mt*16 + i][k + q] and B[k + q][nt*16 + i]), then MT x NT MFMAs per quad into 16x16
+// accumulators (M <= 16 and N <= 32 at fcmy: 16 MFMA cycles per k, not the 32x32 tile's 32).
+// One 1024-thread workgroup per CU (<= 256 of them): its 16 accumulators fold in LDS, and the
+// workgroups' partials fold in ONE ticket level (colsum2d's hand-off: sc1 stores drained by
+// every storing wave, a barrier, one agent-scope ticket per workgroup; the last arrival
+// acquires, then all its 1024 threads sum the partials in a fixed order and apply the GEMM
+// epilogue).  One hand-off instead of a two-level tree: the acquire's price grows with the
+// workgroups per CU (MI355X_MICROARCH.md), so one per CU pays it once.  Deterministic.
+// ---------------------------------------------------------------------------------
+constexpr int kSkU = 16;           // k-quads per load round
+constexpr int kSkWaves = 16;       // waves per workgroup
+constexpr int kSkMaxWg = 256;      // workgroups (partials) at most
+constexpr int kSkinnyMinK = 4096;  // shorter reductions stay on the tiled kernel
+struct SkinnyK {
+  GemmK g;
+  float* part;  // [nwg][P] partials
+  int* cnt;     // one ticket
+  int kpw;      // k per wave (multiple of 4)
+  int nwg, P;   // P = M * N (kernel columns, the column-sum column included)
+  int P4;       // partial row stride: P rounded up to 4 (16-B rows)
+  int stop;     // profiling probe (DSTAGNN_SKINNY_STOP): 1 = after the loads + MFMAs, 2 = after the ticket
+};
+
+__device__ __forceinline__ float sk_ld(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sk_st(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MT, int NT>  // 16-row / 16-column accumulator tiles
+__global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
+  constexpr int kH = kSkWaves / 2;
+  __shared__ float red[kH][32 * 33];
+  __shared__ int last;
+  const GemmK& g = s.g;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, q4 = lane >> 4, i16 = lane & 15;
+  const int k0 = (blockIdx.x * kSkWaves + w) * s.kpw, k1 = min(g.K, k0 + s.kpw);
+  uint32_t ao[MT], bo[NT];
+  bool arow[MT], bcol[NT], ones[NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + i16;
+    arow[mt] = m < g.M;
+    ao[mt] = (uint32_t)g.abias + (arow[mt] ? (uint32_t)koff(g.am, m) : 0u);
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = nt * 16 + i16;
+    bcol[nt] = n < g.nload;
+    ones[nt] = n == g.nload && g.nload < g.N;
+    bo[nt] = (uint32_t)g.bbias + (bcol[nt] ? (uint32_t)koff(g.bn, n) : 0u);
+  }
+  typedef float floatx4 __attribute__((ext_vector_type(4)));
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int kb = k0; kb < k1; kb += 4 * kSkU) {
+    float av[kSkU][MT], bv[kSkU][NT];
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      const int k = kb + 4 * u + q4;
+      const bool ok = k < k1;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) av[u][mt] = ok && arow[mt] ? g.A[ao[mt] + (uint32_t)koff(g.ak, k)] : 0.f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        bv[u][nt] = ok && bcol[nt] ? g.B[bo[nt] + (uint32_t)koff(g.bk, k)] : (ok && ones[nt] ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][mt], bv[u][nt], acc[mt][nt], 0, 0, 0);
+  }
+  // fold the 16 waves: D[m = mt*16 + 4 (l>>4) + r][n = nt*16 + (l&15)]; waves kH.. store, waves
+  // ..kH-1 add theirs (red[w] = acc_w + acc_{w+kH}), then the kH slots in order
+  auto slot = [&](int mt, int nt, int r) { return (mt * 16 + 4 * q4 + r) * 33 + nt * 16 + i16; };
+  if (w >= kH) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[w - kH][slot(mt, nt, r)] = acc[mt][nt][r];
+  }
+  __syncthreads();
+  if (w < kH) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[w][slot(mt, nt, r)] = acc[mt][nt][r] + red[w][slot(mt, nt, r)];
+  }
+  __syncthreads();
+  if (s.stop == 1) return;
+  float* p1 = s.part + (int64_t)blockIdx.x * s.P4;
+  for (int e = t; e < s.P; e += 1024) {
+    const int m = e / g.N, o = m * 33 + (e - m * g.N);
+    float v = red[0][o];
+#pragma unroll
+    for (int q = 1; q < kH; ++q) v += red[q][o];
+    sk_st(p1 + e, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    last = atomicAdd(s.cnt, 1) == s.nwg - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last || s.stop == 2) return;
+  // the last workgroup (plain loads behind its acquire): the partial rows are P4 floats, read
+  // as float4 column groups; S = 1024 / (P4/4) subsets of the partials per group (sub, sub + S,
+  // ...), sixteen 16-B loads in flight per round, then the subsets in order via LDS
+  float4* sums = reinterpret_cast<float4*>(&red[0][0]);  // kH * 32 * 33 floats >= 4096
+  const int C4 = s.P4 / 4, S = max(1, 1024 / C4);
+  const int sub = t / C4, c = t % C4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sub < S) {
+    const float4* p = reinterpret_cast<const float4*>(s.part) + c;
+    int q = sub;
+    for (; q < s.nwg; q += 16 * S) {
+      float4 u[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        u[j] = q + j * S < s.nwg ? p[(int64_t)(q + j * S) * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) { v.x += u[j].x; v.y += u[j].y; v.z += u[j].z; v.w += u[j].w; }
+    }
+  }
+  __syncthreads();
+  if (sub < S) sums[t] = v;
+  __syncthreads();
+  if (t < C4) {
+    float4 tot = sums[t];
+    for (int j = 1; j < S; ++j) {
+      const float4 x = sums[j * C4 + t];
+      tot.x += x.x; tot.y += x.y; tot.z += x.z; tot.w += x.w;
+    }
+    const float tv[4] = {tot.x, tot.y, tot.z, tot.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = 4 * t + i;
+      if (e < s.P) epilogue_store(g, 0, e / g.N, e % g.N, tv[i]);
+    }
+  }
+  if (t == 0) __hip_atomic_store(s.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+void launch_skinny(const SkinnyK& s, hipStream_t st) {
+  const dim3 grid((unsigned)s.nwg), blk(64 * kSkWaves);
+  const int mt = s.g.M > 16 ? 2 : 1, nt = s.g.N > 16 ? 2 : 1;
+  if (mt == 1 && nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<1, 1>), grid, blk, 0, st, s);
+  else if (mt == 1) hipLaunchKernelGGL((skinny_dw_kernel<1, 2>), grid, blk, 0, st, s);
+  else if (nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<2, 1>), grid, blk, 0, st, s);
+  else hipLaunchKernelGGL((skinny_dw_kernel<2, 2>), grid, blk, 0, st, s);
 }
 
 struct Cfg {
@@ -188,11 +363,48 @@ struct Plan {
   char log[220];
   int best, va, vb, ns;
   bool akc, bnc, ktwo, hot, acc2;
+  bool skinny;  // runs as skinny_dw_kernel (sk), never grouped
+  SkinnyK sk;
   bool same_kernel(const Plan& o) const {
-    return best == o.best && va == o.va && vb == o.vb && ns == o.ns && akc == o.akc && bnc == o.bnc &&
-           ktwo == o.ktwo && hot == o.hot && acc2 == o.acc2;
+    return !skinny && !o.skinny && best == o.best && va == o.va && vb == o.vb && ns == o.ns && akc == o.akc &&
+           bnc == o.bnc && ktwo == o.ktwo && hot == o.hot && acc2 == o.acc2;
+  }
+  // split-K slab floats this plan takes from the workspace
+  size_t ws_floats() const {
+    if (skinny) return (size_t)sk.nwg * sk.P4;
+    return k.splitk > 1 ? (size_t)k.batch * k.splitk * k.M * k.N : 0;
   }
 };
+
+// the skinny kernel's plan (plan_gemm has filled pl.k); false: keep the tiled kernel
+bool plan_skinny(Plan& pl, float* ws, size_t ws_floats, hipStream_t st) {
+  static const bool on = !getenv("DSTAGNN_GEMM_SKINNY") || atoi(getenv("DSTAGNN_GEMM_SKINNY")) != 0;
+  const GemmK& k = pl.k;
+  if (!on || g_bf16 || !ws || k.batch != 1 || k.M > 32 || k.N > 32 || k.K < kSkinnyMinK) return false;
+  SkinnyK& s = pl.sk;
+  s = SkinnyK{};
+  // <= kSkMaxWg workgroups of kSkWaves waves, a multiple of 4 k per wave
+  static const int env_kpw = getenv("DSTAGNN_SKINNY_KPW") ? atoi(getenv("DSTAGNN_SKINNY_KPW")) : 0;
+  s.kpw = (int)std::max<int64_t>(4, cdiv64(cdiv64(k.K, (int64_t)kSkMaxWg * kSkWaves), 4) * 4);
+  if (env_kpw > 0) s.kpw = (int)std::max<int64_t>(s.kpw, cdiv64(env_kpw, 4) * 4);
+  s.nwg = (int)cdiv64(k.K, (int64_t)kSkWaves * s.kpw);
+  s.P = k.M * k.N;
+  s.P4 = (s.P + 3) / 4 * 4;
+  if ((size_t)s.nwg * s.P4 > ws_floats || (reinterpret_cast<uintptr_t>(ws) & 15) != 0) return false;
+  s.cnt = stream_counters(st, 1);
+  if (!s.cnt) return false;
+  s.stop = getenv("DSTAGNN_SKINNY_STOP") ? atoi(getenv("DSTAGNN_SKINNY_STOP")) : 0;
+  pl.k.splitk = 1;
+  pl.k.kchunk = k.K;
+  s.g = pl.k;
+  s.part = ws;
+  pl.skinny = true;
+  if (gemm_log_on()) {
+    const size_t n = strlen(pl.log);
+    snprintf(pl.log + n, sizeof(pl.log) - n, " skinny kpw=%d nwg=%d", s.kpw, s.nwg);
+  }
+  return true;
+}
 
 // a split-K workgroup reducing more than this many k in one fp32 chain takes the two-level
 // accumulation (gemm_kern.hpp ACC2); DSTAGNN_GEMM_ACC2_MINK overrides
@@ -211,6 +423,7 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   Plan& pl = *out;
   GemmK& k = pl.k;
   k = GemmK{};
+  pl.skinny = false;
   const int Nk = g.N + (g.ones_out ? 1 : 0);  // kernel columns (the column-sum column last)
   k.M = g.M; k.N = Nk; k.K = g.K; k.batch = g.batch;
   k.nload = g.N; k.ones_out = g.ones_out; k.ones_stride = (int32_t)g.ones_stride;
@@ -351,8 +564,8 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
     const Gemm& g = gs[i];
     if (g.M <= 0 || g.N <= 0 || g.batch <= 0) continue;
     DS_TRY(plan_gemm(g, ws ? ws + ws_used : nullptr, ws_floats - ws_used, &plans[i]));
-    const GemmK& k = plans[i].k;
-    if (k.splitk > 1) ws_used += (size_t)k.batch * k.splitk * k.M * k.N;
+    plan_skinny(plans[i], ws ? ws + ws_used : nullptr, ws_floats - ws_used, st);
+    ws_used += plans[i].ws_floats();
     flops += 2.0 * g.M * g.N * (double)g.K * g.batch;
     bytes += 4.0 * g.batch * ((double)g.M * g.K + (double)g.K * g.N + (double)g.M * g.N * (g.beta != 0.f ? 2 : 1));
     live[nl++] = &plans[i];
@@ -371,7 +584,8 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
   for (int i = 0; i < nl;) {
     int j = i + 1;
     while (j < nl && j - i < kGroupMax && live[j]->same_kernel(*live[i])) ++j;
-    launch_plans(live + i, j - i, st);
+    if (live[i]->skinny) launch_skinny(live[i]->sk, st);
+    else launch_plans(live + i, j - i, st);
     DS_CHECK_LAUNCH();
     if (gemm_log_on()) {
       fprintf(stderr, "[gemm] %s", live[i]->log);
@@ -386,7 +600,7 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
   int nr = 0;
   for (int i = 0; i < nl; ++i) {
     const GemmK& k = live[i]->k;
-    if (k.splitk <= 1) continue;
+    if (k.splitk <= 1 || live[i]->skinny) continue;
     rk[nr] = &k;
     rc[nr] = (uint32_t)cdiv64((int64_t)k.batch * k.M * k.N, 256 / k.red_g);
     ++nr;

@@ -47,7 +47,8 @@ def _gemm(A, B, C, M, N, K, am, ak, bk, bn, cm, cn, batch=1, az=(0, 0, 0), bz=(0
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M,N,K", [(64, 64, 16), (100, 70, 33), (5440, 512, 384), (300, 96, 20000), (7, 3, 1)])
+@pytest.mark.parametrize("M,N,K", [(64, 64, 16), (100, 70, 33), (5440, 512, 384), (300, 96, 20000), (7, 3, 1),
+                                   (12, 24, 174080), (32, 32, 9000), (5, 7, 4097)])
 def test_gemm_plain(M, N, K):
     _need_gpu()
     g = torch.Generator().manual_seed(M + N + K)
@@ -59,6 +60,29 @@ def test_gemm_plain(M, N, K):
     _gemm(A.cuda(), B.cuda(), C, M, N, K, (0, K, 0), (0, 1, 0), (0, N, 0), (0, 1, 0), (0, N, 0), (0, 1, 0),
           bias=bias.cuda())
     close(C, ref, tol=1e-5 * max(1.0, K ** 0.5), what="plain")
+
+
+def test_gemm_skinny_epilogue():
+    """The skinny long-reduction kernel (M, N <= 32, K >= 4096: gemm.hip skinny_dw_kernel, the
+    fcmy weight gradient's shape) with a transposed A map, alpha, beta * C and ReLU, and the
+    tiled kernel on the same problem (DSTAGNN_GEMM_SKINNY is read once per process, so the
+    comparison is against the fp64 product)."""
+    _need_gpu()
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 12, 25, 70001
+    A = torch.randn(K, M, generator=g)   # A[m][k] = At[k][m]: m-contiguous, like fcmy's dtc
+    B = torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    ref = torch.relu(0.5 * (A.double().t() @ B.double()) + 2.0 * C0.double()).float()
+    C = C0.clone().cuda()
+    _gemm(A.cuda(), B.cuda(), C, M, N, K, (0, 1, 0), (0, M, 0), (0, N, 0), (0, 1, 0), (0, N, 0), (0, 1, 0),
+          alpha=0.5, beta=2.0, relu=1)
+    close(C, ref, tol=1e-5 * K ** 0.5, what="skinny")
+    # deterministic: a second run gives the same bits
+    C2 = C0.clone().cuda()
+    _gemm(A.cuda(), B.cuda(), C2, M, N, K, (0, 1, 0), (0, M, 0), (0, N, 0), (0, 1, 0), (0, N, 0), (0, 1, 0),
+          alpha=0.5, beta=2.0, relu=1)
+    assert torch.equal(C, C2)
 
 
 def test_gemm_transposed_batched_two_level():
