@@ -440,6 +440,12 @@ struct SideStream {
   hipStream_t side = nullptr;
   hipEvent_t ev[64] = {};
   int next = 0;
+  // flag words for stream-ordered write / wait-value synchronisation (see Streams)
+  static constexpr int kSlots = 4096;
+  uint32_t* flags = nullptr;
+  uint32_t gseq = 0;
+  int fnext = 0;
+  bool use_flags = true;
   bool ok = false;
 };
 
@@ -447,6 +453,7 @@ SideStream* side_stream_for_device() {
   static std::mutex mu;
   static SideStream cache[64];
   static const bool enabled = !getenv("DSTAGNN_SIDE_STREAM") || atoi(getenv("DSTAGNN_SIDE_STREAM")) != 0;
+  static const bool events = getenv("DSTAGNN_SYNC_EVENTS") && atoi(getenv("DSTAGNN_SYNC_EVENTS")) != 0;
   if (!enabled) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
@@ -458,12 +465,35 @@ SideStream* side_stream_for_device() {
     if (hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
     for (auto& e : s.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    s.use_flags = !events;
+    if (s.use_flags) {
+      if (hipMalloc(&s.flags, sizeof(uint32_t) * SideStream::kSlots) != hipSuccess ||
+          hipMemset(s.flags, 0, sizeof(uint32_t) * SideStream::kSlots) != hipSuccess ||
+          hipDeviceSynchronize() != hipSuccess)
+        return nullptr;
+    }
     s.ok = true;
   }
   return &s;
 }
 
-// fork / join between the caller's stream and the side stream (no-ops when disabled)
+// One cross-stream dependency: the consumer stream's later work waits for everything the
+// producer stream had issued when the token was made.
+struct SyncTok {
+  hipEvent_t ev = nullptr;
+  int slot = -1;
+  uint32_t seq = 0;
+};
+
+// fork / join between the caller's stream and the side stream (no-ops when disabled).
+// Default: stream-ordered flag writes (hipStreamWriteValue32 of a fresh sequence number into a
+// flag word, after all prior work of the producer stream) and waits (hipStreamWaitValue32,
+// >= that number) — on gfx950 / ROCm 7.2 an hipEventRecord between two kernels leaves the
+// recording stream idle for ~5.6 us (tools/fork_probe.hip: 5.56 us median gap) while the
+// write / wait-value packets cost nothing on the device timeline; tools/flag_sync_probe.hip
+// checks the data dependency both ways (0 stale reads in 600 rounds).  Flag words rotate over
+// kSlots; numbers only grow, so a wait can only be released by its own write or a later one
+// issued behind it.  DSTAGNN_SYNC_EVENTS=1 restores the event pairs.
 struct Streams {
   hipStream_t st = nullptr, sd = nullptr;
   SideStream* ss = nullptr;
@@ -472,14 +502,38 @@ struct Streams {
     ss = gemm_prof_on() ? nullptr : side_stream_for_device();
     sd = ss ? ss->side : st;
   }
+  static int fail(hipError_t r) {
+    set_last_error(std::string("side stream: ") + hipGetErrorString(r));
+    return (int)r;
+  }
+  int signal(hipStream_t from, SyncTok* t) {
+    *t = SyncTok{};
+    if (!ss) return 0;
+    if (ss->use_flags) {
+      t->slot = ss->fnext;
+      ss->fnext = (ss->fnext + 1) % SideStream::kSlots;
+      t->seq = ++ss->gseq;
+      const hipError_t r = hipStreamWriteValue32(from, ss->flags + t->slot, t->seq, 0);
+      return r == hipSuccess ? 0 : fail(r);
+    }
+    t->ev = ss->ev[ss->next];
+    ss->next = (ss->next + 1) % 64;
+    const hipError_t r = hipEventRecord(t->ev, from);
+    return r == hipSuccess ? 0 : fail(r);
+  }
+  int wait(hipStream_t to, const SyncTok& t) {
+    hipError_t r = hipSuccess;
+    if (t.slot >= 0)
+      r = hipStreamWaitValue32(to, ss->flags + t.slot, t.seq, hipStreamWaitValueGte, 0xffffffffu);
+    else if (t.ev)
+      r = hipStreamWaitEvent(to, t.ev, 0);
+    return r == hipSuccess ? 0 : fail(r);
+  }
   int event_pair(hipStream_t from, hipStream_t to) {
     if (from == to) return 0;
-    hipEvent_t e = ss->ev[ss->next];
-    ss->next = (ss->next + 1) % 64;
-    hipError_t r = hipEventRecord(e, from);
-    if (r == hipSuccess) r = hipStreamWaitEvent(to, e, 0);
-    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
-    return 0;
+    SyncTok t;
+    DS_TRY(signal(from, &t));
+    return wait(to, t);
   }
   int fork() { return event_pair(st, sd); }  // side sees everything the main chain issued so far
   int join() { return event_pair(sd, st); }  // main waits for everything issued on the side
@@ -502,8 +556,8 @@ struct Fwd {
   hipStream_t st;
   Streams ks;
   bool params_forked = false;
-  bool e_side = false;           // E = x transposed is issued on the side stream (event e_ready)
-  hipEvent_t e_ready = nullptr;
+  bool e_side = false;           // E = x transposed is issued on the side stream (token e_ready)
+  SyncTok e_ready;
   ChebFl fl;
 
   int stage_tat() {
@@ -547,10 +601,7 @@ struct Fwd {
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
     // LN_N(fc + E) (:100)
-    if (e_side) {
-      const hipError_t r = hipStreamWaitEvent(st, e_ready, 0);
-      if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
-    }
+    if (e_side) DS_TRY(ks.wait(st, e_ready));
     {
       LnFwd a;
       a.R = (int)m.BFT; a.L = m.N;
@@ -702,10 +753,7 @@ struct Fwd {
       DS_TRY(ks.fork());
       if (!m.first) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
         DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, (int64_t)m.N * m.FT, m.FT * m.N, 0.f, ks.sd));
-        e_ready = ks.ss->ev[ks.ss->next];
-        ks.ss->next = (ks.ss->next + 1) % 64;
-        const hipError_t r = hipEventRecord(e_ready, ks.sd);
-        if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
+        DS_TRY(ks.signal(ks.sd, &e_ready));
         e_side = true;
       }
       if (!m.agg) DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
@@ -758,21 +806,16 @@ struct Bwd {
   }
   int fork() { return ks.fork(); }
   int join() { return ks.join(); }
-  // an event on the side stream that the main stream can wait for later (wait_side)
-  hipEvent_t dx_ready = nullptr;
-  int mark_side(hipEvent_t* ev) {
-    if (sd == st) { *ev = nullptr; return 0; }
-    *ev = ks.ss->ev[ks.ss->next];
-    ks.ss->next = (ks.ss->next + 1) % 64;
-    const hipError_t r = hipEventRecord(*ev, sd);
-    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
-    return 0;
+  // a point on the side stream that the main stream can wait for later (wait_side)
+  SyncTok dx_ready;
+  int mark_side(SyncTok* t) {
+    *t = SyncTok{};
+    if (sd == st) return 0;
+    return ks.signal(sd, t);
   }
-  int wait_side(hipEvent_t ev) {
-    if (!ev) return 0;
-    const hipError_t r = hipStreamWaitEvent(st, ev, 0);
-    if (r != hipSuccess) { set_last_error(std::string("side stream: ") + hipGetErrorString(r)); return (int)r; }
-    return 0;
+  int wait_side(const SyncTok& t) {
+    if (sd == st) return 0;
+    return ks.wait(st, t);
   }
 
   // TAt LayerNorm backward: gamma / beta partial slabs (both fit in the (BFT, N) gcon_a)
