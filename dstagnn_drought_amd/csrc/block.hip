@@ -44,7 +44,7 @@ struct Arena {
 struct Dims {
   int B, N, F, T, h, dk, dv, D, K, C;
   int64_t FT, BFT, BN, NN, HQ, HV, QW, KD, KC, CT, KCT, S;
-  int Tg[3], Lp[3], ks[3];
+  int Tg[3], ks[3];
   bool first, sparse, flash;
   bool fsmall;      // flash on a small graph (flash_small): the LDS-staged kernels
   bool agg;         // sparse path in aggregate-first order (cheb_agg.hip): no x Theta GEMM
@@ -59,7 +59,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.FT = (int64_t)m.F * m.T; m.BFT = (int64_t)m.B * m.FT; m.BN = (int64_t)m.B * m.N; m.NN = (int64_t)m.N * m.N;
   m.HQ = (int64_t)m.h * m.dk; m.HV = (int64_t)m.h * m.dv; m.QW = 2 * m.HQ + m.HV; m.KD = (int64_t)m.K * m.dk;
   m.KC = (int64_t)m.K * m.C; m.CT = (int64_t)m.C * m.T; m.KCT = m.KC * m.T; m.S = 3 * (int64_t)m.T - 12;
-  for (int g = 0; g < 3; ++g) { m.ks[g] = 3 + 2 * g; m.Tg[g] = m.T - m.ks[g] + 1; m.Lp[g] = m.T + m.ks[g] - 1; }
+  for (int g = 0; g < 3; ++g) { m.ks[g] = 3 + 2 * g; m.Tg[g] = m.T - m.ks[g] + 1; }
   m.first = (m.F == 1);
   m.sparse = d.cheb_sparse != 0;
   m.flash = m.sparse && d.cheb_flash != 0;
@@ -161,7 +161,7 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.bcon_s = a.take(m.BN * m.D);
   s.gcon_a = a.take(m.BFT * m.N);
   s.gcon_e = m.first ? a.take((int64_t)m.B * m.T * m.N) : nullptr;
-  for (int g = 0; g < 3; ++g) s.dconv[g] = a.take(m.BN * 2 * m.C * m.Lp[g]);
+  for (int g = 0; g < 3; ++g) s.dconv[g] = a.take((m.BN * m.T + m.ks[g] - 1) * 2 * m.C);  // gtu_tail.hip layout
   s.dW = m.flash ? nullptr : a.take((int64_t)m.B * m.K * m.NN);
   s.dzs = m.flash ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
   s.dzs_r = m.fsmall ? a.take((int64_t)m.B * m.K * m.nnz) : nullptr;
@@ -446,6 +446,7 @@ struct SideStream {
   uint32_t gseq = 0;
   int fnext = 0;
   bool use_flags = true;
+  bool side_flags = false;  // DSTAGNN_SYNC_EVENTS=2: flags for the side stream's signals too
   bool ok = false;
 };
 
@@ -465,7 +466,8 @@ SideStream* side_stream_for_device() {
     if (hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
     for (auto& e : s.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    s.use_flags = !events;
+    s.use_flags = !events || atoi(getenv("DSTAGNN_SYNC_EVENTS")) == 2;
+    s.side_flags = events && atoi(getenv("DSTAGNN_SYNC_EVENTS")) == 2;
     if (s.use_flags) {
       if (hipMalloc(&s.flags, sizeof(uint32_t) * SideStream::kSlots) != hipSuccess ||
           hipMemset(s.flags, 0, sizeof(uint32_t) * SideStream::kSlots) != hipSuccess ||
@@ -486,14 +488,19 @@ struct SyncTok {
 };
 
 // fork / join between the caller's stream and the side stream (no-ops when disabled).
-// Default: stream-ordered flag writes (hipStreamWriteValue32 of a fresh sequence number into a
-// flag word, after all prior work of the producer stream) and waits (hipStreamWaitValue32,
-// >= that number) — on gfx950 / ROCm 7.2 an hipEventRecord between two kernels leaves the
-// recording stream idle for ~5.6 us (tools/fork_probe.hip: 5.56 us median gap) while the
-// write / wait-value packets cost nothing on the device timeline; tools/flag_sync_probe.hip
-// checks the data dependency both ways (0 stale reads in 600 rounds).  Flag words rotate over
-// kSlots; numbers only grow, so a wait can only be released by its own write or a later one
-// issued behind it.  DSTAGNN_SYNC_EVENTS=1 restores the event pairs.
+// Prices on gfx950 / ROCm 7.2 (tools/fork_probe.hip, tools/flag_sync_probe.hip, step timelines):
+// an hipEventRecord between two kernels idles the RECORDING stream ~5.6 us, while waiting for an
+// event that has already completed costs the waiting stream nothing; a stream-ordered flag write
+// (hipStreamWriteValue32 of a fresh sequence number into a device-memory flag word, after all
+// prior work of the producer stream) and a flag wait (hipStreamWaitValue32, >= that number) run
+// as small ROCclr kernels of ~4 us each on their streams.  (Flags in hipMallocSignalMemory do
+// NOT order the data: stale reads in flag_sync_probe; device memory: 0 stale reads in 600
+// rounds both ways.)  So the main chain never records an event: a dependency made BY the main
+// stream (fork) is a flag write on main + a flag wait on the side; one made by the side stream
+// (join, dx_ready) is an event recorded on the side, usually complete by the time the main
+// stream waits for it.  Flag words rotate over kSlots; numbers only grow, so a wait can only
+// be released by its own write or a later one issued behind it.  DSTAGNN_SYNC_EVENTS=1: events
+// both ways; =2: flags both ways.
 struct Streams {
   hipStream_t st = nullptr, sd = nullptr;
   SideStream* ss = nullptr;
@@ -509,7 +516,7 @@ struct Streams {
   int signal(hipStream_t from, SyncTok* t) {
     *t = SyncTok{};
     if (!ss) return 0;
-    if (ss->use_flags) {
+    if (ss->use_flags && (from != ss->side || ss->side_flags)) {
       t->slot = ss->fnext;
       ss->fnext = (ss->fnext + 1) % SideStream::kSlots;
       t->seq = ++ss->gseq;
@@ -749,14 +756,17 @@ struct Fwd {
     DS_TRY(stage_params());
     ht.lap("params");
     ChebIO c = cheb_io();
-    if (split) {  // x Theta needs only x and Theta: it runs beside the whole attention chain
+    // aggregate-first Chebyshev (m.agg) has no x Theta GEMM: the side stream then carries only
+    // E = x transposed, which the main chain awaits by its own token (e_ready)
+    const bool side_xth = split && !m.agg;
+    if (split && (side_xth || !m.first)) {  // x Theta needs only x and Theta: it runs beside the whole attention chain
       DS_TRY(ks.fork());
       if (!m.first) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
         DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, (int64_t)m.N * m.FT, m.FT * m.N, 0.f, ks.sd));
         DS_TRY(ks.signal(ks.sd, &e_ready));
         e_side = true;
       }
-      if (!m.agg) DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
+      if (side_xth) DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
     }
     DS_TRY(stage_tat());
     ht.lap("tat");
@@ -766,7 +776,7 @@ struct Fwd {
     ht.lap("sat");
     if (split) {
       DS_TRY(cheb_softmax(c, st));
-      DS_TRY(ks.join());
+      if (side_xth) DS_TRY(ks.join());
       DS_TRY(cheb_aggregate(c, w.gemm_ws, st));
     } else {
       DS_TRY(stage_cheb());
@@ -849,11 +859,15 @@ struct Bwd {
     t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c;
     t.dout = dout; t.gcontrib = w.gcon_t; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
     t.rcontrib = w.bcon_t; t.dres = w.dres_t; t.dG = w.dGt;
+    // per-node [bn][C] partial sums of the LN gamma / beta (and first-block residual_conv)
+    // contributions instead of the (B,N,C,T) tensors: the column sums below read BN*C floats
+    t.gpart = w.gcon_t; t.bpart = w.gcon_t + m.BN * m.C;
+    if (m.first) { t.rpart = w.bcon_t; t.dpart = w.bcon_t + m.BN * m.C; }
     DS_TRY(op_gtu_tail_bwd(t, st));
     // --- side: LN / residual / fcmy / GTU parameter gradients (one fork)
     DS_TRY(fork());
-    DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {dout, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
-                    {w.dres_t, m.first ? gd.res_b : nullptr}}, m.BN, m.C, m.T));
+    DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + m.BN * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
+                    {w.bcon_t + m.BN * m.C, m.first ? gd.res_b : nullptr}}, m.BN, m.C, 1));
     // the bias gradients ride on their weight-gradient GEMMs as a column-sum column
     // (Gemm::ones_out: sum over the reduction of the gradient operand); a bias whose weight
     // gradient is not requested gets its own column sum
@@ -872,9 +886,9 @@ struct Bwd {
       Gemm dws[3];
       int nw = 0;
       for (int q = 0; q < 3; ++q) {
-        const int ks = m.ks[q], Tg = m.Tg[q], Lp = m.Lp[q];
+        const int ks = m.ks[q], Tg = m.Tg[q];
         const int64_t C2 = 2 * (int64_t)m.C;
-        const int64_t cs = C2 * Lp;  // per-(b,n) stride of the padded dconv rows (t', o)
+        const int64_t cs = C2 * m.T;  // per-(b,n) stride of the padded dconv rows (t', o)
         if (gd.gtu_w[q]) {
           Gemm& g = dws[nw++];  // dW[o,c,j] = sum_{(bn,t')} dconv[bn,t',o] X[bn,t'+j,c]; db[o] = sum dconv[.,o]
           g.M = (int)C2; g.N = m.C * ks; g.K = (int)(m.BN * Tg);
@@ -883,7 +897,7 @@ struct Bwd {
           g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx2(m.C, ks, 1);
           g.ones_out = gd.gtu_b[q];
         } else {
-          DS_TRY(colsum_on(sd, w.dconv[q], m.BN * Lp, (int)C2, 1, gd.gtu_b[q]));
+          DS_TRY(colsum_on(sd, w.dconv[q], m.BN * m.T + ks - 1, (int)C2, 1, gd.gtu_b[q]));
         }
       }
       if (nw) DS_TRY(run_gemm_group(dws, nw, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd));
@@ -896,7 +910,7 @@ struct Bwd {
       for (int q = 0; q < 3; ++q) {
         const int ks = m.ks[q];
         const int64_t C2 = 2 * (int64_t)m.C;
-        const int64_t cs = C2 * m.Lp[q];
+        const int64_t cs = C2 * m.T;
         Gemm& g = segs[q];
         g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
         g.A = w.dconv[q]; g.am = idx2(m.T, C2, cs); g.ak = idx1(1);

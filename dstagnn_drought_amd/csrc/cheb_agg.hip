@@ -60,19 +60,37 @@ __device__ __forceinline__ int64_t xcd_block(int on) {
   return (p & 7) * per + (p >> 3);
 }
 
-constexpr int kE = 4;      // support entries per batch (one memory round per batch)
-// occupancy the register allocator targets (waves per SIMD): these kernels are chains of
-// dependent gathers, so resident waves hide the latency
-#ifndef DSTAGNN_AGG_WPE
-#define DSTAGNN_AGG_WPE 4
-#endif
+constexpr int kE = 4;      // support entries per batch
+// Support walks: a chunk of up to 64 entries is loaded ONE per lane (indices and the K weights),
+// entry e's values then come back by v_readlane (wave-uniform e: the gathered row's base is an
+// SGPR), and the gathered rows of batch e0 + kE are issued before batch e0 is multiplied (two
+// batches in flight instead of three dependent round trips per batch).
+__device__ __forceinline__ int rl_i(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+__device__ __forceinline__ float rl_f(float v, int i) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+}
+// occupancy the register allocator targets (waves per SIMD) from an estimate of the VGPRs a
+// variant needs (two batches of gathered rows, the K accumulators / dot products, addresses):
+// as many resident waves as fit without spills (PEMS08: fwd / spmm_t 4, sddmm 3)
+// (thresholds fitted to the compiler's allocation of every instantiated variant: no spills)
+template <int kNQ>
+constexpr bool agg_prefetch() { return kNQ <= 8; }  // wider rows: one batch in flight
+template <int kNQ, int KM>
+constexpr int gather_wpe() {
+  return kNQ >= 12 ? 2 : (agg_prefetch<kNQ>() ? 2 : 1) * kE * kNQ + KM * kNQ + 40 <= 110 ? 4
+       : ((agg_prefetch<kNQ>() ? 2 : 1) * kE * kNQ + KM * kNQ + 40 <= 125 ? 3 : 2);
+}
+template <int kNQ, int KM>
+constexpr int sddmm_wpe() {
+  return KM <= 3 && (agg_prefetch<kNQ>() ? 2 : 1) * kE * kNQ + 16 + KM * kNQ + 64 <= 150 ? 3 : 2;
+}
 constexpr int kAs = 33;    // LDS row stride of a 32 x 32 operand tile
 
 // ---------------------------------------------------------------------------------------
 // forward: one wave per (b, j, time chunk)
 // ---------------------------------------------------------------------------------------
 template <int kNQ, int KM>  // kNQ >= F * Tc / 64, KM >= K
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <= 24 ? DSTAGNN_AGG_WPE : 2, 8))) void cheb_agg_fwd_kernel(ChebAg a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<kNQ, KM>(), 8))) void cheb_agg_fwd_kernel(ChebAg a) {
   __shared__ float As[4][32 * kAs];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
@@ -96,33 +114,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <=
   for (int k = 0; k < KM; ++k)
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) ag[k][q] = 0.f;
-  for (int pb = p0; pb < p1; pb += kE) {
-    int rows[kE];
+  for (int c0 = p0; c0 < p1; c0 += 64) {
+    const int nc = min(64, p1 - c0), pl = c0 + min(lane, nc - 1);
+    const int rowl = a.csc_row[pl];
+    float wl[KM];  // W_k[row, j] of this lane's entry (0 past the chunk)
 #pragma unroll
-    for (int e = 0; e < kE; ++e) rows[e] = a.csc_row[min(pb + e, p1 - 1)];
-    float wk[KM][kE], v[kE][kNQ];
-#pragma unroll
-    for (int e = 0; e < kE; ++e) {
-      const int p = min(pb + e, p1 - 1);
-      const int64_t o = (int64_t)rows[e] * a.N + j;
-#pragma unroll
-      for (int k = 0; k < KM; ++k) {
-        float ww = 0.f;
-        if (k < a.K)
-          ww = a.wsupp ? a.wsupp[((int64_t)b * a.K + k) * a.nnz + p]
-                       : a.cheb[(int64_t)k * NN + o] * a.P[((int64_t)b * a.K + k) * NN + o];
-        wk[k][e] = pb + e < p1 ? ww : 0.f;
+    for (int k = 0; k < KM; ++k) {
+      float ww = 0.f;
+      if (k < a.K) {
+        const int64_t o = (int64_t)rowl * a.N + j;
+        ww = a.wsupp ? a.wsupp[((int64_t)b * a.K + k) * a.nnz + pl]
+                     : a.cheb[(int64_t)k * NN + o] * a.P[((int64_t)b * a.K + k) * NN + o];
       }
-      const float* xr = xb + (int64_t)rows[e] * FT;
-#pragma unroll
-      for (int q = 0; q < kNQ; ++q) v[e][q] = xr[xo[q]];
+      wl[k] = lane < nc ? ww : 0.f;
     }
+    auto gather = [&](int e0, float (&dst)[kE][kNQ]) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k)
+      for (int e = 0; e < kE; ++e) {
+        const float* xr = xb + (int64_t)rl_i(rowl, min(e0 + e, nc - 1)) * FT;
 #pragma unroll
-      for (int e = 0; e < kE; ++e)
+        for (int q = 0; q < kNQ; ++q) dst[e][q] = xr[xo[q]];
+      }
+    };
+    float v[kE][kNQ];
+    if constexpr (agg_prefetch<kNQ>()) gather(0, v);
+    for (int e0 = 0; e0 < nc; e0 += kE) {
+      float vn[kE][kNQ];
+      if constexpr (agg_prefetch<kNQ>()) gather(e0 + kE, vn);  // the next batch (clamped: harmless re-reads past the chunk)
+      else gather(e0, v);
 #pragma unroll
-        for (int q = 0; q < kNQ; ++q) ag[k][q] = fmaf(wk[k][e], v[e][q], ag[k][q]);
+      for (int k = 0; k < KM; ++k)
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          const float wk = rl_f(wl[k], e0 + e);  // e0 + e <= 63; lanes >= nc hold 0
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) ag[k][q] = fmaf(wk, v[e][q], ag[k][q]);
+        }
+      if constexpr (agg_prefetch<kNQ>()) {
+#pragma unroll
+        for (int e = 0; e < kE; ++e)
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) v[e][q] = vn[e][q];
+      }
+    }
   }
   floatx16 acc = zero16();
 #pragma unroll
@@ -170,7 +204,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <=
 // dzs = P T dW and c_j instead, as cheb_sparse.hip).
 // ---------------------------------------------------------------------------------------
 template <int kNQ, int KM>  // kNQ >= min(F*T, 1024) / 64
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <= 24 ? DSTAGNN_AGG_WPE : 2, 8))) void cheb_agg_sddmm_kernel(ChebAg a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<kNQ, KM>(), 8))) void cheb_agg_sddmm_kernel(ChebAg a) {
   extern __shared__ float Dg[];  // [waves][K][F * T]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
@@ -205,64 +239,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <=
   }
   wave_lds_sync();
   const float* xb = a.x + (int64_t)b * a.N * FT;
-  float csum[KM];
-#pragma unroll
-  for (int k = 0; k < KM; ++k) csum[k] = 0.f;
-  for (int pb = p0; pb < p1; pb += kE) {
-    int rows[kE];
-#pragma unroll
-    for (int e = 0; e < kE; ++e) rows[e] = a.csc_row[min(pb + e, p1 - 1)];
-    float s4[KM][kE];
-#pragma unroll
-    for (int k = 0; k < KM; ++k)
-#pragma unroll
-      for (int e = 0; e < kE; ++e) s4[k][e] = 0.f;
-    for (int e0 = 0; e0 < FT; e0 += 64 * kNQ) {  // one pass unless F*T > 64 kNQ (long series)
-      float v[kE][kNQ];
+  // the KM x kE dot products of a batch reduce across the wave together (wave_sum_many):
+  // lane owns value j = k kE + e, one lane of each 64 / NV does the stores
+  constexpr int NV0 = KM * kE, NV = NV0 <= 16 ? 16 : (NV0 <= 32 ? 32 : 64);
+  constexpr int LG = NV == 16 ? 4 : (NV == 32 ? 5 : 6);
+  const int jl = (lane >> (6 - LG)) & (NV - 1), kl = jl / kE, el = jl - kl * kE;
+  const bool owner = (lane & ((64 >> LG) - 1)) == 0 && jl < NV0 && kl < a.K;
+  float csum = 0.f;  // this lane's share of c_j for order kl
+  for (int c0 = p0; c0 < p1; c0 += 64) {
+    const int nc = min(64, p1 - c0);
+    const int rowl = a.csc_row[c0 + min(lane, nc - 1)];
+    // rows of entries e0.. (elements e1 + lane + 64 q of each x row)
+    auto gather = [&](int e0, int e1, float (&dst)[kE][kNQ]) {
 #pragma unroll
       for (int e = 0; e < kE; ++e) {
-        const float* xr = xb + (int64_t)rows[e] * FT;
+        const float* xr = xb + (int64_t)rl_i(rowl, min(e0 + e, nc - 1)) * FT;
 #pragma unroll
-        for (int q = 0; q < kNQ; ++q) v[e][q] = xr[min(e0 + lane + 64 * q, FT - 1)];
+        for (int q = 0; q < kNQ; ++q) dst[e][q] = xr[min(e1 + lane + 64 * q, FT - 1)];
       }
+    };
+    auto accum = [&](int e1, const float (&v)[kE][kNQ], float (&sf)[NV]) {
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         if (k >= a.K) break;
 #pragma unroll
         for (int q = 0; q < kNQ; ++q) {
-          const int el = e0 + lane + 64 * q;
-          const float d = el < FT ? dg[(int64_t)k * FT + el] : 0.f;
+          const int el2 = e1 + lane + 64 * q;
+          const float d = el2 < FT ? dg[(int64_t)k * FT + el2] : 0.f;
 #pragma unroll
-          for (int e = 0; e < kE; ++e) s4[k][e] = fmaf(v[e][q], d, s4[k][e]);
+          for (int e = 0; e < kE; ++e) sf[k * kE + e] = fmaf(v[e][q], d, sf[k * kE + e]);
         }
       }
-    }
+    };
+    float v[kE][kNQ];
+    if constexpr (agg_prefetch<kNQ>()) gather(0, 0, v);
+    for (int e0 = 0; e0 < nc; e0 += kE) {
+      float vn[kE][kNQ];
+      if constexpr (agg_prefetch<kNQ>()) gather(e0 + kE, 0, vn);  // the next batch's first element range, in flight meanwhile
+      else gather(e0, 0, v);
+      float sf[NV];  // dot products, value k kE + e (zero padded to NV: reduced in place)
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      if (k >= a.K) break;
-      const int64_t zk = ((int64_t)b * a.K + k) * a.nnz;
-#pragma unroll
-      for (int e = 0; e < kE; ++e) {
-        const float s = wave_sum(s4[k][e]);
-        const int p = pb + e;
-        if (p >= p1) break;
-        if (a.dzs) {
-          const float dd = a.psupp[zk + p] * (a.tsupp[(int64_t)k * a.nnz + p] * s);
-          csum[k] += dd;
-          if (lane == 0) {
-            a.dzs[zk + p] = dd;
-            if (a.dzs_r) a.dzs_r[zk + a.csc2csr[p]] = dd;
-          }
-        } else if (lane == 0) {
-          a.dW[((int64_t)b * a.K + k) * NN + (int64_t)rows[e] * a.N + j] = s;
+      for (int jj = 0; jj < NV; ++jj) sf[jj] = 0.f;
+      accum(0, v, sf);
+      if constexpr (kNQ == 16) {  // F*T > 1024 (long series; nq_of gives 16): the rest of the rows
+        for (int e1 = 64 * kNQ; e1 < FT; e1 += 64 * kNQ) {
+          float vx[kE][kNQ];
+          gather(e0, e1, vx);
+          accum(e1, vx, sf);
         }
+      }
+      // the support weights of the owned entry, loaded before the reduction (independent of it)
+      const int p = c0 + e0 + el;
+      const bool mine = owner && e0 + el < nc;
+      const int64_t zk = ((int64_t)b * a.K + kl) * a.nnz;
+      float ps = 0.f, ts = 0.f;
+      if (mine && a.dzs) {
+        ps = a.psupp[zk + p];
+        ts = a.tsupp[(int64_t)kl * a.nnz + p];
+      }
+      const float sv = wave_sum_many<NV>(sf);
+      if (mine) {
+        if (a.dzs) {
+          const float dd = ps * (ts * sv);
+          csum += dd;
+          a.dzs[zk + p] = dd;
+          if (a.dzs_r) a.dzs_r[zk + a.csc2csr[p]] = dd;
+        } else {
+          a.dW[((int64_t)b * a.K + kl) * NN + (int64_t)a.csc_row[p] * a.N + j] = sv;
+        }
+      }
+      if constexpr (agg_prefetch<kNQ>()) {
+#pragma unroll
+        for (int e = 0; e < kE; ++e)
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) v[e][q] = vn[e][q];
       }
     }
   }
-  if (a.dzs && lane == 0) {
+  if (a.dzs) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k)
-      if (k < a.K) a.cc[((int64_t)b * a.K + k) * a.N + j] = csum[k];
+    for (int k = 0; k < KM; ++k) {
+      if (k >= a.K) break;
+      const float c = wave_sum(owner && kl == k ? csum : 0.f);
+      if (lane == 0) a.cc[((int64_t)b * a.K + k) * a.N + j] = c;
+    }
   }
 }
 
@@ -272,7 +332,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <=
 // dx_i[f, t'] += sum_k sum_c Theta_k[f][c] h_k[t'][c] on the matrix cores.
 // ---------------------------------------------------------------------------------------
 template <int kNQ, int KM>  // kNQ >= Tc * C / 64
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <= 24 ? DSTAGNN_AGG_WPE : 2, 8))) void cheb_agg_spmm_t_kernel(ChebAg a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<kNQ, KM>(), 8))) void cheb_agg_spmm_t_kernel(ChebAg a) {
   __shared__ float Hs[4][32 * kAs];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
@@ -296,36 +356,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNQ * KM <=
   for (int k = 0; k < KM; ++k)
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) hv[k][q] = 0.f;
-  for (int pb = q0; pb < q1; pb += kE) {
-    int cols[kE], ci[kE];
-#pragma unroll
-    for (int e = 0; e < kE; ++e) {
-      const int p = min(pb + e, q1 - 1);
-      cols[e] = a.csr_col[p];
-      ci[e] = a.wsupp ? a.csr2csc[p] : 0;
-    }
-    float wk[KM][kE], v[kE][kNQ];
-#pragma unroll
-    for (int e = 0; e < kE; ++e) {
-      const int64_t o = (int64_t)i * a.N + cols[e];
+  for (int c0 = q0; c0 < q1; c0 += 64) {
+    const int nc = min(64, q1 - c0), pl = c0 + min(lane, nc - 1);
+    const int coll = a.csr_col[pl];
+    float wl[KM];  // W_k[i, col] of this lane's entry (0 past the chunk)
+    {
+      const int ci = a.wsupp ? a.csr2csc[pl] : 0;
+      const int64_t o = (int64_t)i * a.N + coll;
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         float ww = 0.f;
         if (k < a.K)
-          ww = a.wsupp ? a.wsupp[((int64_t)b * a.K + k) * a.nnz + ci[e]]
+          ww = a.wsupp ? a.wsupp[((int64_t)b * a.K + k) * a.nnz + ci]
                        : a.cheb[(int64_t)k * NN + o] * a.P[((int64_t)b * a.K + k) * NN + o];
-        wk[k][e] = pb + e < q1 ? ww : 0.f;
+        wl[k] = lane < nc ? ww : 0.f;
       }
-      const float* gr = gb + (int64_t)cols[e] * a.T * a.C;
-#pragma unroll
-      for (int q = 0; q < kNQ; ++q) v[e][q] = gr[go[q]];
     }
+    auto gather = [&](int e0, float (&dst)[kE][kNQ]) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k)
+      for (int e = 0; e < kE; ++e) {
+        const float* gr = gb + (int64_t)rl_i(coll, min(e0 + e, nc - 1)) * a.T * a.C;
 #pragma unroll
-      for (int e = 0; e < kE; ++e)
+        for (int q = 0; q < kNQ; ++q) dst[e][q] = gr[go[q]];
+      }
+    };
+    float v[kE][kNQ];
+    if constexpr (agg_prefetch<kNQ>()) gather(0, v);
+    for (int e0 = 0; e0 < nc; e0 += kE) {
+      float vn[kE][kNQ];
+      if constexpr (agg_prefetch<kNQ>()) gather(e0 + kE, vn);  // the next batch, in flight meanwhile
+      else gather(e0, v);
 #pragma unroll
-        for (int q = 0; q < kNQ; ++q) hv[k][q] = fmaf(wk[k][e], v[e][q], hv[k][q]);
+      for (int k = 0; k < KM; ++k)
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          const float wk = rl_f(wl[k], e0 + e);  // e0 + e <= 63; lanes >= nc hold 0
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) hv[k][q] = fmaf(wk, v[e][q], hv[k][q]);
+        }
+      if constexpr (agg_prefetch<kNQ>()) {
+#pragma unroll
+        for (int e = 0; e < kE; ++e)
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) v[e][q] = vn[e][q];
+      }
+    }
   }
   floatx16 acc = zero16();
 #pragma unroll

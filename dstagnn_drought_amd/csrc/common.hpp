@@ -167,6 +167,31 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// NV independent full-wave sums at once (NV = 2^L <= 64): L halving exchange steps (offsets
+// 32, 16, ...: each lane keeps the half of its values its offset bit selects and adds the
+// partner's copy of that half), then plain butterflies; NV - 1 + 6 - L shuffles instead of 6 NV.
+// Returns the total of value j = (lane >> (6 - L)) & (NV - 1) (held by 64 / NV lanes).  Fixed
+// order: deterministic.
+template <int NV>
+__device__ __forceinline__ float wave_sum_many(float (&v)[NV]) {
+  static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "power of two <= 64");
+  const int lane = (int)(threadIdx.x & 63);
+  int o = 32;
+#pragma unroll
+  for (int n = NV; n > 1; n >>= 1, o >>= 1) {
+    const bool hi = (lane & o) != 0;
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i) {
+      const float keep = hi ? v[i + n / 2] : v[i];
+      const float send = hi ? v[i] : v[i + n / 2];
+      v[i] = keep + __shfl_xor(send, o, 64);
+    }
+  }
+  float r = v[0];
+#pragma unroll
+  for (; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+  return r;
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -242,8 +242,8 @@ __global__ __launch_bounds__(256) void gtu_gates_kernel(GtuTailArgs a, int nchun
   }
 }
 
-// Split path, gates backward: one (node, gate, 64-row chunk of the zero-padded (t', o)
-// output) per 256-thread workgroup.  The dG slice is read along s (coalesced), transposed
+// Split path, gates backward: one (node, gate, 64-row chunk of the node's zero-padded (t', o)
+// rows, the shared-pad layout of the fused kernel) per 256-thread workgroup.  The dG slice is read along s (coalesced), transposed
 // through LDS to [t][c]; conv rows and the output rows are walked with o fastest.
 __global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int nchunk) {
   extern __shared__ float lds[];
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int n
   const int chunk = id % nchunk; id /= nchunk;
   const int gi = id % 3;
   const int64_t bn = id / 3;
-  const int ks = 3 + 2 * gi, Tg = T - ks + 1, Lp = T + ks - 1;
+  const int ks = 3 + 2 * gi, Tg = T - ks + 1, Lp = T + (bn == a.BN - 1 ? ks - 1 : 0);  // rows of this node
   const int off = gi == 0 ? 0 : (gi == 1 ? T - 2 : 2 * T - 6);
   const int tp0 = chunk * kGsW;
   if (tp0 >= Lp) return;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int n
   }
   __syncthreads();
   const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
-  float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * (int64_t)C2 * Lp;
+  float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * (int64_t)C2 * T;
   for (int e = tid; e < kGsW * C2; e += 256) {
     const int tl = e / C2, o = e - tl * C2, tp = tp0 + tl;
     if (tp >= Lp) continue;
@@ -295,6 +295,8 @@ struct TailBwdLds {
     total = wl + (stage_w ? T * S : 0);
   }
 };
+
+
 
 // PH: 0 = fused, 1 = split path: LN / residual backward to dtc only (dG by a GEMM, the
 // gates backward in gtu_gates_bwd_kernel)
@@ -343,10 +345,23 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         xhl[e] = xh;
         rr[e] = rv[u];
         dxh[e] = dyv[u] * a.ln_g[c];
-        a.gcontrib[base + e] = dyv[u] * xh;
+        if (!a.gpart) a.gcontrib[base + e] = dyv[u] * xh;
       }
     }
     __syncthreads();
+    if (a.gpart) {  // LN gamma / beta: sum_t dout * xhat and sum_t dout per channel of this node
+      // (dout re-read from L1 / L2: the node's 4*C*T bytes were just loaded)
+      for (int c = tid; c < C; c += NT) {
+        float g = 0.f, b = 0.f;
+        for (int t = 0; t < T; ++t) {
+          const float dy = a.dout[base + c * T + t];
+          g = fmaf(dy, xhl[c * T + t], g);
+          b += dy;
+        }
+        a.gpart[bn * C + c] = g;
+        a.bpart[bn * C + c] = b;
+      }
+    }
     for (int l = tid; l < L.P * T; l += NT) {  // sum_c dxhat and dxhat*xhat per t, P lane groups
       const int t = l % T, part = l / T;
       float s1 = 0.f, s2 = 0.f;
@@ -387,9 +402,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         a.dtc[base + e] = dtc;
         if (a.first) {
           dXs[t * CP + c] = 0.f;
-          a.rcontrib[base + e] = dr * xv[u];
-          a.dres[base + e] = dr;
-          xhl[e] = dr;  // for the residual_conv channel reduction below
+          if (!a.rpart) {
+            a.rcontrib[base + e] = dr * xv[u];
+            a.dres[base + e] = dr;
+          }
+          xhl[e] = dr;  // for the residual_conv channel reduction below (and its partial sums)
         } else {
           dXs[t * CP + c] = dtco;  // dX rows are (t, c), like X
           a.dx[base + e] = dr;
@@ -406,6 +423,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         for (int c = 0; c < C; ++c) sum += a.res_w[c] * xhl[c * T + t];
         a.dx[bn * T + t] = sum;
       }
+      if (a.rpart) {  // residual_conv weight / bias: sum_t dr * x and sum_t dr per channel
+        for (int c = tid; c < C; c += NT) {
+          float rw = 0.f, rb = 0.f;
+          for (int t = 0; t < T; ++t) {
+            rw = fmaf(xhl[c * T + t], a.x[bn * T + t], rw);
+            rb += xhl[c * T + t];
+          }
+          a.rpart[bn * C + c] = rw;
+          a.dpart[bn * C + c] = rb;
+        }
+      }
     }
     if (PH == 1) {
       __syncthreads();  // LDS reuse by the next node
@@ -420,15 +448,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       dGs[c * SP + s] = g;
     }
     __syncthreads();
-    // gates backward into the zero-padded (t', o) rows of each GTU
+    // gates backward into the zero-padded (t', o) rows of each GTU: node bn owns rows
+    // [bn*T, bn*T + T) = ks-1 zero rows, then its Tg gate rows; a transposed-convolution
+    // window of node bn reaches ks-1 rows into node bn+1, i.e. exactly its zero rows (the
+    // last node writes ks-1 trailing zero rows): half the zeros of a per-node [ks-1 | Tg |
+    // ks-1] layout
 #pragma unroll 1
     for (int gi = 0; gi < 3; ++gi) {
       const int ks = 3 + 2 * gi;
       const int Tg = T - ks + 1;
-      const int Lp = T + ks - 1;
       const int off = gi == 0 ? 0 : (gi == 1 ? T - 2 : 2 * T - 6);
-      const int E = C2 * Lp;
-      float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * E;
+      const int E = C2 * (T + (bn == a.BN - 1 ? ks - 1 : 0));
+      float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * C2 * T;
       const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
       #pragma unroll 1
       for (int e0 = 0; e0 < E; e0 += NT * kU) {

@@ -115,7 +115,10 @@ struct GtuTailArgs {
   float* dX = nullptr;            // residual part of d cheb output (B,N,T,C)
   float* dx = nullptr;            // d block input
   float* rcontrib = nullptr; float* dres = nullptr;  // first block residual_conv grads
-  float* dconv_pad[3] = {};       // [bn][T+ks-1][2C]
+  // per-node partial sums over t instead of the contribution tensors above ([bn][C] each;
+  // gpart: sum dout*xhat, bpart: sum dout; first block rpart: sum dr*x, dpart: sum dr)
+  float* gpart = nullptr; float* bpart = nullptr; float* rpart = nullptr; float* dpart = nullptr;
+  float* dconv_pad[3] = {};       // rows [bn*T + t'][2C]: ks-1 zero rows + T-ks+1 gate rows per node, ks-1 zero rows after the last
   float* dG = nullptr;            // [bn][C][3T-12] scratch of the split (long-series) backward
 };
 

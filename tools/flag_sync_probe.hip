@@ -4,6 +4,7 @@
 // on its stream; the consumer stream waits for flag >= tag and its kernel checks every X[i]
 // (all XCDs) and counts mismatches.  Both directions, 300 rounds each, and the same with the
 // event pair for reference.  Prints the mismatch counts (must be 0) and the wall time.
+// argv[1] = s: the flag words in hipMallocSignalMemory (else hipMalloc).
 //   hipcc -O3 --offload-arch=gfx950 tools/flag_sync_probe.hip -o tools/flag_sync_probe
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -24,14 +25,16 @@ __global__ void consume(const float* x, float tag, unsigned* err, float* y) {
   y[i] = v;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool sig = argc > 1 && argv[1][0] == 's';  // flags in hipMallocSignalMemory
   float *x, *y;
   unsigned* err;
   uint32_t* flag;
   (void)hipMalloc(&x, kN * 4);
   (void)hipMalloc(&y, kN * 4);
   (void)hipMalloc(&err, 64);
-  (void)hipMalloc(&flag, 4096);
+  if (sig) (void)hipExtMallocWithFlags((void**)&flag, 4096, hipMallocSignalMemory);
+  else (void)hipMalloc(&flag, 4096);
   (void)hipMemset(x, 0, kN * 4);
   (void)hipMemset(err, 0, 64);
   (void)hipMemset(flag, 0, 4096);
@@ -73,7 +76,7 @@ int main() {
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     unsigned h[4];
     (void)hipMemcpy(h, err, 16, hipMemcpyDeviceToHost);
-    printf("mode %d (%s %s): mismatches %u, %.3f ms per round\n", mode, mode < 2 ? "flags" : "events",
+    printf("%s mode %d (%s %s): mismatches %u, %.3f ms per round\n", sig ? "signal-mem" : "device-mem", mode, mode < 2 ? "flags" : "events",
            (mode & 1) ? "side->main" : "main->side", h[mode], ms / 300);
   }
   return 0;
