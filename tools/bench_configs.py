@@ -34,6 +34,8 @@ def flops(N, T, K, h, D, dk, C):
 
 def run(name, steps=10, warmup=3):
     import dstagnn_drought_amd as D_
+    steps = int(os.environ.get("BENCH_CONFIGS_STEPS", steps))  # short runs under the profiler
+    warmup = int(os.environ.get("BENCH_CONFIGS_WARMUP", warmup))
     N, T, K, h, Dm, dk, C, B = CONFIGS[name]
     B = int(os.environ.get("BENCH_CONFIGS_B", B))  # batch override (large-batch robustness runs)
     rs = np.random.RandomState(0)

@@ -28,6 +28,14 @@ for s in "${S[@]}"; do
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     dp2)    DSTAGNN_DIST_BACKEND=gloo DSTAGNN_DEVICE_MOD=1 run dp2 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-extras ;;
     pmcs)   echo "== pmcs ($(date +%T))"; bash tools/pmc_step.sh || exit $? ;;
+    pmcs_gambia) echo "== pmcs GAMBIA ($(date +%T))"; PMC_CONFIG=GAMBIA bash tools/pmc_step.sh || exit $? ;;
+    pmcs_syn)    echo "== pmcs SYN ($(date +%T))"; PMC_CONFIG=SYN bash tools/pmc_step.sh || exit $? ;;
+    pmcb)   echo "== pmcb ($(date +%T))"; bash tools/pmc_block.sh || exit $?; python3 tools/pmc_block_summary.py gpurun_out/pmcb > gpurun_out/pmcb_summary.txt ;;
+    steptrace) bash tools/step_trace.sh final || exit $? ;;
+    configs) BENCH_CONFIGS_STEPS=5 run configs 900 python tools/bench_configs.py ;;
+    trace_cfg) for c in GAMBIA SYN; do
+                 BENCH_CONFIGS_STEPS=3 BENCH_CONFIGS_WARMUP=1 run trace_$c 300 rocprofv3 --kernel-trace --stats -d gpurun_out/trace_cfg_$c -o run --output-format csv -- python3 tools/bench_configs.py $c
+               done ;;
     sweep)  run gemm_sweep 600 python tools/gemm_sweep.py ;;
     *) echo "unknown step $s" ;;
   esac

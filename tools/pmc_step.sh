@@ -4,10 +4,18 @@
 # WRITE_SIZE width calibration (tools/fetch_calib).  Summary: tools/pmc_step_summary.py.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/pmcs
+# PMC_CONFIG=GAMBIA|SYN|PEMS04|PEMS07: that BASELINE config through tools/bench_configs.py
+# (3 steps, one warmup) into gpurun_out/pmcs_<config>; default the bench block (PEMS08)
+CFG=${PMC_CONFIG:-}
+OUT=gpurun_out/pmcs${CFG:+_$CFG}
 mkdir -p $OUT
 export PYTHONDONTWRITEBYTECODE=1 DSTAGNN_SIDE_STREAM=0
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --hot-iters 2 --prof-steps 0"
+if [ -n "$CFG" ]; then
+  export BENCH_CONFIGS_STEPS=2 BENCH_CONFIGS_WARMUP=1
+  B="python3 tools/bench_configs.py $CFG"
+else
+  B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --hot-iters 2 --prof-steps 0"
+fi
 pass() {
   local name=$1; shift
   local ctrs=()
