@@ -11,7 +11,11 @@ logs = [l.strip()[7:] for l in open(sys.argv[2]) if l.startswith("[gemm]")]
 step = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 marks = [i for i, r in enumerate(rows) if "param_prep" in r["Kernel_Name"]]
 s0, s1 = marks[step], marks[step + 1]
-gi = sum(1 for r in rows[:s0] if "gemm_f32" in r["Kernel_Name"])
+def is_gemm(name):  # a launch that consumed one "[gemm]" host log line
+    return "gemm_f32" in name or "skinny_dw" in name
+
+
+gi = sum(1 for r in rows[:s0] if is_gemm(r["Kernel_Name"]))
 tot = 0.0
 cat = {}
 for r in rows[s0:s1]:
@@ -19,7 +23,7 @@ for r in rows[s0:s1]:
     tot += d
     nm = re.sub(r"\(anonymous namespace\)::|GemmK|\(.*", "", r["Kernel_Name"])[:44]
     extra = ""
-    if "gemm_f32" in r["Kernel_Name"]:
+    if is_gemm(r["Kernel_Name"]):
         extra = logs[gi] if gi < len(logs) else "?"
         gi += 1
         key = "gemm"
