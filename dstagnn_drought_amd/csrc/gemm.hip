@@ -73,31 +73,37 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmG gin) {
 }
 
 // ---------------------------------------------------------------------------------
-// Skinny long reductions: M and the kernel's N (with the column-sum column) <= 32, batch 1,
-// K >= kSkinnyMinK — the fcmy weight gradient (12 x 25 over B*N*C = 174K rows at PEMS08).
-// The tiled kernel's 128x32 tile wastes 90 % of its loads and MFMAs on clamped rows and
-// spends its time in per-k-tile DMA round trips.  Here every wave owns kpw consecutive k and
-// loads a round of kSkU k-quads at once (v_mfma_f32_16x16x4_f32, lane (q = l>>4, i = l&15):
-// A[mt*16 + i][k + q] and B[k + q][nt*16 + i]), then MT x NT MFMAs per quad into 16x16
-// accumulators (M <= 16 and N <= 32 at fcmy: 16 MFMA cycles per k, not the 32x32 tile's 32).
-// One 1024-thread workgroup per CU (<= 256 of them): its 16 accumulators fold in LDS, and the
-// workgroups' partials fold in ONE ticket level (colsum2d's hand-off: sc1 stores drained by
-// every storing wave, a barrier, one agent-scope ticket per workgroup; the last arrival
-// acquires, then all its 1024 threads sum the partials in a fixed order and apply the GEMM
-// epilogue).  One hand-off instead of a two-level tree: the acquire's price grows with the
-// workgroups per CU (MI355X_MICROARCH.md), so one per CU pays it once.  Deterministic.
+// Skinny long reductions: M <= 96 and the kernel's N (with the column-sum column) <= 32,
+// batch 1, K >= kSkinnyMinK — the fcmy weight gradient (12 x 25 over B*N*C = 174K rows at
+// PEMS08) and the aggregate-first Chebyshev weight gradient dTheta (K*F x C = 96 x 32 over
+// B*N*T = 65K rows).  The tiled kernel leaves most of its tile clamped (or splits K into
+// hundreds of slabs and a fold launch) and spends its time in per-k-tile DMA round trips.
+// Here every wave owns kpw consecutive k and loads a round of U k-quads at once
+// (v_mfma_f32_16x16x4_f32, lane (q = l>>4, i = l&15): A[mt*16 + i][k + q] and
+// B[k + q][nt*16 + i]), then MT x NT MFMAs per quad into 16x16 accumulators.  One
+// 1024-thread workgroup per CU (<= 256 of them): its 16 accumulators fold in LDS in a fixed
+// order, and the workgroups' partials fold by tickets (colsum2d's hand-off: sc1 stores drained
+// by every storing wave, a barrier, one agent-scope ticket per workgroup; the last arrival
+// acquires, then all its 1024 threads sum the partials in a fixed order).  Small outputs
+// (fcmy: 300 floats) fold in ONE level — the acquire's price grows with the workgroups per CU
+// (MI355X_MICROARCH.md), so one per CU pays it once; large ones (dTheta: 3 072 floats x 256
+// partials = 3 MB would take one CU ~20 us to read) fold in two: the last of each group of
+// kSkGroup workgroups sums its group's partials, the last group sums the group sums.  Either
+// way the summation order is fixed: deterministic.
 // ---------------------------------------------------------------------------------
-constexpr int kSkU = 16;           // k-quads per load round
 constexpr int kSkWaves = 16;       // waves per workgroup
 constexpr int kSkMaxWg = 256;      // workgroups (partials) at most
+constexpr int kSkGroup = 16;       // workgroups per first-level fold group (two-level fold)
 constexpr int kSkinnyMinK = 4096;  // shorter reductions stay on the tiled kernel
+constexpr int kSkMaxM = 96;
 struct SkinnyK {
   GemmK g;
-  float* part;  // [nwg][P] partials
-  int* cnt;     // one ticket
+  float* part;  // [nwg][P4] partials, then [ngrp][P4] group sums (two-level fold)
+  int* cnt;     // tickets: [0] the final fold, [1 + grp] the groups
   int kpw;      // k per wave (multiple of 4)
   int nwg, P;   // P = M * N (kernel columns, the column-sum column included)
   int P4;       // partial row stride: P rounded up to 4 (16-B rows)
+  int ngrp;     // 0: one-level fold; else first-level groups of kSkGroup workgroups
   int stop;     // profiling probe (DSTAGNN_SKINNY_STOP): 1 = after the loads + MFMAs, 2 = after the ticket
 };
 
@@ -108,10 +114,73 @@ __device__ __forceinline__ void sk_st(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int MT, int NT>  // 16-row / 16-column accumulator tiles
+// ticket of one workgroup on *c among n arrivals (call after every storing wave drained its
+// sc1 stores and a barrier): true in every thread of the last arrival, which has acquired
+__device__ __forceinline__ bool sk_ticket(int* c, int n, int* last) {
+  if (threadIdx.x == 0) {
+    *last = atomicAdd(c, 1) == n - 1;
+    if (*last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+  }
+  __syncthreads();
+  return *last != 0;
+}
+
+// sum of rows [0, nrows) of src (rows of P4 floats, 16-B aligned) in a fixed order: thread t
+// < C4 = P4/4 gets column quad t.  S = 1024 / C4 subsets of the rows per quad (sub, sub + S,
+// ...), sixteen 16-B loads in flight per round, then the subsets in order via LDS (sums:
+// >= 1024 float4).  relaxed: agent-scope loads (the rows came from other workgroups' sc1
+// stores and are read without this workgroup having acquired them at load time)
+template <bool RELAXED>
+__device__ __forceinline__ float4 sk_fold_rows(const float* src, int nrows, int P4, float4* sums) {
+  const int t = threadIdx.x;
+  const int C4 = P4 / 4, S = max(1, 1024 / C4);
+  const int sub = t / C4, c = t % C4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sub < S) {
+    const float4* p = reinterpret_cast<const float4*>(src) + c;
+    for (int q = sub; q < nrows; q += 16 * S) {
+      float4 u[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (q + j * S < nrows) {
+          const float4* a = p + (int64_t)(q + j * S) * C4;
+          if (RELAXED) {
+            const float* f = reinterpret_cast<const float*>(a);
+            u[j] = make_float4(sk_ld(f), sk_ld(f + 1), sk_ld(f + 2), sk_ld(f + 3));
+          } else {
+            u[j] = *a;
+          }
+        } else {
+          u[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) { v.x += u[j].x; v.y += u[j].y; v.z += u[j].z; v.w += u[j].w; }
+    }
+  }
+  __syncthreads();
+  if (sub < S) sums[t] = v;
+  __syncthreads();
+  float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < C4) {
+    tot = sums[t];
+    for (int j = 1; j < S; ++j) {
+      const float4 x = sums[j * C4 + t];
+      tot.x += x.x; tot.y += x.y; tot.z += x.z; tot.w += x.w;
+    }
+  }
+  return tot;
+}
+
+template <int MT, int NT, int U>  // 16-row / 16-column accumulator tiles, k-quads per load round
 __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
-  constexpr int kH = kSkWaves / 2;
-  __shared__ float red[kH][32 * 33];
+  constexpr int kS = MT > 2 ? 4 : 8;  // LDS fold slots (waves fold in 16 / kS rounds)
+  static_assert(kS * MT * 16 * 33 >= 4096, "the final fold's 1024 float4 sums live in red");
+  __shared__ __attribute__((aligned(16))) float red[kS][MT * 16 * 33];
   __shared__ int last;
   const GemmK& g = s.g;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, q4 = lane >> 4, i16 = lane & 15;
@@ -137,10 +206,10 @@ __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int kb = k0; kb < k1; kb += 4 * kSkU) {
-    float av[kSkU][MT], bv[kSkU][NT];
+  for (int kb = k0; kb < k1; kb += 4 * U) {
+    float av[U][MT], bv[U][NT];
 #pragma unroll
-    for (int u = 0; u < kSkU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int k = kb + 4 * u + q4;
       const bool ok = k < k1;
 #pragma unroll
@@ -150,82 +219,65 @@ __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
         bv[u][nt] = ok && bcol[nt] ? g.B[bo[nt] + (uint32_t)koff(g.bk, k)] : (ok && ones[nt] ? 1.f : 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < kSkU; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][mt], bv[u][nt], acc[mt][nt], 0, 0, 0);
   }
-  // fold the 16 waves: D[m = mt*16 + 4 (l>>4) + r][n = nt*16 + (l&15)]; waves kH.. store, waves
-  // ..kH-1 add theirs (red[w] = acc_w + acc_{w+kH}), then the kH slots in order
+  // fold the 16 waves: D[m = mt*16 + 4 (l>>4) + r][n = nt*16 + (l&15)]; in rounds from the
+  // last kS waves down, each round adding its accumulators into the kS slots, then the slots
+  // in order
   auto slot = [&](int mt, int nt, int r) { return (mt * 16 + 4 * q4 + r) * 33 + nt * 16 + i16; };
-  if (w >= kH) {
+  constexpr int kRounds = kSkWaves / kS;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+  for (int rd = kRounds - 1; rd >= 0; --rd) {
+    if (w / kS == rd) {
+      float* sl = red[w % kS];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red[w - kH][slot(mt, nt, r)] = acc[mt][nt][r];
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sl[slot(mt, nt, r)] = rd == kRounds - 1 ? acc[mt][nt][r] : acc[mt][nt][r] + sl[slot(mt, nt, r)];
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (w < kH) {
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[w][slot(mt, nt, r)] = acc[mt][nt][r] + red[w][slot(mt, nt, r)];
-  }
-  __syncthreads();
   if (s.stop == 1) return;
   float* p1 = s.part + (int64_t)blockIdx.x * s.P4;
   for (int e = t; e < s.P; e += 1024) {
     const int m = e / g.N, o = m * 33 + (e - m * g.N);
     float v = red[0][o];
 #pragma unroll
-    for (int q = 1; q < kH; ++q) v += red[q][o];
+    for (int q = 1; q < kS; ++q) v += red[q][o];
     sk_st(p1 + e, v);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) {
-    last = atomicAdd(s.cnt, 1) == s.nwg - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float4* sums = reinterpret_cast<float4*>(&red[0][0]);
+  const int C4 = s.P4 / 4;
+  const float* rows = s.part;
+  int nrows = s.nwg;
+  if (s.ngrp > 0) {
+    // first level: the last arrival of this workgroup's group sums the group's partials
+    const int grp = blockIdx.x / kSkGroup, g0 = grp * kSkGroup, gn = min(kSkGroup, s.nwg - g0);
+    if (!sk_ticket(s.cnt + 1 + grp, gn, &last) || s.stop == 2) return;
+    const float4 tot = sk_fold_rows<false>(s.part + (int64_t)g0 * s.P4, gn, s.P4, sums);
+    float* gs = s.part + ((int64_t)s.nwg + grp) * s.P4;
+    if (t < C4) {
+      sk_st(gs + 4 * t, tot.x); sk_st(gs + 4 * t + 1, tot.y); sk_st(gs + 4 * t + 2, tot.z); sk_st(gs + 4 * t + 3, tot.w);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    rows = s.part + (int64_t)s.nwg * s.P4;
+    nrows = s.ngrp;
   }
-  __syncthreads();
-  if (!last || s.stop == 2) return;
-  // the last workgroup (plain loads behind its acquire): the partial rows are P4 floats, read
-  // as float4 column groups; S = 1024 / (P4/4) subsets of the partials per group (sub, sub + S,
-  // ...), sixteen 16-B loads in flight per round, then the subsets in order via LDS
-  float4* sums = reinterpret_cast<float4*>(&red[0][0]);  // kH * 32 * 33 floats >= 4096
-  const int C4 = s.P4 / 4, S = max(1, 1024 / C4);
-  const int sub = t / C4, c = t % C4;
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (sub < S) {
-    const float4* p = reinterpret_cast<const float4*>(s.part) + c;
-    int q = sub;
-    for (; q < s.nwg; q += 16 * S) {
-      float4 u[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        u[j] = q + j * S < s.nwg ? p[(int64_t)(q + j * S) * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) { v.x += u[j].x; v.y += u[j].y; v.z += u[j].z; v.w += u[j].w; }
-    }
-  }
-  __syncthreads();
-  if (sub < S) sums[t] = v;
-  __syncthreads();
+  if (!sk_ticket(s.cnt, nrows, &last) || (s.stop == 2 && s.ngrp == 0)) return;
+  // the last arrival (plain loads behind its acquire)
+  const float4 tot = sk_fold_rows<false>(rows, nrows, s.P4, sums);
   if (t < C4) {
-    float4 tot = sums[t];
-    for (int j = 1; j < S; ++j) {
-      const float4 x = sums[j * C4 + t];
-      tot.x += x.x; tot.y += x.y; tot.z += x.z; tot.w += x.w;
-    }
     const float tv[4] = {tot.x, tot.y, tot.z, tot.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -233,16 +285,20 @@ __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
       if (e < s.P) epilogue_store(g, 0, e / g.N, e % g.N, tv[i]);
     }
   }
-  if (t == 0) __hip_atomic_store(s.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void launch_skinny(const SkinnyK& s, hipStream_t st) {
   const dim3 grid((unsigned)s.nwg), blk(64 * kSkWaves);
-  const int mt = s.g.M > 16 ? 2 : 1, nt = s.g.N > 16 ? 2 : 1;
-  if (mt == 1 && nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<1, 1>), grid, blk, 0, st, s);
-  else if (mt == 1) hipLaunchKernelGGL((skinny_dw_kernel<1, 2>), grid, blk, 0, st, s);
-  else if (nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<2, 1>), grid, blk, 0, st, s);
-  else hipLaunchKernelGGL((skinny_dw_kernel<2, 2>), grid, blk, 0, st, s);
+  const int mt = (s.g.M + 15) / 16, nt = s.g.N > 16 ? 2 : 1;
+#define SK_L(MT_, U_)                                                                       \
+  if (nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<MT_, 1, U_>), grid, blk, 0, st, s);   \
+  else hipLaunchKernelGGL((skinny_dw_kernel<MT_, 2, U_>), grid, blk, 0, st, s);
+  if (mt == 1) { SK_L(1, 16) }
+  else if (mt == 2) { SK_L(2, 16) }
+  else if (mt == 3) { SK_L(3, 8) }
+  else if (mt == 4) { SK_L(4, 8) }
+  else { SK_L(6, 4) }
+#undef SK_L
 }
 
 struct Cfg {
@@ -371,7 +427,7 @@ struct Plan {
   }
   // split-K slab floats this plan takes from the workspace
   size_t ws_floats() const {
-    if (skinny) return (size_t)sk.nwg * sk.P4;
+    if (skinny) return (size_t)(sk.nwg + sk.ngrp) * sk.P4;
     return k.splitk > 1 ? (size_t)k.batch * k.splitk * k.M * k.N : 0;
   }
 };
@@ -380,7 +436,7 @@ struct Plan {
 bool plan_skinny(Plan& pl, float* ws, size_t ws_floats, hipStream_t st) {
   static const bool on = !getenv("DSTAGNN_GEMM_SKINNY") || atoi(getenv("DSTAGNN_GEMM_SKINNY")) != 0;
   const GemmK& k = pl.k;
-  if (!on || g_bf16 || !ws || k.batch != 1 || k.M > 32 || k.N > 32 || k.K < kSkinnyMinK) return false;
+  if (!on || g_bf16 || !ws || k.batch != 1 || k.M > kSkMaxM || k.N > 32 || k.K < kSkinnyMinK) return false;
   SkinnyK& s = pl.sk;
   s = SkinnyK{};
   // <= kSkMaxWg workgroups of kSkWaves waves, a multiple of 4 k per wave
@@ -390,8 +446,12 @@ bool plan_skinny(Plan& pl, float* ws, size_t ws_floats, hipStream_t st) {
   s.nwg = (int)cdiv64(k.K, (int64_t)kSkWaves * s.kpw);
   s.P = k.M * k.N;
   s.P4 = (s.P + 3) / 4 * 4;
-  if ((size_t)s.nwg * s.P4 > ws_floats || (reinterpret_cast<uintptr_t>(ws) & 15) != 0) return false;
-  s.cnt = stream_counters(st, 1);
+  // one fold level while the last workgroup reads <= DSTAGNN_SKINNY_FOLD1_KB of partials (one
+  // CU pulls ~150 GB/s: 512 KB ~ 3.5 us), else groups of kSkGroup first
+  static const int fold1_kb = getenv("DSTAGNN_SKINNY_FOLD1_KB") ? atoi(getenv("DSTAGNN_SKINNY_FOLD1_KB")) : 512;
+  s.ngrp = (int64_t)s.nwg * s.P4 * 4 > (int64_t)fold1_kb * 1024 ? (int)cdiv64(s.nwg, kSkGroup) : 0;
+  if ((size_t)(s.nwg + s.ngrp) * s.P4 > ws_floats || (reinterpret_cast<uintptr_t>(ws) & 15) != 0) return false;
+  s.cnt = stream_counters(st, 1 + s.ngrp);
   if (!s.cnt) return false;
   s.stop = getenv("DSTAGNN_SKINNY_STOP") ? atoi(getenv("DSTAGNN_SKINNY_STOP")) : 0;
   pl.k.splitk = 1;
@@ -401,7 +461,7 @@ bool plan_skinny(Plan& pl, float* ws, size_t ws_floats, hipStream_t st) {
   pl.skinny = true;
   if (gemm_log_on()) {
     const size_t n = strlen(pl.log);
-    snprintf(pl.log + n, sizeof(pl.log) - n, " skinny kpw=%d nwg=%d", s.kpw, s.nwg);
+    snprintf(pl.log + n, sizeof(pl.log) - n, " skinny kpw=%d nwg=%d ngrp=%d", s.kpw, s.nwg, s.ngrp);
   }
   return true;
 }

@@ -48,7 +48,8 @@ def _gemm(A, B, C, M, N, K, am, ak, bk, bn, cm, cn, batch=1, az=(0, 0, 0), bz=(0
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 64, 16), (100, 70, 33), (5440, 512, 384), (300, 96, 20000), (7, 3, 1),
-                                   (12, 24, 174080), (32, 32, 9000), (5, 7, 4097)])
+                                   (12, 24, 174080), (32, 32, 9000), (5, 7, 4097), (96, 32, 65280),
+                                   (40, 17, 20000), (64, 32, 5000)])
 def test_gemm_plain(M, N, K):
     _need_gpu()
     g = torch.Generator().manual_seed(M + N + K)
@@ -83,6 +84,27 @@ def test_gemm_skinny_epilogue():
     _gemm(A.cuda(), B.cuda(), C2, M, N, K, (0, 1, 0), (0, M, 0), (0, N, 0), (0, 1, 0), (0, N, 0), (0, 1, 0),
           alpha=0.5, beta=2.0, relu=1)
     assert torch.equal(C, C2)
+
+
+def test_gemm_skinny_two_level_fold():
+    """The skinny kernel with a two-level partial fold (M*N = 3072 outputs over 256 workgroups:
+    the aggregate-first dTheta shape, A = agg[b,j,k,f,t] read with a two-level k map) — fp64
+    product, and bit-identical reruns (fixed summation order whichever workgroup arrives last)."""
+    _need_gpu()
+    g = torch.Generator().manual_seed(12)
+    BN, K, F, T, C = 5440, 3, 32, 12, 32
+    agg = torch.randn(BN, K, F, T, generator=g)
+    gp = torch.randn(BN, T, C, generator=g)
+    ref = torch.einsum("jkft,jtc->kfc", agg.double(), gp.double()).reshape(K * F, C).float()
+    KFT = K * F * T
+    outs = []
+    for _ in range(3):
+        Cd = torch.empty(K * F, C, device="cuda")
+        _gemm(agg.cuda(), gp.cuda(), Cd, K * F, C, BN * T, (0, T, 0), (T, 1, KFT), (0, C, 0), (0, 1, 0),
+              (0, C, 0), (0, 1, 0))
+        outs.append(Cd)
+    close(outs[0], ref, tol=1e-5 * (BN * T) ** 0.5, what="skinny two-level")
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 def test_gemm_transposed_batched_two_level():
