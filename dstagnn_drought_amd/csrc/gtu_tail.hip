@@ -494,6 +494,305 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Compile-time C / T fused tail (the C = 32, T = 12 blocks of PEMS04/07/08): the arithmetic of
+// gtu_tail_{fwd,bwd}_kernel<C, T, true, 0, NT> element for element (bit-identical outputs),
+// restructured for latency.  The per-node kernels above walk a node in phases that each
+// start with their own global loads (fwd: conv rows, then X, then x; bwd: dout / r / mu / rs,
+// dout again for the LN partials, tco, then the conv rows of each GTU), and a node's lifetime
+// is ~5 dependent memory round trips (46 us for the PEMS08 backward at ~7 resident nodes per
+// CU).  Here every global load of a node — activations, conv rows of all three GTUs (one
+// thread per (row, channel) pair: its P and Q values feed both output halves), the small
+// parameter vectors — is issued in ONE round at the node's start, into registers; everything
+// after that reads LDS and registers only and ends in stores.
+// ---------------------------------------------------------------------------------------
+template <int C, int T, int NT, int W>  // W: occupancy floor for the register allocator (waves / SIMD)
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void gtu_tail_fwd_ct_kernel(GtuTailArgs a) {
+  constexpr int S = 3 * T - 12, CT = C * T, C2 = 2 * C, CS = C * S, SP = S + 1, CP = C + 1;
+  constexpr int P = T < NT ? NT / T : 1, NRED = P * T > NT ? P * T : NT;
+  constexpr int NG = (CS + NT - 1) / NT, NE = (CT + NT - 1) / NT;
+  __shared__ float Gs[C * SP], rl[CT], Xs[T * CP], red[NRED], mus[T], rss[T], Wl[T * SP];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < T * S; e += NT) Wl[(e / S) * SP + e % S] = a.fcmy_w[e];
+  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
+    const int64_t base = bn * CT;
+    // every load of the node, one round
+    float pv[NG], qv[NG], Xv[NE], xv[NE], fb[NE], rw[NE], rb[NE], lg[NE], lb[NE];
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+      const int e = min(tid + NT * u, CS - 1);
+      const int sidx = e / C, c = e - sidx * C;
+      int gi, t;
+      gate_index(sidx, T, &gi, &t);
+      const int Tg = T - 2 - 2 * gi;
+      const float* cg = gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2]);
+      const float* cv = cg + (bn * Tg + t) * C2;
+      pv[u] = cv[c];
+      qv[u] = cv[C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = min(tid + NT * u, CT - 1);
+      const int c = e / T, t = e - c * T;
+      Xv[u] = a.first ? 0.f : a.X[base + e];  // (t, c) order, staged below
+      xv[u] = a.first ? a.x[bn * T + t] : a.x[base + e];
+      fb[u] = a.fcmy_b[t];
+      rw[u] = a.first ? a.res_w[c] : 0.f;
+      rb[u] = a.first ? a.res_b[c] : 0.f;
+      lg[u] = a.ln_g[c];
+      lb[u] = a.ln_b[c];
+    }
+    // gates, element (s, c) with c fastest
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+      const int e = tid + NT * u;
+      if (e < CS) {
+        const int sidx = e / C, c = e - sidx * C;
+        Gs[c * SP + sidx] = fast_tanh(pv[u]) * fast_sigmoid(qv[u]);
+      }
+    }
+    if (!a.first) {
+#pragma unroll
+      for (int u = 0; u < NE; ++u) {
+        const int e = tid + NT * u;
+        if (e < CT) Xs[(e / C) * CP + e % C] = Xv[u];  // X rows (t, c)
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < CS; e += NT) a.G[bn * CS + e] = Gs[(e / S) * SP + e % S];  // [c][s], coalesced
+    // fcmy + dropout + residual + ReLUs; element e = (c, t) of the (C, T) output
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + NT * u;
+      if (e >= CT) continue;
+      const int c = e / T, t = e - c * T;
+      float tc = fb[u];
+      const float* gr = Gs + c * SP;
+      const float* wr = Wl + t * SP;
+      for (int sidx = 0; sidx < S; ++sidx) tc = fmaf(gr[sidx], wr[sidx], tc);
+      if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+      float tco, xres;
+      if (a.first) {
+        tco = fmaxf(tc, 0.f);
+        xres = rw[u] * xv[u] + rb[u];
+      } else {
+        tco = fmaxf(Xs[t * CP + c] + tc, 0.f);
+        xres = xv[u];
+      }
+      const float r = fmaxf(xres + tco, 0.f);
+      a.tco[base + e] = tco;
+      a.r[base + e] = r;
+      rl[e] = r;
+    }
+    __syncthreads();
+    // LayerNorm over C: mean, then the centred second moment (two fixed-order passes)
+    col_sums_over_c<NT>(rl, C, T, P, red, mus, tid);
+    for (int t = tid; t < T; t += NT) mus[t] *= 1.f / C;
+    __syncthreads();
+    for (int l = tid; l < P * T; l += NT) {
+      const int t = l % T, part = l / T;
+      const float mean = mus[t];
+      float acc = 0.f;
+      for (int c = part; c < C; c += P) { const float d = rl[c * T + t] - mean; acc += d * d; }
+      red[l] = acc;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += NT) {
+      float var = 0.f;
+      for (int q = 0; q < P; ++q) var += red[q * T + t];
+      const float rs = rsqrtf(var * (1.f / C) + 1e-5f);
+      rss[t] = rs;
+      a.mu[bn * T + t] = mus[t];
+      a.rs[bn * T + t] = rs;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + NT * u;
+      if (e >= CT) continue;
+      const int t = e % T;
+      a.out[base + e] = (rl[e] - mus[t]) * rss[t] * lg[u] + lb[u];
+    }
+    __syncthreads();  // LDS reuse by the next node
+  }
+}
+
+// the conv rows of GTU gi (kernel width ks) this thread's gate items need: item i = (tp, c)
+// of the node's zero-padded output rows, tp < T (+ ks - 1 trailing rows on the last node);
+// clamped addresses (always inside the node's rows), zeroed where the item is not a gate row
+template <int C, int T, int NT, int NQ>
+__device__ __forceinline__ void tail_gate_loads(const float* conv, int ks, int64_t bn, float (&p)[NQ], float (&q)[NQ]) {
+  constexpr int C2 = 2 * C;
+  const int Tg = T - ks + 1;
+  const float* cv = conv + bn * C2 * Tg;
+#pragma unroll
+  for (int u = 0; u < NQ; ++u) {
+    const int i = threadIdx.x + NT * u, tp = i / C, c = i - tp * C;
+    const int t = min(max(tp - (ks - 1), 0), Tg - 1);
+    p[u] = cv[t * C2 + c];
+    q[u] = cv[t * C2 + C + c];
+  }
+}
+// the gates' backward into the node's zero-padded rows: both halves (o = c: tanh side,
+// o = C + c: sigmoid side) of item (tp, c) from the preloaded P / Q values
+template <int C, int T, int NT, int NQ>
+__device__ __forceinline__ void tail_gate_bwd(float* dconv, int ks, int off, int64_t bn, bool last, const float* dGs,
+                                              int SP, const float (&p)[NQ], const float (&q)[NQ]) {
+  constexpr int C2 = 2 * C;
+  const int Tg = T - ks + 1, items = (T + (last ? ks - 1 : 0)) * C;
+  float* orow = dconv + bn * C2 * T;
+#pragma unroll
+  for (int u = 0; u < NQ; ++u) {
+    const int i = threadIdx.x + NT * u;
+    if (i >= items) continue;
+    const int tp = i / C, c = i - tp * C, t = tp - (ks - 1);
+    float v0 = 0.f, v1 = 0.f;
+    if (t >= 0 && t < Tg) {
+      const float dg = dGs[c * SP + off + t];
+      const float th = fast_tanh(p[u]), sg = fast_sigmoid(q[u]);
+      v0 = dg * (1.f - th * th) * sg;
+      v1 = dg * th * sg * (1.f - sg);
+    }
+    orow[tp * C2 + c] = v0;
+    orow[tp * C2 + C + c] = v1;
+  }
+}
+
+template <int C, int T, int NT, int W>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void gtu_tail_bwd_ct_kernel(GtuTailArgs a) {
+  constexpr int S = 3 * T - 12, CT = C * T, SP = S + 1, CP = C + 1;
+  constexpr int P = T < NT ? NT / T : 1, NRED2 = 2 * (P * T > NT ? P * T : NT);
+  constexpr int SH0 = C * SP > T * CP ? C * SP : T * CP, SH = SH0 > NRED2 ? SH0 : NRED2;
+  constexpr int NE = (CT + NT - 1) / NT;
+  constexpr int NQ3 = ((T + 2) * C + NT - 1) / NT, NQ5 = ((T + 4) * C + NT - 1) / NT, NQ7 = ((T + 6) * C + NT - 1) / NT;
+  __shared__ float dxh[CT], xhl[CT], rr[CT], dys[CT], sh[SH], s1s[T], s2s[T], Wl[T * S];
+  float* dGs = sh;  // [c][SP]
+  float* dXs = sh;  // [t][CP] (dX tile, written to HBM coalesced)
+  float* red = sh;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < T * S; e += NT) Wl[e] = a.fcmy_w[e];
+  for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
+    const int64_t base = bn * CT;
+    const bool last = bn == a.BN - 1;
+    // every load of the node, one round
+    float dyv[NE], rv[NE], muv[NE], rsw[NE], tcov[NE], xv[NE], lg[NE];
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = min(tid + NT * u, CT - 1);
+      const int c = e / T, t = e - c * T;
+      dyv[u] = a.dout[base + e];
+      rv[u] = a.r[base + e];
+      muv[u] = a.mu[bn * T + t];
+      rsw[u] = a.rs[bn * T + t];
+      tcov[u] = a.tco[base + e];
+      xv[u] = a.first ? a.x[bn * T + t] : 0.f;
+      lg[u] = a.ln_g[c];
+    }
+    float p3[NQ3], q3[NQ3], p5[NQ5], q5[NQ5], p7[NQ7], q7[NQ7];
+    tail_gate_loads<C, T, NT, NQ3>(a.conv[0], 3, bn, p3, q3);
+    tail_gate_loads<C, T, NT, NQ5>(a.conv[1], 5, bn, p5, q5);
+    tail_gate_loads<C, T, NT, NQ7>(a.conv[2], 7, bn, p7, q7);
+    // LayerNorm over C backward
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + NT * u;
+      if (e >= CT) continue;
+      const float xh = (rv[u] - muv[u]) * rsw[u];
+      xhl[e] = xh;
+      rr[e] = rv[u];
+      dxh[e] = dyv[u] * lg[u];
+      dys[e] = dyv[u];
+      if (!a.gpart) a.gcontrib[base + e] = dyv[u] * xh;
+    }
+    __syncthreads();
+    if (a.gpart) {  // LN gamma / beta: sum_t dout * xhat and sum_t dout per channel of this node
+      for (int c = tid; c < C; c += NT) {
+        float g = 0.f, b = 0.f;
+        for (int t = 0; t < T; ++t) {
+          const float dy = dys[c * T + t];
+          g = fmaf(dy, xhl[c * T + t], g);
+          b += dy;
+        }
+        a.gpart[bn * C + c] = g;
+        a.bpart[bn * C + c] = b;
+      }
+    }
+    for (int l = tid; l < P * T; l += NT) {  // sum_c dxhat and dxhat*xhat per t, P lane groups
+      const int t = l % T, part = l / T;
+      float s1 = 0.f, s2 = 0.f;
+      for (int c = part; c < C; c += P) { s1 += dxh[c * T + t]; s2 += dxh[c * T + t] * xhl[c * T + t]; }
+      red[l] = s1;
+      red[P * T + l] = s2;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += NT) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int q = 0; q < P; ++q) { s1 += red[q * T + t]; s2 += red[P * T + q * T + t]; }
+      s1s[t] = s1 * (1.f / C); s2s[t] = s2 * (1.f / C);
+    }
+    __syncthreads();
+    // ReLUs, residual, dropout: dtc (kept in LDS, dxh reused) and the direct grads
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + NT * u;
+      if (e >= CT) continue;
+      const int c = e / T, t = e - c * T;
+      float dr = rsw[u] * (dxh[e] - s1s[t] - xhl[e] * s2s[t]);
+      dr = rr[e] > 0.f ? dr : 0.f;                 // relu(xres + tco)
+      const float dtco = tcov[u] > 0.f ? dr : 0.f;  // tco = relu(...)
+      float dtc = dtco;
+      if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+      a.dtc[base + e] = dtc;
+      if (a.first) {
+        dXs[t * CP + c] = 0.f;
+        if (!a.rpart) {
+          a.rcontrib[base + e] = dr * xv[u];
+          a.dres[base + e] = dr;
+        }
+        xhl[e] = dr;  // for the residual_conv channel reduction below (and its partial sums)
+      } else {
+        dXs[t * CP + c] = dtco;  // dX rows are (t, c), like X
+        a.dx[base + e] = dr;
+      }
+      dxh[e] = dtc;
+    }
+    __syncthreads();
+    for (int e = tid; e < CT; e += NT) a.dX[base + e] = dXs[(e / C) * CP + e % C];  // coalesced
+    __syncthreads();  // dXs shares its LDS with dGs
+    if (a.first) {
+      for (int t = tid; t < T; t += NT) {
+        float sum = 0.f;
+        for (int c = 0; c < C; ++c) sum += a.res_w[c] * xhl[c * T + t];
+        a.dx[bn * T + t] = sum;
+      }
+      if (a.rpart) {  // residual_conv weight / bias: sum_t dr * x and sum_t dr per channel
+        for (int c = tid; c < C; c += NT) {
+          float rw = 0.f, rb = 0.f;
+          for (int t = 0; t < T; ++t) {
+            rw = fmaf(xhl[c * T + t], a.x[bn * T + t], rw);
+            rb += xhl[c * T + t];
+          }
+          a.rpart[bn * C + c] = rw;
+          a.dpart[bn * C + c] = rb;
+        }
+      }
+    }
+    // fcmy backward: dG[c, s] = sum_t dtc[c, t] W[t, s]
+    for (int e = tid; e < C * S; e += NT) {
+      const int c = e / S, s = e - c * S;
+      float g = 0.f;
+      for (int t = 0; t < T; ++t) g = fmaf(dxh[c * T + t], Wl[t * S + s], g);
+      dGs[c * SP + s] = g;
+    }
+    __syncthreads();
+    // gates backward into the zero-padded (t', o) rows of each GTU (layout: gtu_tail_bwd_kernel)
+    tail_gate_bwd<C, T, NT, NQ3>(a.dconv_pad[0], 3, 0, bn, last, dGs, SP, p3, q3);
+    tail_gate_bwd<C, T, NT, NQ5>(a.dconv_pad[1], 5, T - 2, bn, last, dGs, SP, p5, q5);
+    tail_gate_bwd<C, T, NT, NQ7>(a.dconv_pad[2], 7, 2 * T - 6, bn, last, dGs, SP, p7, q7);
+    __syncthreads();  // LDS reuse by the next node
+  }
+}
+
 size_t fwd_lds(const GtuTailArgs& a, bool wl, bool has_g = true, int nt = kNT) {
   return sizeof(float) * (size_t)TailFwdLds(a.C, a.T, wl, has_g, nt).total;
 }
@@ -563,6 +862,13 @@ int fused_nt() {
   return nt;
 }
 
+// the one-round-of-loads C = 32 / T = 12 kernels (DSTAGNN_TAIL_CT=0: the phase-by-phase ones;
+// 2: register cap for 5 waves / SIMD)
+int tail_ct() {
+  static const int v = getenv("DSTAGNN_TAIL_CT") ? atoi(getenv("DSTAGNN_TAIL_CT")) : 1;
+  return v;
+}
+
 bool gtu_tail_bwd_split(int C, int T) {
   GtuTailArgs a;
   a.C = C; a.T = T;
@@ -587,6 +893,12 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
     return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2, 256>, fwd_lds(a, false, false, 256), a, st, 256);
   }
   const size_t lds = fwd_lds(a, true);
+  if (a.C == 32 && a.T == 12 && tail_ct()) {
+    if (tail_ct() == 2) hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 5>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 1>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   if (a.C == 32 && a.T == 12) {
     switch (fused_nt()) {
       case 128: return launch_node_kernel(gtu_tail_fwd_kernel<32, 12, true, 0, 128>, fwd_lds(a, true, true, 128), a, st, 128);
@@ -617,6 +929,12 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
     return 0;
   }
   const size_t lds = bwd_lds(a, true);
+  if (a.C == 32 && a.T == 12 && !generic && tail_ct()) {
+    if (tail_ct() == 2) hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 5>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 1>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   if (a.C == 32 && a.T == 12 && !generic) {
     switch (fused_nt()) {
       case 128: return launch_node_kernel(gtu_tail_bwd_kernel<32, 12, true, 0, 128>, bwd_lds(a, true, true, 128), a, st, 128);
