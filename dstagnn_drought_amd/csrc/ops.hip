@@ -512,44 +512,78 @@ __global__ __launch_bounds__(256) void tat_bwd_cols_kernel(TatArgs a) {
 
 // =====================================================================================
 // LayerNorm over rows of length L; one wave per row, values kept in registers.
+// Every global load of a row (all sources, gamma / beta) is issued in one round, branch-free
+// (out-of-row lanes load the row's last element and are masked after): a per-element
+// `if (e < L)` around a load, or a runtime loop over the sources, made the compiler wait
+// vmcnt(0) after every load — 16 dependent round trips per row for the EmbedS LN (L = 512, two
+// sources), ~1.3 TB/s.
 // =====================================================================================
-template <int VPT>
+template <int VPT, int NSRC>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd a) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.R) return;
-  float v[VPT];
-  int64_t o[3];
-  for (int s = 0; s < a.nsrc; ++s) o[s] = ioff(a.src[s].row, row);
-  float sum = 0.f;
+  const int L = a.L;
+  const float* sp[NSRC];
+  int64_t o[NSRC], es[NSRC];
 #pragma unroll
-  for (int q = 0; q < VPT; ++q) {
-    int e = lane + 64 * q;
-    float u = 0.f;
-    if (e < a.L) {
-      for (int s = 0; s < a.nsrc; ++s) u += a.src[s].p[o[s] + (int64_t)e * a.src[s].es];
-    }
-    v[q] = u;
-    sum += u;
+  for (int s = 0; s < NSRC; ++s) {
+    sp[s] = a.src[s].p;
+    o[s] = ioff(a.src[s].row, row);
+    es[s] = a.src[s].es;
   }
-  const float mean = wave_sum(sum) / a.L;
+  // long rows (VPT > 16: GAMBIA's N = 2139) keep one value per element in registers and read
+  // gamma / beta at the store (register budget); short ones preload everything
+  constexpr bool PRE = VPT <= 16;
+  float v[VPT], gv[PRE ? VPT : 1], bv[PRE ? VPT : 1];
+  float sum = 0.f;
+  if constexpr (PRE) {
+    float xs[NSRC][VPT];
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int e = min(lane + 64 * q, L - 1);
+#pragma unroll
+      for (int s = 0; s < NSRC; ++s) xs[s][q] = sp[s][o[s] + (int64_t)e * es[s]];
+      gv[q] = a.g[e];
+      bv[q] = a.b[e];
+    }
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      float u = 0.f;
+#pragma unroll
+      for (int s = 0; s < NSRC; ++s) u += xs[s][q];
+      v[q] = lane + 64 * q < L ? u : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int e = min(lane + 64 * q, L - 1);
+      float u = 0.f;
+#pragma unroll
+      for (int s = 0; s < NSRC; ++s) u += sp[s][o[s] + (int64_t)e * es[s]];
+      v[q] = lane + 64 * q < L ? u : 0.f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) sum += v[q];
+  const float mean = wave_sum(sum) / L;
   float var = 0.f;
 #pragma unroll
   for (int q = 0; q < VPT; ++q) {
     int e = lane + 64 * q;
-    if (e < a.L) { float d = v[q] - mean; var += d * d; }
+    if (e < L) { float d = v[q] - mean; var += d * d; }
   }
-  var = wave_sum(var) / a.L;
+  var = wave_sum(var) / L;
   const float rs = rsqrtf(var + a.eps);
   if (lane == 0) { a.mu[row] = mean; a.rs[row] = rs; }
   const int64_t yo = ioff(a.yrow, row);
 #pragma unroll
   for (int q = 0; q < VPT; ++q) {
     int e = lane + 64 * q;
-    if (e < a.L) {
-      if (a.u) a.u[(int64_t)row * a.L + e] = v[q];
-      float y = (v[q] - mean) * rs * a.g[e] + a.b[e];
-      if (a.drop_p > 0.f) y *= drop_scale(a.seed, a.which, (uint64_t)row * a.L + e, a.drop_p);
+    if (e < L) {
+      if (a.u) a.u[(int64_t)row * L + e] = v[q];
+      float y = (v[q] - mean) * rs * (PRE ? gv[PRE ? q : 0] : a.g[e]) + (PRE ? bv[PRE ? q : 0] : a.b[e]);
+      if (a.drop_p > 0.f) y *= drop_scale(a.seed, a.which, (uint64_t)row * L + e, a.drop_p);
       a.y[yo + (int64_t)e * a.yes] = y;
     }
   }
@@ -559,51 +593,65 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd a) {
 // tensors: a wave takes kLnRowsPerWave consecutive rows, keeps the sums over them in
 // registers, and the 4 waves combine through LDS into one row of the (blocks, L) slabs
 // gpart / bpart (reduced over blocks by a column sum afterwards).  Cuts the (R, L) contribution
-// write and its re-read.
+// write and its re-read.  Loads: one branch-free round per row, as ln_fwd_kernel.
 template <int VPT, bool PART>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   constexpr int RPW = PART ? kLnRowsPerWave : 1;
+  const int L = a.L;
   float gp[VPT], bp[VPT];
 #pragma unroll
   for (int q = 0; q < VPT; ++q) { gp[q] = 0.f; bp[q] = 0.f; }
   for (int i = 0; i < RPW; ++i) {
     const int row = (blockIdx.x * 4 + wv) * RPW + i;
     if (row >= a.R) break;  // wave-uniform
-    const float mean = a.mu[row], rs = a.rs[row];
     const int64_t yo = ioff(a.dyrow, row);
+    constexpr bool PRE = VPT <= 16;  // long rows: gamma read at its use (register budget)
+    float dyl[VPT], ul[VPT], gl[PRE ? VPT : 1], xin[VPT];
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int e = min(lane + 64 * q, L - 1);
+      dyl[q] = a.dy[yo + (int64_t)e * a.dyes];
+      ul[q] = a.u[(int64_t)row * L + e];
+      if constexpr (PRE) gl[q] = a.g[e];
+    }
+    const int64_t xo = ioff(a.dxrow, row);
+    if (a.beta != 0.f) {
+#pragma unroll
+      for (int q = 0; q < VPT; ++q) xin[q] = a.dx[xo + (int64_t)min(lane + 64 * q, L - 1) * a.dxes];
+    }
+    const float mean = a.mu[row], rs = a.rs[row];
     float dyv[VPT], xh[VPT];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
       int e = lane + 64 * q;
       dyv[q] = 0.f; xh[q] = 0.f;
-      if (e < a.L) {
-        float dy = a.dy[yo + (int64_t)e * a.dyes];
-        if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * a.L + e, a.drop_p);
-        float x = (a.u[(int64_t)row * a.L + e] - mean) * rs;
+      if (e < L) {
+        float dy = dyl[q];
+        if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * L + e, a.drop_p);
+        float x = (ul[q] - mean) * rs;
         dyv[q] = dy; xh[q] = x;
-        float dxh = dy * a.g[e];
+        float dxh = dy * (PRE ? gl[PRE ? q : 0] : a.g[e]);
         s1 += dxh; s2 += dxh * x;
         if (PART) {
           gp[q] += dy * x;
           bp[q] += dy;
         } else {
-          if (a.gcontrib) a.gcontrib[(int64_t)row * a.L + e] = dy * x;
-          if (a.bcontrib) a.bcontrib[(int64_t)row * a.L + e] = dy;
+          if (a.gcontrib) a.gcontrib[(int64_t)row * L + e] = dy * x;
+          if (a.bcontrib) a.bcontrib[(int64_t)row * L + e] = dy;
         }
       }
     }
-    s1 = wave_sum(s1) / a.L;
-    s2 = wave_sum(s2) / a.L;
-    const int64_t xo = ioff(a.dxrow, row);
+    s1 = wave_sum(s1) / L;
+    s2 = wave_sum(s2) / L;
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
       int e = lane + 64 * q;
-      if (e < a.L) {
-        float dx = rs * (dyv[q] * a.g[e] - s1 - xh[q] * s2);
+      if (e < L) {
+        float dx = rs * (dyv[q] * (PRE ? gl[PRE ? q : 0] : a.g[e]) - s1 - xh[q] * s2);
         int64_t oo = xo + (int64_t)e * a.dxes;
-        if (a.beta != 0.f) dx += a.beta * a.dx[oo];
+        if (a.beta != 0.f) dx += a.beta * xin[q];
         a.dx[oo] = dx;
       }
     }
@@ -616,11 +664,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
       red[1][wv][lane + 64 * q] = bp[q];
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < a.L; e += 256) {
+    for (int e = threadIdx.x; e < L; e += 256) {
       const float g = red[0][0][e] + red[0][1][e] + red[0][2][e] + red[0][3][e];
       const float b = red[1][0][e] + red[1][1][e] + red[1][2][e] + red[1][3][e];
-      if (a.gpart) a.gpart[(int64_t)blockIdx.x * a.L + e] = g;
-      if (a.bpart) a.bpart[(int64_t)blockIdx.x * a.L + e] = b;
+      if (a.gpart) a.gpart[(int64_t)blockIdx.x * L + e] = g;
+      if (a.bpart) a.bpart[(int64_t)blockIdx.x * L + e] = b;
     }
   }
 }
@@ -1275,15 +1323,23 @@ int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
   return 0;
 }
 
+template <int VPT>
+static void launch_ln_fwd(const LnFwd& a, dim3 grid, hipStream_t st) {
+  if (a.nsrc == 1) hipLaunchKernelGGL((ln_fwd_kernel<VPT, 1>), grid, dim3(256), 0, st, a);
+  else if (a.nsrc == 2) hipLaunchKernelGGL((ln_fwd_kernel<VPT, 2>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((ln_fwd_kernel<VPT, 3>), grid, dim3(256), 0, st, a);
+}
+
 int op_ln_fwd(const LnFwd& a, hipStream_t st) {
+  if (a.nsrc < 1 || a.nsrc > 3 || a.L < 1) { set_last_error("ln_fwd: 1..3 sources, L >= 1"); return DSTAGNN_E_ARG; }
   dim3 grid((unsigned)cdiv64(a.R, 4));
   int vpt = (int)cdiv64(a.L, 64);
-  if (vpt <= 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 4) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 8) hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 16) hipLaunchKernelGGL(ln_fwd_kernel<16>, grid, dim3(256), 0, st, a);
-  else if (vpt <= 64) hipLaunchKernelGGL(ln_fwd_kernel<64>, grid, dim3(256), 0, st, a);
+  if (vpt <= 1) launch_ln_fwd<1>(a, grid, st);
+  else if (vpt <= 2) launch_ln_fwd<2>(a, grid, st);
+  else if (vpt <= 4) launch_ln_fwd<4>(a, grid, st);
+  else if (vpt <= 8) launch_ln_fwd<8>(a, grid, st);
+  else if (vpt <= 16) launch_ln_fwd<16>(a, grid, st);
+  else if (vpt <= 64) launch_ln_fwd<64>(a, grid, st);
   else { set_last_error("ln_fwd: row too long"); return DSTAGNN_E_SHAPE; }
   DS_CHECK_LAUNCH();
   return 0;
