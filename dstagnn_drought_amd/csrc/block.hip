@@ -616,7 +616,9 @@ struct Fwd {
       a.src[1].p = s.E; a.src[1].row = idx1(N);
       a.nsrc = 2;
       a.g = p.tat_ln_g; a.b = p.tat_ln_b;
-      a.y = s.O; a.yrow = idx1(N);
+      // O in [(f,t)][(b,n)] order: the pre_conv products read it with single-level unit-stride
+      // maps (16-B DMA; no two-level k map in the weight gradient), row r = (b, ft) of the LN
+      a.y = s.O; a.yrow = idx2(m.FT, m.BN, N);
       a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat;
       DS_TRY(op_ln_fwd(a, st));
     }
@@ -626,7 +628,7 @@ struct Fwd {
   Gemm preconv_gemm() {
     Gemm g;  // u_s[(b,n), d] = bias[d] + sum_{(f,t)} O[b,f,t,n] Wp[d,(f,t)]
     g.M = (int)m.BN; g.N = m.D; g.K = (int)m.FT;
-    g.A = s.O; g.am = idx2(m.N, 1, m.FT * m.N); g.ak = idx1(m.N);
+    g.A = s.O; g.am = idx1(1); g.ak = idx1(m.BN);
     g.B = s.Wp; g.bk = idx1(1); g.bn = idx1(m.FT);
     g.C = s.u_s; g.cm = idx1(m.D); g.cn = idx1(1);
     g.bias = p.pre_conv_b;
@@ -1110,7 +1112,7 @@ struct Bwd {
       Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
       g.M = m.D; g.N = (int)m.FT; g.K = (int)m.BN;
       g.A = w.dY; g.am = idx1(1); g.ak = idx1(m.D);
-      g.B = s.O; g.bk = idx2(m.N, 1, m.FT * m.N); g.bn = idx1(m.N);
+      g.B = s.O; g.bk = idx1(1); g.bn = idx1(m.BN);
       // written straight into pre_conv.weight's [d][t][0][f] layout: n = f*T + t
       g.C = gd.pre_conv_w; g.cm = idx1(m.FT); g.cn = idx2(m.T, m.F, 1);
       DS_TRY(sgemm(g));
@@ -1123,7 +1125,7 @@ struct Bwd {
     g.M = (int)m.FT; g.N = (int)m.BN; g.K = m.D;
     g.A = s.Wp; g.am = idx1(1); g.ak = idx1(m.FT);
     g.B = w.dY; g.bk = idx1(1); g.bn = idx1(m.D);
-    g.C = w.dO; g.cm = idx1(m.N); g.cn = idx2(m.N, 1, m.FT * m.N);
+    g.C = w.dO; g.cm = idx1(m.BN); g.cn = idx1(1);  // dO in O's [(f,t)][(b,n)] order
     return gemm(g);
   }
 
@@ -1132,7 +1134,7 @@ struct Bwd {
     {  // LN_N backward (:100); dU = d(fc + E)
       LnBwd a;
       a.R = (int)m.BFT; a.L = m.N;
-      a.dy = w.dO; a.dyrow = idx1(N);
+      a.dy = w.dO; a.dyrow = idx2(m.FT, m.BN, N);
       a.u = s.u_tat; a.mu = s.mu_tat; a.rs = s.rs_tat; a.g = p.tat_ln_g;
       a.dx = w.dU; a.dxrow = idx1(N);
       if (tat_part()) {  // both slabs in gcon_a ((BFT, N) holds 2 slabs)
