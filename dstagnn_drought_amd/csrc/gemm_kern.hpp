@@ -165,63 +165,77 @@ __device__ __forceinline__ TileCoord decode_tile(const GemmK& g, uint32_t bid, u
 }
 
 // --- epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+// Row offsets: a single-level row map (d = 2^31, the common case) gives row r's offset as the
+// lane's base row offset plus a compile-time multiple of the uniform stride (one scalar
+// multiply, one add), instead of a full koff (three 32-bit vector multiplies and a high
+// multiply) per row; split-K slab offsets likewise from one 64-bit base per accumulator.
+__device__ __forceinline__ int rrow(int r) { return (r & 3) + 8 * (r >> 2); }
 template <int WM, int WN>
 __device__ __forceinline__ void gemm_epilogue(const GemmK& g, const TileCoord& c, int wrow0, int wcol0, int lane,
                                               floatx16 (&acc)[WM][WN]) {
   const int lr = lane & 31, lk = lane >> 5;
   const bool reads = g.splitk == 1 && (g.beta != 0.f || g.emask);
+  const bool cm1 = g.cm.d == 0x80000000u;  // single-level row map (uniform)
+  const int64_t zo = zoff(g.cz, c.zb);
 #pragma unroll
   for (int i = 0; i < WM; ++i)
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
       const int n = c.n0 + wcol0 + j * 32 + lr;
       if (n >= g.N) continue;
+      const int mb = c.m0 + wrow0 + i * 32 + 4 * lk;  // row of r = 0
       if (n == g.nload) {  // column-sum column
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          const int m = mb + rrow(r);
           if (m >= g.M) continue;
           if (g.splitk > 1) g.ws[(((int64_t)c.zb * g.splitk + c.sp) * g.M + m) * g.N + n] = acc[i][j][r];
           else epilogue_store(g, c.zb, m, n, acc[i][j][r]);
         }
         continue;
       }
+      if (g.splitk > 1) {
+        float* wsp = g.ws + (((int64_t)c.zb * g.splitk + c.sp) * g.M + mb) * g.N + n;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (mb + rrow(r) < g.M) wsp[(int64_t)rrow(r) * g.N] = acc[i][j][r];
+        continue;
+      }
+      const int32_t no = koff(g.cn, n);
+      const int32_t mob = cm1 ? mb * g.cm.s0 : 0;
+      auto mo = [&](int r) -> int32_t { return cm1 ? mob + rrow(r) * g.cm.s0 : koff(g.cm, mb + rrow(r)); };
+      float* dst = g.Cout ? g.Cout : g.C;
       if (reads) {
         // beta * C and the ReLU mask: all 16 loads issued before the first store (the
         // stores may alias C, so element-wise load/store pairs would serialise 16 memory
         // round trips per lane)
-        const int64_t zo = zoff(g.cz, c.zb);
-        const int32_t no = koff(g.cn, n);
         float cin[16], em[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = min(c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk, g.M - 1);
-          const int64_t o = zo + koff(g.cm, m) + no;
+          const int m = min(mb + rrow(r), g.M - 1);
+          const int64_t o = zo + (cm1 ? mob + (m - mb) * g.cm.s0 : koff(g.cm, m)) + no;
           cin[r] = g.beta != 0.f ? g.C[o] : 0.f;
           em[r] = g.emask ? g.emask[o] : 1.f;
         }
-        float* dst = g.Cout ? g.Cout : g.C;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          if (m >= g.M) continue;
+          if (mb + rrow(r) >= g.M) continue;
           float v = acc[i][j][r] * g.alpha + g.beta * cin[r];
           if (g.bias) v += g.bias[n * g.bias_stride];
           if (g.relu) v = fmaxf(v, 0.f);
           if (em[r] <= 0.f) v = 0.f;
-          dst[zo + koff(g.cm, m) + no] = v;
+          dst[zo + mo(r) + no] = v;
         }
         continue;
       }
+      const float bv = g.bias ? g.bias[n * g.bias_stride] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = c.m0 + wrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (m >= g.M) continue;
-        if (g.splitk > 1) {
-          g.ws[(((int64_t)c.zb * g.splitk + c.sp) * g.M + m) * g.N + n] = acc[i][j][r];
-        } else {
-          epilogue_store(g, c.zb, m, n, acc[i][j][r]);
-        }
+        if (mb + rrow(r) >= g.M) continue;
+        float v = acc[i][j][r] * g.alpha;
+        if (g.bias) v += bv;
+        if (g.relu) v = fmaxf(v, 0.f);
+        dst[zo + mo(r) + no] = v;
       }
     }
 }
@@ -439,7 +453,11 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
     } else {  // partial tile: element by element, zeros past kend
       // (from the loop-invariant start of the last tile, not k0: with k0 the compiler keeps
       // every element's k as an induction variable, +32 VALU adds per k-tile iteration)
-      const int kt = kbeg + (kend - kbeg - 1) / BK * BK;
+      int kt = kbeg + (kend - kbeg - 1) / BK * BK;
+      // opaque here, so the partial tile's ~32 index-map evaluations (about a hundred 32-bit
+      // vector multiplies) are not hoisted into every workgroup's prologue by LICM: only the
+      // workgroups that reach a partial tile pay them
+      asm volatile("" : "+s"(kt));
 #pragma unroll
       for (int j = 0; j < LA1; ++j) {
         int row, k;
