@@ -830,6 +830,13 @@ struct Bwd {
     return ks.wait(st, t);
   }
 
+  // EmbedS LayerNorm backward: its dY partial sums (the pre_conv bias gradient) in the (BN, D)
+  // gcon_s after the gamma slab, when both fit
+  float* preconv_bias_part() const {
+    const int64_t pb = ln_bwd_part_blocks(m.BN);
+    if (!gd.pre_conv_b || !ln_bwd_partials_ok(m.D) || 2 * pb > m.BN) return nullptr;
+    return w.gcon_s + pb * m.D;
+  }
   // TAt LayerNorm backward: gamma / beta partial slabs (both fit in the (BFT, N) gcon_a)
   bool tat_part() const { return ln_bwd_partials_ok(m.N) && 2 * ln_bwd_part_blocks(m.BFT) <= m.BFT; }
 
@@ -912,10 +919,11 @@ struct Bwd {
       for (int q = 0; q < 3; ++q) {
         const int ks = m.ks[q];
         const int64_t C2 = 2 * (int64_t)m.C;
-        const int64_t cs = C2 * m.T;
         Gemm& g = segs[q];
         g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
-        g.A = w.dconv[q]; g.am = idx2(m.T, C2, cs); g.ak = idx1(1);
+        // row (bn, t) of the padded layout sits at (bn T + t) C2 (node stride T C2): a
+        // single-level row map (cheap prologue / epilogue row offsets)
+        g.A = w.dconv[q]; g.am = idx1(C2); g.ak = idx1(1);
         g.B = s.Wgb[q]; g.bk = idx1(m.C); g.bn = idx1(1);  // flipped (j', o, c)
         g.C = w.dX; g.cm = idx1(m.C); g.cn = idx1(1);
       }
@@ -1078,8 +1086,12 @@ struct Bwd {
       a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s; a.g = p.embS_g;
       if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
       a.dx = w.dY; a.dxrow = idx1(m.D);
-      if (ln_bwd_partials_ok(m.D)) { a.gpart = w.gcon_s; a.bpart = w.bcon_s; }
-      else { a.gcontrib = w.gcon_s; a.bcontrib = w.bcon_s; }
+      if (ln_bwd_partials_ok(m.D)) {
+        a.gpart = w.gcon_s; a.bpart = w.bcon_s;
+        a.xpart = preconv_bias_part();  // the pre_conv bias sums ride on this launch
+      } else {
+        a.gcontrib = w.gcon_s; a.bcontrib = w.bcon_s;
+      }
       DS_TRY(op_ln_bwd(a, st));
     }
     // --- side: SAt projection, EmbedS gamma / beta / pos-embedding, pre_conv bias and weight grads
@@ -1102,11 +1114,13 @@ struct Bwd {
       }
     }
     // gamma / beta: column sums of the LN backward's partial slabs (or contribution tensors)
-    DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}},
+    // pre_conv bias = column sum of dY: from the LN backward's per-workgroup dY sums in the same
+    // launch as gamma / beta (as a column-sum column of the dW GEMM it would add a whole 64-wide
+    // column tile to the 384-wide output: measured slower), else its own column sum
+    float* xpart = preconv_bias_part();
+    DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}, {xpart, xpart ? gd.pre_conv_b : nullptr}},
                    ln_bwd_partials_ok(m.D) ? ln_bwd_part_blocks(m.BN) : m.BN, m.D, 1));
-    // pre_conv bias: its own column sum (as a column-sum column of the dW GEMM it would add a
-    // whole 64-wide column tile to the 384-wide output: measured slower)
-    DS_TRY(colsum_on(sd, w.dY, m.BN, m.D, 1, gd.pre_conv_b));
+    if (!xpart) DS_TRY(colsum_on(sd, w.dY, m.BN, m.D, 1, gd.pre_conv_b));
     if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sd));
     if (gd.pre_conv_w) {
       Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
@@ -1172,6 +1186,7 @@ struct Bwd {
       g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
       DS_TRY(sgemm(g));
     }
+    if (wqkv_side()) DS_TRY(tat_wqkv_grad(true));
     {  // dE = dU + dqkv [Wq; Wk; Wv]
       Gemm g;
       g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.QW;
@@ -1212,8 +1227,15 @@ struct Bwd {
   // stream after dx: the side stream is still busy with the earlier parameter gradients
   // (pre_conv, SAt), while the main chain has nothing left (measured: the side stream's tail
   // was the step's critical path)
-  int tat_wqkv_grad() {
+  // DSTAGNN_WQKV_SIDE=1: issue it on the side stream right after the TAt backward instead (beside
+  // the main chain's dE GEMM and transpose, once the side stream's earlier work has drained)
+  static bool wqkv_side() {
+    static const bool on = getenv("DSTAGNN_WQKV_SIDE") && atoi(getenv("DSTAGNN_WQKV_SIDE")) != 0;
+    return on;
+  }
+  int tat_wqkv_grad(bool side) {
     if (!(gd.tat_wq || gd.tat_wk || gd.tat_wv)) return 0;
+    hipStream_t q = side ? sd : st;
     const int64_t N = m.N;
     Gemm g;
     g.M = (int)m.QW; g.N = m.N; g.K = (int)m.BFT;
@@ -1221,13 +1243,13 @@ struct Bwd {
     g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
     const bool adjacent = gd.tat_wq && gd.tat_wk == gd.tat_wq + m.HQ * N && gd.tat_wv == gd.tat_wk + m.HQ * N;
     g.C = adjacent ? gd.tat_wq : w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
-    DS_TRY(gemm(g));
+    DS_TRY(side ? sgemm(g) : gemm(g));
     if (!adjacent) {
       PackRows pk;
       pk.n = 3; pk.cols = m.N; pk.unpack = 1;
       pk.src[0] = w.dWqkv; pk.rows[0] = (int)m.HQ; pk.rows[1] = (int)m.HQ; pk.rows[2] = (int)m.HV;
       pk.dst[0] = gd.tat_wq; pk.dst[1] = gd.tat_wk; pk.dst[2] = gd.tat_wv;
-      DS_TRY(op_pack_rows(pk, st));
+      DS_TRY(op_pack_rows(pk, q));
     }
     return 0;
   }
@@ -1248,7 +1270,7 @@ struct Bwd {
     ht.lap("preconv");
     DS_TRY(stage_tat());
     ht.lap("tat");
-    DS_TRY(tat_wqkv_grad());
+    if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));
     DS_TRY(join());
     ht.lap("join");
     return 0;

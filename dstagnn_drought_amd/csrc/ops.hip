@@ -28,17 +28,29 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
   const float* ip = in + (int64_t)b * in_bs;
   float* op = out + (int64_t)b * out_bs;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  for (int y = ty; y < 32; y += 8) {
-    int r = r0 + y, c = c0 + tx;
+  // the accumulated output's old values are loaded in the same round as the input tile (they do
+  // not depend on it): one memory round trip per workgroup instead of two
+  float old[4] = {0.f, 0.f, 0.f, 0.f};
+  if (beta != 0.f) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + ty + 8 * u, r = r0 + tx;
+      if (r < R && c < Cc) old[u] = op[(int64_t)c * R + r];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int y = ty + 8 * u, r = r0 + y, c = c0 + tx;
     tile[y][tx] = (r < R && c < Cc) ? ip[(int64_t)r * Cc + c] : 0.f;
   }
   __syncthreads();
-  for (int y = ty; y < 32; y += 8) {
-    int c = c0 + y, r = r0 + tx;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int y = ty + 8 * u, c = c0 + y, r = r0 + tx;
     if (r < R && c < Cc) {
-      int64_t o = (int64_t)c * R + r;
+      const int64_t o = (int64_t)c * R + r;
       float v = tile[tx][y];
-      if (beta != 0.f) v += beta * op[o];
+      if (beta != 0.f) v += beta * old[u];
       op[o] = v;
     }
   }
@@ -599,9 +611,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   constexpr int RPW = PART ? kLnRowsPerWave : 1;
   const int L = a.L;
-  float gp[VPT], bp[VPT];
+  float gp[VPT], bp[VPT], xp[VPT];
 #pragma unroll
-  for (int q = 0; q < VPT; ++q) { gp[q] = 0.f; bp[q] = 0.f; }
+  for (int q = 0; q < VPT; ++q) { gp[q] = 0.f; bp[q] = 0.f; xp[q] = 0.f; }
   for (int i = 0; i < RPW; ++i) {
     const int row = (blockIdx.x * 4 + wv) * RPW + i;
     if (row >= a.R) break;  // wave-uniform
@@ -653,6 +665,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
         int64_t oo = xo + (int64_t)e * a.dxes;
         if (a.beta != 0.f) dx += a.beta * xin[q];
         a.dx[oo] = dx;
+        if (PART) xp[q] += dx;
       }
     }
   }
@@ -669,6 +682,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
       const float b = red[1][0][e] + red[1][1][e] + red[1][2][e] + red[1][3][e];
       if (a.gpart) a.gpart[(int64_t)blockIdx.x * L + e] = g;
       if (a.bpart) a.bpart[(int64_t)blockIdx.x * L + e] = b;
+    }
+    if (a.xpart) {  // the dx sums through the same LDS rows (workgroup-uniform branch)
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < VPT; ++q) red[0][wv][lane + 64 * q] = xp[q];
+      __syncthreads();
+      for (int e = threadIdx.x; e < L; e += 256)
+        a.xpart[(int64_t)blockIdx.x * L + e] = red[0][0][e] + red[0][1][e] + red[0][2][e] + red[0][3][e];
     }
   }
 }
@@ -1347,7 +1368,7 @@ int op_ln_fwd(const LnFwd& a, hipStream_t st) {
 
 int op_ln_bwd(const LnBwd& a, hipStream_t st) {
   int vpt = (int)cdiv64(a.L, 64);
-  if (a.gpart || a.bpart) {
+  if (a.gpart || a.bpart || a.xpart) {
     if (!ln_bwd_partials_ok(a.L)) { set_last_error("ln_bwd: partial slabs need L <= 1024"); return DSTAGNN_E_SHAPE; }
     dim3 grid((unsigned)ln_bwd_part_blocks(a.R));
     if (vpt <= 1) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, st, a);

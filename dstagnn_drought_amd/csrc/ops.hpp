@@ -33,6 +33,9 @@ struct LnBwd {
   // (ln_bwd_part_blocks(R), L) slabs, L <= 1024 (ln_bwd_partials_ok)
   float* gpart = nullptr;
   float* bpart = nullptr;
+  // optional with the slabs: per-workgroup sums of the written dx rows (a following linear
+  // layer's bias gradient: the column sum of dx, with no re-read of dx)
+  float* xpart = nullptr;
 };
 constexpr int kLnRowsPerWave = 1;  // rows per wave of the partial-slab LN backward (measured: 4 is slower)
 inline int64_t ln_bwd_part_blocks(int64_t R) { return (R + 4 * kLnRowsPerWave - 1) / (4 * kLnRowsPerWave); }
