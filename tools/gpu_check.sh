@@ -19,6 +19,9 @@ run() {
   return 0
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
+# steps appended from an (untracked) tools/.extra_steps file: extends a queued call's list
+[ -f tools/.extra_steps ] && STEPS="$STEPS,$(tr -d '[:space:]' < tools/.extra_steps)"
+echo "steps: $STEPS"
 IFS=',' read -ra S <<< "$STEPS"
 for s in "${S[@]}"; do
   case $s in
