@@ -170,8 +170,10 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(budget_s=12.0):
-    """Oracle (literal restatement of the reference loops) on this host's cores."""
+def cpu_baseline(budget_s=12.0, warmup=2, min_iters=5, max_iters=20):
+    """Oracle (literal restatement of the reference loops) on this host's cores, per BASELINE.md:
+    `warmup` untimed iterations, then each fwd+bwd iteration timed on its own — at least
+    `min_iters`, more while within `budget_s` — and the MEDIAN iteration reported."""
     from oracle import dstagnn_ref as ref
     c = CFG
     torch.set_num_threads(host_cores())
@@ -189,17 +191,18 @@ def cpu_baseline(budget_s=12.0):
     g_re = torch.randn(B, c["C"], c["n_heads"], c["T"], c["T"], generator=gen)
     dims = dict(n_heads=c["n_heads"], d_k=c["d_k"], d_v=c["d_k"], K=c["K"])
     apa = torch.from_numpy(pa).float()
-    ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, hoist=False)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+    for _ in range(warmup):
         ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, hoist=False)
-        n += 1
-        if time.perf_counter() - t0 > budget_s or n >= 20:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(n * B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} fwd+bwd iterations of the PEMS08 inner block at B={B} (oracle, literal T x K loop), "
-                      f"{dt:.1f} s"}
+    times, t0 = [], time.perf_counter()
+    while len(times) < min_iters or (len(times) < max_iters and time.perf_counter() - t0 < budget_s):
+        t1 = time.perf_counter()
+        ref.block_forward_backward(p, x, res, cheb, apa, dims, g_out, g_re, hoist=False)
+        times.append(time.perf_counter() - t1)
+    med = float(np.median(times))
+    return {"value": round(B / med, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"median of {len(times)} timed fwd+bwd iterations (after {warmup} warm-ups) of the PEMS08 inner "
+                      f"block at B={B} (oracle, literal T x K loop), {sum(times):.1f} s timed; "
+                      f"min / max {B / max(times):.1f} / {B / min(times):.1f} samples/s"}
 
 
 def _free_port():

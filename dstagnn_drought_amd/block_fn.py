@@ -100,38 +100,57 @@ def cfg_of(meta):
     return [meta["n_heads"], meta["d_k"], meta["d_v"], meta["d_model"], meta["K"], meta["C"]]
 
 
-def flags_of(train, sparse, direct, flash=False):
+SAMPLE_SHIFT = 32  # flags bits 32..: the call's first global sample index (torch_ops.cpp kSampleShift)
+
+
+def flags_of(train, sparse, direct, flash=False, sample_base=0):
+    if sample_base < 0:
+        raise ValueError("sample_base must be >= 0")
     return ((_lib.F_TRAIN if train else 0) | (_lib.F_SPARSE if sparse else 0) | (_lib.F_DIRECT if direct else 0)
-            | (_lib.F_POISON if _POISON else 0) | (_lib.F_FLASH if flash else 0))
+            | (_lib.F_POISON if _POISON else 0) | (_lib.F_FLASH if flash else 0) | (int(sample_base) << SAMPLE_SHIFT))
 
 
-def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False, flash=None, plan_cache=None):
+def block_call(x, res_att, params, slots, graph, meta, train, seed, direct=False, flash=None, plan_cache=None,
+               sample_base=0):
     """(out, re_at) = dstagnn::block(...) — autograd-tracked.  In direct-gradient mode with a
     plan_cache dict (the module's), the block's constant arguments go to the library once, as a
-    cached BlockPlan (dstagnn::block_planned): same kernels, less host work per call."""
+    cached BlockPlan (dstagnn::block_planned): same kernels, less host work per call.
+    sample_base: global index of x[0] (a data-parallel shard's offset; keys the dropout masks)."""
     ops = _lib.load()
     x = x.float().contiguous()
     sparse = use_sparse(graph, meta, x.shape[3])
     fl = use_flash(graph, meta, x.shape[3], flash, x.shape[0])
-    flags = flags_of(train, sparse, direct, fl)
+    flags = flags_of(train, sparse, direct, fl, sample_base)
     if direct and plan_cache is not None:
         key = (id(params), id(graph), sparse, fl)
         ent = plan_cache.get("plan")
         if ent is None or ent[0] != key:
             plist = list(params)
             plan = torch.classes.dstagnn.BlockPlan(plist, list(slots), graph_list(graph, sparse, fl), cfg_of(meta))
-            anchor = next((p for p in plist if p.requires_grad), plist[0])
-            ent = (key, plan, anchor, params, graph)  # params / graph kept alive: the key holds their ids
+            ent = [key, plan, _anchor(plist, None), params, graph]  # params / graph kept alive: the key holds their ids
             plan_cache["plan"] = ent
+        elif not ent[2].requires_grad:
+            # the anchor (the autograd input that keeps the node in the graph when x needs no
+            # gradient) was frozen since: re-pick among the parameters that train now (ADVICE r3)
+            ent[2] = _anchor(ent[3], ent[2])
         return ops.block_planned(x, res_arg(res_att, x.shape[2]), ent[1], ent[2], float(meta.get("drop_p", 0.05)),
                                  int(seed), flags)
     return ops.block(x, res_arg(res_att, x.shape[2]), list(params), slots, graph_list(graph, sparse, fl),
                      cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed), flags)
 
 
-def dropout_masks(meta, x_shape, seed):
-    """The exact keep-masks (scaled by 1/(1-p)) the HIP forward draws for `seed`:
-    (mask after EmbedS (B,N,D), mask after fcmy (B,N,C,T)) — for parity tests."""
+def _anchor(params, fallback):
+    """A parameter that currently requires grad (the planned op's autograd anchor), else
+    `fallback` (else the first parameter): with none trainable and x not requiring grad no node
+    is recorded, and there is nothing to differentiate."""
+    return next((p for p in params if p.requires_grad), fallback if fallback is not None else params[0])
+
+
+def dropout_masks(meta, x_shape, seed, sample_base=0):
+    """The exact keep-masks (scaled by 1/(1-p)) the HIP forward draws for `seed` on samples
+    sample_base .. sample_base + B - 1 of the global batch: (mask after EmbedS (B,N,D), mask
+    after fcmy (B,N,C,T)) — for parity tests."""
     ops = _lib.load()
     like = torch.empty(0, device="cuda")
-    return ops.dropout_masks(like, list(x_shape), cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed))
+    return ops.dropout_masks(like, list(x_shape), cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed),
+                             int(sample_base))

@@ -9,6 +9,7 @@
 //                         Chebyshev product, so the aggregation writes (B,N,C,T) directly)
 //   X (B,N,C,T)           conv_g (B*N, 2C, T-k+1)   G (B*N, C, 3T-12)   out (B,N,C,T)
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -66,7 +67,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.nnz = m.flash ? d.cheb_nnz : 0;
   m.fsmall = m.flash && flash_small(m.N);
   static const bool agg_env = !getenv("DSTAGNN_CHEB_AGG") || atoi(getenv("DSTAGNN_CHEB_AGG")) != 0;
-  m.agg = agg_env && m.sparse && cheb_agg_ok(m.F, m.C);
+  m.agg = agg_env && m.sparse && cheb_agg_ok(m.F, m.C, m.K, m.T);
   m.apa_nnz = m.fsmall ? std::max(d.cheb_apa_nnz, 0) : 0;
   return m;
 }
@@ -209,6 +210,7 @@ int check_dims(const dstagnn_block_dims* d) {
     set_last_error("cheb_flash requires cheb_sparse, d_k == 32, cheb_nnz > 0 and B <= 128");
     return DSTAGNN_E_SHAPE;
   }
+  if (d->sample_base < 0) { set_last_error("sample_base < 0"); return DSTAGNN_E_ARG; }
   if (d->F != 1 && d->F != d->C) {
     // the reference fails at model/DSTAGNN_my.py:252 (x.permute + time_conv_output)
     set_last_error("The size of tensor a (" + std::to_string(d->F) + ") must match the size of tensor b (" +
@@ -216,6 +218,16 @@ int check_dims(const dstagnn_block_dims* d) {
     return DSTAGNN_E_SHAPE;
   }
   return 0;
+}
+
+// Dropout mask index offset of a dropout site (which 0: after EmbedS, (B,N,D) order; 1: after
+// fcmy, (B,N,C,T) order): the keep-mask of an element is a hash of (seed, site, global index),
+// and the global index counts from sample `sample_base` (a data-parallel shard's first sample in
+// the global batch), so a sharded train step draws exactly the masks of the 1-GPU step on the
+// concatenated batch.
+uint64_t drop_off(const dstagnn_block_dims& d, int which) {
+  const uint64_t per = which == 0 ? (uint64_t)d.N * d.d_model : (uint64_t)d.N * d.C * d.T;
+  return (uint64_t)d.sample_base * per;
 }
 
 // ------------------------------------------------------------------------------
@@ -439,12 +451,15 @@ struct HostTimer {
 struct SideStream {
   hipStream_t side = nullptr;
   hipEvent_t ev[64] = {};
-  int next = 0;
+  // ring positions and sequence numbers are claimed atomically: the SideStream is shared by
+  // every caller on the device (e.g. the autograd device thread and a forward on another
+  // thread), and two callers must never get the same slot or sequence number
+  std::atomic<uint32_t> next{0};
   // flag words for stream-ordered write / wait-value synchronisation (see Streams)
-  static constexpr int kSlots = 4096;
+  static constexpr int kSlots = 4096;  // divides 2^32: the claimed counters wrap consistently
   uint32_t* flags = nullptr;
-  uint32_t gseq = 0;
-  int fnext = 0;
+  std::atomic<uint32_t> gseq{0};
+  std::atomic<uint32_t> fnext{0};
   bool use_flags = true;
   bool side_flags = false;  // DSTAGNN_SYNC_EVENTS=2: flags for the side stream's signals too
   bool ok = false;
@@ -517,14 +532,12 @@ struct Streams {
     *t = SyncTok{};
     if (!ss) return 0;
     if (ss->use_flags && (from != ss->side || ss->side_flags)) {
-      t->slot = ss->fnext;
-      ss->fnext = (ss->fnext + 1) % SideStream::kSlots;
-      t->seq = ++ss->gseq;
+      t->slot = (int)(ss->fnext.fetch_add(1, std::memory_order_relaxed) % SideStream::kSlots);
+      t->seq = ss->gseq.fetch_add(1, std::memory_order_relaxed) + 1;
       const hipError_t r = hipStreamWriteValue32(from, ss->flags + t->slot, t->seq, 0);
       return r == hipSuccess ? 0 : fail(r);
     }
-    t->ev = ss->ev[ss->next];
-    ss->next = (ss->next + 1) % 64;
+    t->ev = ss->ev[ss->next.fetch_add(1, std::memory_order_relaxed) % 64];
     const hipError_t r = hipEventRecord(t->ev, from);
     return r == hipSuccess ? 0 : fail(r);
   }
@@ -685,7 +698,9 @@ struct Fwd {
       a.g = p.embS_g; a.b = p.embS_b;
       a.y = s.Zd; a.yrow = idx1(m.D);
       a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s;
-      if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
+      if (d.train && d.drop_p > 0.f) {
+        a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; a.drop_off = drop_off(d, 0);
+      }
       DS_TRY(op_ln_fwd(a, st));
     }
     {  // SMultiHeadAttention W_Q / W_K (:62-63) as ONE GEMM over the stacked weights
@@ -744,7 +759,7 @@ struct Fwd {
     for (int q = 0; q < 3; ++q) t.conv[q] = s.conv[q];
     t.fcmy_w = p.fcmy_w; t.fcmy_b = p.fcmy_b;
     t.X = s.X; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
-    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
+    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; t.drop_off = drop_off(d, 1); }
     t.G = s.G; t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c; t.out = out;
     return op_gtu_tail_fwd(t, st);
   }
@@ -864,7 +879,7 @@ struct Bwd {
     for (int q = 0; q < 3; ++q) { t.conv[q] = s.conv[q]; t.dconv_pad[q] = w.dconv[q]; }
     t.fcmy_w = p.fcmy_w;
     t.X = s.X; t.x = x; t.res_w = p.res_w; t.res_b = p.res_b; t.ln_g = p.ln_g; t.ln_b = p.ln_b;
-    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; }
+    if (d.train && d.drop_p > 0.f) { t.drop_p = d.drop_p; t.seed = d.seed; t.drop_off = drop_off(d, 1); }
     t.tco = s.tco; t.r = s.r; t.mu = s.mu_c; t.rs = s.rs_c;
     t.dout = dout; t.gcontrib = w.gcon_t; t.dtc = w.dtc; t.dX = w.dX; t.dx = dx;
     t.rcontrib = w.bcon_t; t.dres = w.dres_t; t.dG = w.dGt;
@@ -1084,7 +1099,9 @@ struct Bwd {
       a.R = (int)m.BN; a.L = m.D;
       a.dy = w.dZd; a.dyrow = idx1(m.D);
       a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s; a.g = p.embS_g;
-      if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; }
+      if (d.train && d.drop_p > 0.f) {
+        a.drop_p = d.drop_p; a.seed = d.seed; a.which = 0; a.drop_off = drop_off(d, 0);
+      }
       a.dx = w.dY; a.dxrow = idx1(m.D);
       if (ln_bwd_partials_ok(m.D)) {
         a.gpart = w.gcon_s; a.bpart = w.bcon_s;
@@ -1453,8 +1470,9 @@ int dstagnn_colsum(const float* in, int64_t A, int O, int I, float* out, int64_t
 
 int dstagnn_dropout_mask(const dstagnn_block_dims* d, int which, float* mask, dstagnn_stream_t stream) {
   if (!d || !mask) return DSTAGNN_E_ARG;
+  if (which != 0 && which != 1) return DSTAGNN_E_ARG;
   int64_t n = which == 0 ? (int64_t)d->B * d->N * d->d_model : (int64_t)d->B * d->N * d->C * d->T;
-  return op_dropout_mask(mask, n, d->seed, (uint32_t)which, d->drop_p, (hipStream_t)stream);
+  return op_dropout_mask(mask, n, d->seed, (uint32_t)which, d->drop_p, drop_off(*d, which), (hipStream_t)stream);
 }
 
 int dstagnn_block_time_stage(const dstagnn_block_dims* d, const dstagnn_block_params* p, const dstagnn_graph* g,

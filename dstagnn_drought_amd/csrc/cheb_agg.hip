@@ -499,17 +499,26 @@ struct SpmmTL {
 };
 
 int check(const ChebAg& a) {
-  if (!cheb_agg_ok(a.F, a.C) || a.K < 1 || a.K > 8) {
-    set_last_error("cheb_agg: F in 1..32, C in {16, 32}, K in 1..8");
+  if (!cheb_agg_ok(a.F, a.C, a.K, a.T)) {
+    set_last_error("cheb_agg: F in 1..32, C in {16, 32}, K in 1..8, SDDMM LDS 16*K*F*T <= 160 KB");
     return DSTAGNN_E_SHAPE;
   }
   return 0;
 }
 
+size_t sddmm_lds_bytes(int K, int F, int T) { return (size_t)4 * K * F * T * sizeof(float); }
+
 }  // namespace
 
-// F <= 32 (one MFMA contraction / tile side), C = 16 or 32 (16-float operand rows)
-bool cheb_agg_ok(int F, int C) { return F >= 1 && F <= 32 && (C == 16 || C == 32); }
+// F <= 32 (one MFMA contraction / tile side), C = 16 or 32 (16-float operand rows), K <= 8
+// (the kernels' order templates), and the backward SDDMM's per-workgroup LDS image of the K
+// dagg_k = Theta_k g_j^T tiles (4 waves x K x F x T floats) within the CU's 160 KB — checked
+// here, where the block picks its path, so a shape the backward cannot run (e.g. K = 3, F = 32,
+// T = 144) takes the Theta-first sparse path from the forward on
+bool cheb_agg_ok(int F, int C, int K, int T) {
+  return F >= 1 && F <= 32 && (C == 16 || C == 32) && K >= 1 && K <= 8 && T >= 1 &&
+         sddmm_lds_bytes(K, F, T) <= (160u << 10);
+}
 
 int op_cheb_agg_fwd(const ChebAg& a0, hipStream_t st) {
   DS_TRY(check(a0));
@@ -524,8 +533,7 @@ int op_cheb_agg_sddmm(const ChebAg& a0, hipStream_t st) {
   DS_TRY(check(a0));
   const ChebAg a = with_order(a0);
   const int FT = a.F * a.T;
-  const size_t lds = (size_t)4 * a.K * FT * sizeof(float);
-  if (lds > (160u << 10)) { set_last_error("cheb_agg: K*F*T too large for the LDS"); return DSTAGNN_E_SHAPE; }
+  const size_t lds = sddmm_lds_bytes(a.K, a.F, a.T);
   dispatch<SddmmL>(nq_of(std::min(FT, 1024)), km_of(a.K), Launch{a, dim3(grid_rows((int64_t)a.B * a.N)), lds, st});
   DS_CHECK_LAUNCH();
   return 0;

@@ -339,10 +339,11 @@ struct Prof {
 };
 Prof g_prof;
 // split-K target grid (workgroups): a GEMM whose grid is below 128 workgroups splits its K
-// range to about this many (320: best of a same-box sweep over 128..1024, tools/knob_sweep.sh,
-// DESIGN §5; 1 = never split: every reduction in one fixed order, so a per-sample result is
-// bit-identical at any batch size); DSTAGNN_SPLITK_TARGET overrides
-int g_splitk_target = getenv("DSTAGNN_SPLITK_TARGET") ? atoi(getenv("DSTAGNN_SPLITK_TARGET")) : 320;
+// range to about this many (448: best of the round-3-end same-box sweep over 256 / 320 / 448,
+// tools/knob_sweep.sh; 1 = never split: every tiled reduction in one fixed order, so
+// a per-sample result is bit-identical at any batch size — the skinny weight-gradient kernel
+// splits regardless, see plan_skinny); DSTAGNN_SPLITK_TARGET overrides
+int g_splitk_target = getenv("DSTAGNN_SPLITK_TARGET") ? atoi(getenv("DSTAGNN_SPLITK_TARGET")) : 448;
 // operand precision of every GEMM: 0 = fp32 (v_mfma_f32_32x32x2_f32, the reference's
 // arithmetic), 1 = bf16 operands rounded to nearest even with fp32 accumulation
 // (v_mfma_f32_32x32x16_bf16) — an opt-in variant, see gemm_set_bf16

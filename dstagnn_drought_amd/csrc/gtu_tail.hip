@@ -167,7 +167,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) void
           const float* wr = Ws + t * WS;
           for (int sidx = 0; sidx < S; ++sidx) tc = fmaf(gr[sidx], wr[sidx], tc);
         }
-        if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+        if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e) + a.drop_off, a.drop_p);
         float tco, xres;
         if (a.first) {
           tco = fmaxf(tc, 0.f);
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         dr = rr[e] > 0.f ? dr : 0.f;                 // relu(xres + tco)
         const float dtco = tcov[u] > 0.f ? dr : 0.f;  // tco = relu(...)
         float dtc = dtco;
-        if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+        if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e) + a.drop_off, a.drop_p);
         a.dtc[base + e] = dtc;
         if (a.first) {
           dXs[t * CP + c] = 0.f;
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
       const float* gr = Gs + c * SP;
       const float* wr = Wl + t * SP;
       for (int sidx = 0; sidx < S; ++sidx) tc = fmaf(gr[sidx], wr[sidx], tc);
-      if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+      if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e) + a.drop_off, a.drop_p);
       float tco, xres;
       if (a.first) {
         tco = fmaxf(tc, 0.f);
@@ -741,7 +741,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
       dr = rr[e] > 0.f ? dr : 0.f;                 // relu(xres + tco)
       const float dtco = tcov[u] > 0.f ? dr : 0.f;  // tco = relu(...)
       float dtc = dtco;
-      if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e), a.drop_p);
+      if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e) + a.drop_off, a.drop_p);
       a.dtc[base + e] = dtc;
       if (a.first) {
         dXs[t * CP + c] = 0.f;

@@ -595,7 +595,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd a) {
     if (e < L) {
       if (a.u) a.u[(int64_t)row * L + e] = v[q];
       float y = (v[q] - mean) * rs * (PRE ? gv[PRE ? q : 0] : a.g[e]) + (PRE ? bv[PRE ? q : 0] : a.b[e]);
-      if (a.drop_p > 0.f) y *= drop_scale(a.seed, a.which, (uint64_t)row * L + e, a.drop_p);
+      if (a.drop_p > 0.f) y *= drop_scale(a.seed, a.which, (uint64_t)row * L + e + a.drop_off, a.drop_p);
       a.y[yo + (int64_t)e * a.yes] = y;
     }
   }
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd a) {
       dyv[q] = 0.f; xh[q] = 0.f;
       if (e < L) {
         float dy = dyl[q];
-        if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * L + e, a.drop_p);
+        if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * L + e + a.drop_off, a.drop_p);
         float x = (ul[q] - mean) * rs;
         dyv[q] = dy; xh[q] = x;
         float dxh = dy * (PRE ? gl[PRE ? q : 0] : a.g[e]);
@@ -1238,9 +1238,9 @@ __global__ __launch_bounds__(256) void pack_theta_kernel(PackTheta a) {
   }
 }
 
-__global__ void dropout_mask_kernel(float* out, int64_t n, uint64_t seed, uint32_t which, float p) {
+__global__ void dropout_mask_kernel(float* out, int64_t n, uint64_t seed, uint32_t which, float p, uint64_t off) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = drop_scale(seed, which, (uint64_t)i, p);
+    out[i] = drop_scale(seed, which, (uint64_t)i + off, p);
 }
 
 inline unsigned grid1d(int64_t n, int64_t cap = 8192) {
@@ -1504,8 +1504,8 @@ int op_pack_rows(const PackRows& a, hipStream_t st) {
 }
 
 
-int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st) {
-  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid1d(n)), dim3(256), 0, st, out, n, seed, which, p);
+int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, uint64_t off, hipStream_t st) {
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid1d(n)), dim3(256), 0, st, out, n, seed, which, p, off);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -19,6 +19,7 @@ struct LnFwd {
   float* u = nullptr;           // optional (R, L) copy of the LN input sum
   float* mu = nullptr; float* rs = nullptr;
   float drop_p = 0.f; uint64_t seed = 0; uint32_t which = 0;  // dropout on the output
+  uint64_t drop_off = 0;  // added to the mask index (row * L + e): the shard's first global sample
 };
 
 struct LnBwd {
@@ -26,6 +27,7 @@ struct LnBwd {
   const float* dy = nullptr; Idx2 dyrow; int64_t dyes = 1;
   const float* u = nullptr; const float* mu = nullptr; const float* rs = nullptr; const float* g = nullptr;
   float drop_p = 0.f; uint64_t seed = 0; uint32_t which = 0;  // mask applied to dy
+  uint64_t drop_off = 0;  // as LnFwd::drop_off
   float* dx = nullptr; Idx2 dxrow; int64_t dxes = 1; float beta = 0.f;
   float* gcontrib = nullptr;    // optional (R, L): dy' * xhat  (gamma grad contributions)
   float* bcontrib = nullptr;    // optional (R, L): dy'         (beta grad contributions)
@@ -108,6 +110,7 @@ struct GtuTailArgs {
   const float* res_w = nullptr; const float* res_b = nullptr;
   const float* ln_g = nullptr; const float* ln_b = nullptr;
   float drop_p = 0.f; uint64_t seed = 0;
+  uint64_t drop_off = 0;  // added to the mask index (bn * C * T + e): the shard's first global sample
   // fwd outputs
   float* G = nullptr;             // [bn][C][3T-12] (saved for the fcmy weight gradient)
   float* tco = nullptr; float* r = nullptr; float* mu = nullptr; float* rs = nullptr; float* out = nullptr;
@@ -183,7 +186,7 @@ struct ChebAg {
   float* dx = nullptr; float dx_beta = 1.f;  // spmm_t: dx = dx_beta dx + (the Chebyshev path's gradient)
   int xcd_order = 0;
 };
-bool cheb_agg_ok(int F, int C);
+bool cheb_agg_ok(int F, int C, int K, int T);
 int op_cheb_agg_fwd(const ChebAg& a, hipStream_t st);
 int op_cheb_agg_sddmm(const ChebAg& a, hipStream_t st);
 int op_cheb_agg_spmm_t(const ChebAg& a, hipStream_t st);
@@ -248,4 +251,4 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st);
 // true when the backward runs split (LN | dG GEMM | gates) and needs GtuTailArgs::dG
 bool gtu_tail_bwd_split(int C, int T);
 int op_param_prep(const ParamPrep& a, hipStream_t st);
-int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, hipStream_t st);
+int op_dropout_mask(float* out, int64_t n, uint64_t seed, uint32_t which, float p, uint64_t off, hipStream_t st);

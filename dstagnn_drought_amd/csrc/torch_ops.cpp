@@ -71,8 +71,10 @@ static_assert(sizeof(dstagnn_block_grads) == kSlots * sizeof(void*), "grads stru
 bool unused_inner(int64_t slot) { return slot == 2 || slot == 3 || slot == 4 || slot == 38 || slot == 39; }
 
 // cfg = [n_heads, d_k, d_v, d_model, K, C]; flags: 1 train, 2 sparse, 4 direct grads, 8 poison,
-// 16 fused (flash) Chebyshev attention
+// 16 fused (flash) Chebyshev attention; bits 32.. carry the call's first global sample index
+// (dstagnn_block_dims::sample_base: a data-parallel shard's offset, keys the dropout masks)
 enum { kTrain = 1, kSparse = 2, kDirect = 4, kPoison = 8, kFlash = 16 };
+constexpr int kSampleShift = 32;
 
 int res_mode_of(const c10::optional<Tensor>& res, int64_t F) {
   if (!res.has_value() || !res->defined()) return DSTAGNN_RES_NONE;
@@ -116,6 +118,8 @@ BlockCall make_call(const Tensor& x, const c10::optional<Tensor>& res, at::Tenso
   d.train = (flags & kTrain) ? 1 : 0;
   d.drop_p = (float)drop_p;
   d.seed = (uint64_t)seed;
+  TORCH_CHECK(flags >= 0, "flags: negative sample base");
+  d.sample_base = flags >> kSampleShift;
   d.cheb_sparse = (flags & kSparse) ? 1 : 0;
   const float** arr = reinterpret_cast<const float**>(&c.p);
   for (size_t i = 0; i < params.size(); ++i) {
@@ -447,10 +451,10 @@ double block_time_stage(const Tensor& x, const c10::optional<Tensor>& res, at::T
   return ms;
 }
 
-// the dropout keep-masks (1/(1-p) or 0) the block draws for `seed`:
-// (after EmbedS (B,N,D), after fcmy (B,N,C,T))
+// the dropout keep-masks (1/(1-p) or 0) the block draws for `seed` on samples sample_base ..
+// sample_base + B - 1 of the global batch: (after EmbedS (B,N,D), after fcmy (B,N,C,T))
 std::tuple<Tensor, Tensor> dropout_masks(const Tensor& like, at::IntArrayRef shape, at::IntArrayRef cfg, double drop_p,
-                                         int64_t seed) {
+                                         int64_t seed, int64_t sample_base) {
   TORCH_CHECK(shape.size() == 4 && cfg.size() == 6, "dropout_masks: shape (B,N,F,T), cfg[6]");
   c10::DeviceGuard guard(like.device());
   dstagnn_block_dims d{};
@@ -458,6 +462,8 @@ std::tuple<Tensor, Tensor> dropout_masks(const Tensor& like, at::IntArrayRef sha
   d.n_heads = (int)cfg[0]; d.d_k = (int)cfg[1]; d.d_v = (int)cfg[2]; d.d_model = (int)cfg[3]; d.K = (int)cfg[4];
   d.C = (int)cfg[5];
   d.train = 1; d.drop_p = (float)drop_p; d.seed = (uint64_t)seed;
+  TORCH_CHECK(sample_base >= 0, "dropout_masks: sample_base must be >= 0");
+  d.sample_base = sample_base;
   Tensor m0 = at::empty({d.B, d.N, d.d_model}, f32(like));
   Tensor m1 = at::empty({d.B, d.N, d.C, d.T}, f32(like));
   check_rc(dstagnn_dropout_mask(&d, 0, m0.data_ptr<float>(), stream_of(like)), "dstagnn_dropout_mask");
@@ -794,7 +800,7 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("block_cheb_out(" DSTAGNN_BLK_ARGS ") -> Tensor");
   m.def("block_relu_out(" DSTAGNN_BLK_ARGS ", int which) -> Tensor");
 #undef DSTAGNN_BLK_ARGS
-  m.def("dropout_masks(Tensor like, int[] shape, int[] cfg, float drop_p, int seed) -> (Tensor, Tensor)");
+  m.def("dropout_masks(Tensor like, int[] shape, int[] cfg, float drop_p, int seed, int sample_base=0) -> (Tensor, Tensor)");
   m.def("cheb_sat_fwd(Tensor x, Tensor sat, Tensor theta_cat, Tensor mask_cat, Tensor[] graph, int C, bool sparse) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("cheb_sat_bwd(Tensor x, Tensor theta_cat, Tensor[] graph, Tensor out, Tensor P, Tensor W, Tensor xth, "

@@ -194,16 +194,17 @@ class GTU(nn.Module):
         self.con2out = nn.Conv2d(in_channels, 2 * in_channels, kernel_size=(1, kernel_size), stride=(1, time_strides))
 
 
-def _rank_seed(seed):
-    """Per-forward dropout seed, mixed with the data-parallel rank.  Every rank draws the same
-    value from torch's global RNG (all ranks keep one RNG state: the epoch permutation must be
-    identical), so without the mix every replica would drop the same positions of its own
-    shard; the reference's 8 replicas see the same batch (quirk 15), here they do not."""
+def _default_sample_base(B):
+    """Global index of this rank's first sample: rank * B under torch.distributed (equal shards,
+    as dp.shard_batch / train.DeviceBatches cut them), else 0.  Every rank draws the same dropout
+    seed from torch's global RNG (all ranks keep one RNG state: the epoch permutation must be
+    identical), and the library keys each keep-mask by (seed, global sample index, position), so
+    the shards drop different positions and a data-parallel train step draws exactly the masks
+    of the 1-GPU step on the concatenated batch (the reference's 8 replicas see the same batch,
+    quirk 15; here they do not)."""
     if torch.distributed.is_available() and torch.distributed.is_initialized():
-        r = torch.distributed.get_rank()
-        if r:
-            seed = (seed ^ ((r * 0x9E3779B97F4A7C15) & ((1 << 64) - 1))) & ((1 << 62) - 1)
-    return seed
+        return torch.distributed.get_rank() * B
+    return 0
 
 
 class DSTAGNN_block(nn.Module):
@@ -245,6 +246,9 @@ class DSTAGNN_block(nn.Module):
         self.flash_cheb = None
         self.direct_grads = False  # see set_direct_grads
         self.grads_ready = None    # DP hook: called with the block once its gradients are final
+        # global index of x[0] for the dropout masks (None: rank * B under torch.distributed,
+        # else 0; set it for unequal shards, see set_sample_base)
+        self.sample_base = None
 
     def forward(self, x, res_att):
         B, N, Fd, T = x.shape
@@ -260,13 +264,15 @@ class DSTAGNN_block(nn.Module):
         # a fresh dropout seed per training forward, drawn from torch's global RNG (no draw
         # when dropout is off: like F.dropout(p=0), which consumes no random numbers)
         drop = self.training and meta.get("drop_p", 0.0) > 0.0
-        meta["seed"] = _rank_seed(int(torch.randint(0, 2 ** 62, (1,)).item())) if drop else 0
+        meta["seed"] = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop else 0
+        base = (self.sample_base if self.sample_base is not None else _default_sample_base(B)) if drop else 0
         names, params, slots = self._param_list()
         graph = self._graph()
         if use_flash(graph, meta, T, self.flash_cheb, B):
             graph = self._flash_graph(graph)
         out, re_at = block_call(x, res_att, params, slots, graph, meta, meta["train"], meta["seed"],
-                                self.direct_grads, flash=self.flash_cheb, plan_cache=self.__dict__.setdefault("_pcache", {}))
+                                self.direct_grads, flash=self.flash_cheb, plan_cache=self.__dict__.setdefault("_pcache", {}),
+                                sample_base=base)
         if self.grads_ready is not None and out.requires_grad:
             # DP overlap (dp.GradAllReducer.attach): once this block's backward node has run,
             # its parameter gradients are final — hand them over from a post-hook on the node
@@ -275,6 +281,16 @@ class DSTAGNN_block(nn.Module):
 
     def _post_backward(self, grad_inputs, grad_outputs):
         self.grads_ready(self)
+
+    # the host-side caches hold library objects (a torch.classes BlockPlan has no pickler) and
+    # Parameter identities: rebuilt on demand, never pickled (torch.save(model) / deepcopy)
+    _CACHES = ("_pcache", "_plist", "_gcache")
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        for k in self._CACHES:
+            state.pop(k, None)
+        return state
 
     # host-side caches (the launch path is host-bound at these sizes): the parameter list
     # (Parameter objects survive .to()/.cuda()) and the graph dict (rebuilt when a buffer
@@ -374,6 +390,15 @@ def set_dropout(model, p):
             m.meta["drop_p"] = float(p)
             m.dropout.p = float(p)
             m.fcmy[1].p = float(p)
+    return model
+
+
+def set_sample_base(model, base):
+    """Global index of the first sample of `model`'s input batch on this process (dropout masks
+    are keyed by it); None restores the default rank * B under torch.distributed."""
+    for m in model.modules():
+        if isinstance(m, DSTAGNN_block):
+            m.sample_base = None if base is None else int(base)
     return model
 
 

@@ -70,6 +70,11 @@ typedef struct dstagnn_block_dims {
                               S tiles are recomputed from Q', K' on the matrix cores    */
   int cheb_nnz;            /* flash path: entries of the union support (== graph nnz)   */
   int cheb_apa_nnz;        /* flash path, N <= 512: entries of the adj_pa support (== graph apa_nnz) */
+  int64_t sample_base;     /* global index of sample 0 of this call (>= 0): the dropout keep-mask
+                              of an element is keyed by (seed, site, global sample index,
+                              position), so data-parallel shards (rank r holds samples
+                              [r*B, (r+1)*B) of the global batch) draw exactly the masks of a
+                              1-GPU step on the concatenated batch                          */
 } dstagnn_block_dims;
 
 /* Parameter pointers in state_dict order.  For the first block
@@ -230,7 +235,8 @@ int dstagnn_block_time_stage(const dstagnn_block_dims* d, const dstagnn_block_pa
                              int stage, int iters, float* ms_per_launch, dstagnn_stream_t stream);
 
 /* Dropout keep-mask the block draws (value 1/(1-p) or 0) for tests:
- * which = 0 (EmbedS output, (B,N,D)), 1 (fcmy output, (B,N,C,T) order of out). */
+ * which = 0 (EmbedS output, (B,N,D)), 1 (fcmy output, (B,N,C,T) order of out); samples
+ * d->sample_base .. d->sample_base + B - 1 of the global batch. */
 int dstagnn_dropout_mask(const dstagnn_block_dims* d, int which, float* mask, dstagnn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
@@ -312,9 +318,13 @@ int dstagnn_prof_start(int capacity);
 int dstagnn_prof_stop(dstagnn_prof_stats* stats);
 
 /* Split-K policy of the GEMMs: a GEMM with a grid below 128 workgroups splits its K range
- * over about `target` workgroups (default 320).  target = 1 never splits, so every reduction
- * runs in one fixed order and a sample's results are bit-identical at any batch size (parity
- * tests).  Returns the previous target; target <= 0 only queries. */
+ * over about `target` workgroups (default 448).  target = 1 never splits a tiled GEMM, so those
+ * reductions run in one fixed order and a sample's data-path results (outputs, d_x, d_res_att)
+ * are bit-identical at any batch size (parity tests).  Excluded: the skinny weight-gradient
+ * kernel (batch-1 GEMMs with M <= 96, N <= 32, K >= 4096: the fcmy and dTheta gradients) always
+ * splits K over up to 256 workgroups with a fixed-order fold — deterministic run to run, but
+ * its summation order depends on K (so on B).  Returns the previous target; target <= 0 only
+ * queries. */
 int dstagnn_set_splitk_target(int target);
 
 /* Operand precision of the GEMM family (every contraction of the block, its gradients and

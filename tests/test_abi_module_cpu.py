@@ -23,7 +23,8 @@ class BlockDims(ctypes.Structure):  # struct dstagnn_block_dims (include/dstagnn
     _fields_ = [(n, ctypes.c_int) for n in ("B", "N", "F", "T", "n_heads", "d_k", "d_v", "d_model", "K", "C",
                                             "res_mode", "train")] + \
         [("drop_p", ctypes.c_float), ("seed", ctypes.c_uint64), ("cheb_sparse", ctypes.c_int),
-         ("cheb_flash", ctypes.c_int), ("cheb_nnz", ctypes.c_int)]
+         ("cheb_flash", ctypes.c_int), ("cheb_nnz", ctypes.c_int), ("cheb_apa_nnz", ctypes.c_int),
+         ("sample_base", ctypes.c_int64)]
 
 
 def c_abi():
@@ -71,6 +72,34 @@ def test_block_sizes_and_shape_errors():
     rc = lib.dstagnn_block_sizes(ctypes.byref(bad), ctypes.byref(sv), ctypes.byref(sc))
     assert rc == 10001
     assert b"must match" in lib.dstagnn_last_error()
+    neg = BlockDims(32, 170, 32, 12, 3, 32, 32, 512, 3, 32, 1, 1, 0.05, 0)
+    neg.sample_base = -1
+    assert lib.dstagnn_block_sizes(ctypes.byref(neg), ctypes.byref(sv), ctypes.byref(sc)) == 10002
+
+
+def test_block_pickles_without_host_caches():
+    """the module's host-side caches (a torch.classes BlockPlan, which has no
+    pickler, and Parameter identities) stay out of pickled / deep-copied state; a copy rebuilds
+    them on its first call."""
+    import copy
+    import io
+    import dstagnn_drought_amd as D
+    N, T, K = 10, 12, 3
+    adj = np.eye(N) + np.roll(np.eye(N), 1, 1)
+    cheb = [torch.from_numpy(c).float() for c in D.cheb_polynomial(D.scaled_Laplacian(adj), K)]
+    blk = D.DSTAGNN_block("cpu", 1, 1, K, 8, 8, 1, cheb, adj, adj, N, T, 16, 8, 8, 2)
+    blk.__dict__["_pcache"] = {"plan": [None, lambda: None]}  # unpicklable, like a BlockPlan
+    blk._param_list()
+    buf = io.BytesIO()
+    torch.save(blk, buf)
+    buf.seek(0)
+    back = torch.load(buf, weights_only=False)  # our own freshly written object
+    assert "_pcache" not in back.__dict__ and "_plist" not in back.__dict__
+    assert back.sample_base is None
+    dup = copy.deepcopy(blk)
+    assert "_pcache" not in dup.__dict__
+    assert sorted(dup.state_dict()) == sorted(blk.state_dict())
+    assert "_pcache" in blk.__dict__  # the original keeps its caches
 
 
 def _golden_model(golden_dir):

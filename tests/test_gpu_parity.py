@@ -136,7 +136,7 @@ def test_gemm_transposed_batched_two_level():
 # ---------------------------------------------------------------------------------------
 # cheb_conv_withSAt operator vs the reference's golden vectors
 # ---------------------------------------------------------------------------------------
-@pytest.mark.parametrize("name", ["g1_cheb_pems04.npz", "g5_cheb_dense.npz"])
+@pytest.mark.parametrize("name", ["g1_cheb_pems04.npz", "g5_cheb_dense.npz", "g15_cheb_prod.npz"])
 @pytest.mark.parametrize("sparse", [0, 1])
 def test_cheb_sat_golden(golden_dir, name, sparse):
     _need_gpu()
@@ -181,12 +181,24 @@ def _block_from_golden(g, m, num_of_d):
     return blk.cuda().eval()
 
 
-@pytest.mark.parametrize("name", ["g2_block_first.npz", "g3_block_inner.npz", "g3b_block_inner_full.npz"])
+@pytest.mark.parametrize("name", ["g2_block_first.npz", "g3_block_inner.npz", "g3b_block_inner_full.npz",
+                                  "g13_block_inner_prod.npz", "g14_block_first_prod.npz"])
 def test_block_golden(golden_dir, name):
+    """The block against the reference's own outputs and gradients (tests/golden/gen_golden.py,
+    gen_golden_prod.py).  g13 / g14 are at the production geometry (N=170, F=C=32, T=12, K=3,
+    d_k=32): the default path there is the one bench.py times — flash_small_* (fused small-graph
+    attention), cheb_agg_* (aggregate-first Chebyshev), gtu_tail_*_ct (C=32 / T=12 GTU tail) —
+    asserted below, so the timed kernels are pinned to reference-written vectors directly."""
     _need_gpu()
+    from dstagnn_drought_amd import block_fn as bf
     g = load(golden_dir, name)
     m = json.loads(str(g["meta"]))
     blk = _block_from_golden(g, m, m["num_of_d"])
+    if "_prod" in name:
+        graph = blk._graph()
+        meta = dict(blk.meta)
+        assert bf.use_sparse(graph, meta, m["T"]) and bf.use_flash(graph, meta, m["T"], None, m["B"])
+        assert m["N"] <= bf.FLASH_SMALL_N and m["C"] == 32 and m["T"] == 12 and m["d_k"] == 32
     x = torch.from_numpy(g["x"]).cuda().requires_grad_(True)
     res = torch.from_numpy(g["res_att"]).cuda().requires_grad_(True) if "res_att" in g else 0
     out, re_at = blk(x, res)
@@ -352,6 +364,9 @@ CONFIGS = {
     "gambia": (2139, 144, 2, 2, 64, 32, 32),   # long series: sparse Chebyshev rows in 1024-element chunks
     "syn": (4096, 24, 5, 8, 512, 32, 32),
     "t24": (64, 24, 3, 2, 64, 32, 32),         # small graph, T >= 20: the split GTU tail
+    # K = 3 at a long series: the aggregate-first backward's LDS image (16 K F T bytes = 221 KB)
+    # does not fit, so cheb_agg_ok sends the block down the Theta-first sparse path
+    "t144k3": (48, 144, 3, 2, 64, 32, 32),
 }
 RELU_EPS = 1e-5  # ReLU decisions may differ from the fp64 oracle's only where |z| <= RELU_EPS * max|z|
 
@@ -507,7 +522,7 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
     # forced on at PEMS07 (N = 883, streamed) and forced off at small and large N, so both
     # paths are held to the oracle everywhere
     ("pems07", False, 2, True), ("pems08", False, 4, False), ("pems08", True, 2, False), ("pems04", False, 2, False),
-    ("t24", False, 2, False), ("gambia", False, 1, False)])
+    ("t24", False, 2, False), ("gambia", False, 1, False), ("t144k3", False, 2, None), ("t144k3", True, 1, None)])
 def test_block_vs_oracle_configs(name, first, B, flash):
     """Held against the oracle evaluated in float64 (pems08 at B=32: the bench configuration
     itself).  Bound per tensor: the stated 1e-4 (scaled by max(1, max|ref|)), or twice the
@@ -824,3 +839,63 @@ def test_block_never_reads_unwritten_memory(N, T, first, sparse):
     for k in plain:
         assert torch.isfinite(poisoned[k]).all(), f"{k}: NaN from an unwritten buffer"
         assert torch.equal(plain[k], poisoned[k]), f"{k}: differs with poisoned buffers"
+
+
+def test_frozen_anchor_keeps_other_grads():
+    """ADVICE r3: in direct-gradient mode the planned op's only parameter input is one anchor;
+    freezing the parameter that was the anchor when the plan was built must not drop the node
+    (x needs no gradient, res_att = 0: the first block on raw input) — every other trainable
+    parameter still gets its gradient, equal to the unfrozen run's."""
+    _need_gpu()
+    import dstagnn_drought_amd as D
+    B, N, T, K, h, Dm, dk, C = 2, 24, 12, 3, 2, 32, 8, 8
+    rs = np.random.RandomState(4)
+    tmd = np.eye(N)
+    pa = np.zeros((N, N))
+    for i in range(N):
+        tmd[i, rs.choice(N, 2, replace=False)] = 1.0
+        pa[i, rs.choice(N, 3, replace=False)] = 1.0
+    cheb = [torch.from_numpy(c_).float() for c_ in D.cheb_polynomial(D.scaled_Laplacian(tmd), K)]
+    torch.manual_seed(0)
+    blk = D.DSTAGNN_block("cpu", 1, 1, K, C, C, 1, cheb, pa, tmd, N, T, Dm, dk, dk, h)
+    for p in blk.parameters():
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+        else:
+            torch.nn.init.uniform_(p)
+    blk = D.set_direct_grads(blk.cuda().eval())
+    x = torch.randn(B, N, 1, T, device="cuda")
+    go = torch.randn(B, N, C, T, device="cuda")
+
+    def run():
+        for p in blk.parameters():
+            p.grad = None
+        out, _ = blk(x, 0)
+        out.backward(go)
+        return {n: p.grad.clone() for n, p in blk.named_parameters() if p.grad is not None}
+
+    full = run()                       # builds the plan (anchor = first trainable parameter)
+    first = next(iter(blk.parameters()))
+    first.requires_grad_(False)
+    try:
+        part = run()
+    finally:
+        first.requires_grad_(True)
+    name0 = next(iter(blk.state_dict()))
+    assert name0 not in part
+    assert sorted(part) == sorted(k for k in full if k != name0), sorted(set(full) ^ set(part))
+    for k in part:
+        assert torch.equal(part[k], full[k]), k
+
+
+def test_dropout_masks_keyed_by_global_sample():
+    """Data-parallel shards draw the masks of the concatenated batch: the masks of samples
+    [base, base + b) (sample_base = base) are rows [base, base + b) of the full batch's masks."""
+    _need_gpu()
+    from dstagnn_drought_amd.block_fn import dropout_masks
+    meta = dict(n_heads=3, d_k=32, d_v=32, d_model=64, K=3, C=32, drop_p=0.05)
+    full = dropout_masks(meta, (8, 30, 32, 12), 12345)
+    for base, b in ((0, 3), (3, 5), (6, 2)):
+        part = dropout_masks(meta, (b, 30, 32, 12), 12345, sample_base=base)
+        for f, q in zip(full, part):
+            assert torch.equal(f[base:base + b], q)

@@ -40,7 +40,7 @@ def test_laplacian_cheb_pems04(golden_dir):
     assert np.all((g["cheb_2"] != 0) <= supp)
 
 
-@pytest.mark.parametrize("name", ["g1_cheb_pems04.npz", "g5_cheb_dense.npz"])
+@pytest.mark.parametrize("name", ["g1_cheb_pems04.npz", "g5_cheb_dense.npz", "g15_cheb_prod.npz"])
 @pytest.mark.parametrize("hoist", [False, True])
 def test_cheb_conv_sat(golden_dir, name, hoist):
     g = load(golden_dir, name)
@@ -71,7 +71,8 @@ def block_case(golden_dir, name):
     return g, m, p, cheb, dims, res
 
 
-@pytest.mark.parametrize("name", ["g2_block_first.npz", "g3_block_inner.npz", "g3b_block_inner_full.npz"])
+@pytest.mark.parametrize("name", ["g2_block_first.npz", "g3_block_inner.npz", "g3b_block_inner_full.npz",
+                                  "g13_block_inner_prod.npz", "g14_block_first_prod.npz"])
 def test_block(golden_dir, name):
     g, m, p, cheb, dims, res = block_case(golden_dir, name)
     out, re_at, gx, gra, grads = ref.block_forward_backward(p, T(g["x"]), res, cheb, T(g["adj_pa"]), dims,
