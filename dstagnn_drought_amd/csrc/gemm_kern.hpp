@@ -372,6 +372,11 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   // LDS stages (compile-time: the stage addresses fold into immediates); deeper rings for the
   // tiles whose ring still fits 64 KB
   constexpr int NS = (BM + BN) * BK * 4 * DSTAGNN_GEMM_NS <= 65536 ? DSTAGNN_GEMM_NS : 2;
+  // the pipelined K loop (three stages, barrier before the last MFMA step; DSTAGNN_GEMM_PIPE=1)
+#ifndef DSTAGNN_GEMM_PIPE
+#define DSTAGNN_GEMM_PIPE 0
+#endif
+  constexpr bool PIPE = DSTAGNN_GEMM_PIPE && NS == 3 && !BF;
   constexpr int FT = NA + NB, PT = LA1 + LB1;  // DMA instructions of a full / the partial k-tile
   static_assert(NS >= 2 && NS <= 4, "LDS ring of 2..4 stages");
   __shared__ __attribute__((aligned(16))) float Asm[NS * BM * BK];
@@ -479,6 +484,114 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
 
   const int ntiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const bool ones_tile = g.nload < g.N && tc.n0 + BN > g.nload;  // uniform
+  // fragments: lane half lk supplies k = 16 lk + 4 q + c (c = 0..3) at step q (A and B agree)
+  auto read_a_st = [&](const float* as, int i, int q, float* v4) {
+    const int m = arow0 + i * 32 + lr;
+    if (A_KC) {
+      const int pq = (lk * 4 + q) ^ ((m >> 1) & 7);
+      const float4 v = *reinterpret_cast<const float4*>(as + m * BK + pq * 4);
+      v4[0] = v.x; v4[1] = v.y; v4[2] = v.z; v4[3] = v.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v4[c] = as[(lk * 16 + q * 4 + c) * BM + m];
+    }
+  };
+  auto read_b_st = [&](const float* bs, int j, int q, float* v4) {
+    const int n = bcol0 + j * 32 + lr;
+    if (!B_NC) {
+      const int pq = (lk * 4 + q) ^ ((n >> 1) & 7);
+      const float4 v = *reinterpret_cast<const float4*>(bs + n * BK + pq * 4);
+      v4[0] = v.x; v4[1] = v.y; v4[2] = v.z; v4[3] = v.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v4[c] = bs[(lk * 16 + q * 4 + c) * BN + n];
+    }
+  };
+  if constexpr (PIPE) {
+    // Pipelined K loop (three LDS stages, two tiles in flight): the wait + barrier that
+    // publishes tile t+1 sits BEFORE tile t's last MFMA step, and tile t+1's first two
+    // fragment steps are read behind it, so the LDS-read latency at a tile start and the
+    // barrier skew overlap tile t's last four MFMAs instead of idling the matrix pipe.
+    //   iteration t: issue tile t+2 -> stage (t+2)%3 (last read in iteration t-1, whose
+    //   fragments were all read and waited for before that iteration's barrier); MFMA steps
+    //   0..2 of tile t beside the reads of its steps 2, 3; lgkmcnt(0); vmcnt(tile t+2's DMAs)
+    //   + s_barrier; reads of tile t+1 steps 0, 1; MFMA step 3 of tile t.
+    static_assert(NS == 3 && !BF, "pipelined loop: three stages, fp32");
+    if (ntiles == 0) return;
+    const bool lastp = (kend - kbeg) % BK != 0;
+    // retire every DMA but those of tile `younger` (which may still be in flight), then barrier
+    auto retire = [&](int younger) {
+      if (younger >= ntiles) wait_vm_barrier<0>();
+      else if (younger == ntiles - 1 && lastp) wait_vm_barrier<PT>();
+      else wait_vm_barrier<FT>();
+    };
+    auto ones_fix = [&](int stg) {
+      if (ones_tile) {  // column-sum column: B = 1 in this stage's image (see the plain loop)
+        float* bst = Bsm + stg * BN * BK;
+        const int c = g.nload - tc.n0;
+        if (tid < BK) bst[B_NC ? tid * BN + c : c * BK + tid] = 1.f;
+        __syncthreads();
+      }
+    };
+    float fa[4][WM][4], fb[4][WN][4];
+    auto read_step = [&](int stg, int q) {
+      const float* as = Asm + stg * BM * BK;
+      const float* bs = Bsm + stg * BN * BK;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) read_a_st(as, i, q, fa[q][i]);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) read_b_st(bs, j, q, fb[q][j]);
+    };
+    floatx16 tacc[WM][WN];
+    auto mfma_step = [&](int q) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            if constexpr (ACC2)
+              tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][i][c], fb[q][j][c], (q | c) ? tacc[i][j] : zero_acc(),
+                                                               0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][i][c], fb[q][j][c], acc[i][j], 0, 0, 0);
+          }
+    };
+    issue(kbeg, 0);
+    if (ntiles > 1) issue(kbeg + BK, 1);
+    retire(1);
+    ones_fix(0);
+    read_step(0, 0);
+    read_step(0, 1);
+    int st = 0;
+    for (int t = 0; t < ntiles; ++t) {
+      const int st1 = st == 2 ? 0 : st + 1, st2 = st1 == 2 ? 0 : st1 + 1;
+      if (t + 2 < ntiles) issue(kbeg + (t + 2) * BK, st2);
+      read_step(st, 2);
+      mfma_step(0);
+      read_step(st, 3);
+      mfma_step(1);
+      mfma_step(2);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < ntiles) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's reads are complete
+        retire(t + 2);
+        ones_fix(st1);
+        read_step(st1, 0);
+        read_step(st1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mfma_step(3);
+      if constexpr (ACC2) {
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) acc[i][j] += tacc[i][j];
+      }
+      st = st1;
+    }
+    return;
+  }
   for (int s0 = 0; s0 < NS - 1; ++s0)
     if (s0 < ntiles) issue(kbeg + s0 * BK, s0);
   int st = 0;
