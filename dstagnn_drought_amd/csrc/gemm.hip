@@ -409,6 +409,22 @@ int gemm_prof_stop(dstagnn_prof_stats* out) {
 
 namespace {
 
+// persistent tile loop knobs: DSTAGNN_GEMM_PERSIST=1 turns it on; _MIN = fewest tiles that take
+// it; _WPC = workgroups per CU of its grid
+bool gemm_persist_on() {
+  static const bool on = getenv("DSTAGNN_GEMM_PERSIST") && atoi(getenv("DSTAGNN_GEMM_PERSIST")) != 0;
+  return on;
+}
+int64_t gemm_persist_min_tiles() {
+  static const int64_t v = getenv("DSTAGNN_GEMM_PERSIST_MIN") ? atoll(getenv("DSTAGNN_GEMM_PERSIST_MIN")) : 384;
+  return v;
+}
+int gemm_persist_wpc() {
+  static const int v = getenv("DSTAGNN_GEMM_PERSIST_WPC") ? std::max(1, atoi(getenv("DSTAGNN_GEMM_PERSIST_WPC"))) : 1;
+  return v;
+}
+constexpr int kCUs = 256;  // MI355X compute units
+
 // one problem's launch plan: its kernel descriptor and the kernel configuration it needs
 bool gemm_log_on() {
   static const bool on = getenv("DSTAGNN_GEMM_LOG") != nullptr;
@@ -417,15 +433,19 @@ bool gemm_log_on() {
 
 struct Plan {
   GemmK k;
-  char log[220];
+  char log[240];
   int best, va, vb, ns;
   bool akc, bnc, ktwo, hot, acc2;
   bool skinny;  // runs as skinny_dw_kernel (sk), never grouped
+  bool persist; // runs as gemm_f32_persist_kernel: k.count tiles over `wgs` workgroups
+  uint32_t wgs;
   SkinnyK sk;
   bool same_kernel(const Plan& o) const {
     return !skinny && !o.skinny && best == o.best && va == o.va && vb == o.vb && ns == o.ns && akc == o.akc &&
-           bnc == o.bnc && ktwo == o.ktwo && hot == o.hot && acc2 == o.acc2;
+           bnc == o.bnc && ktwo == o.ktwo && hot == o.hot && acc2 == o.acc2 && persist == o.persist;
   }
+  // workgroups of this problem's grid slice (before the padding to a multiple of 8)
+  uint32_t slice() const { return persist ? wgs : k.count; }
   // split-K slab floats this plan takes from the workspace
   size_t ws_floats() const {
     if (skinny) return (size_t)(sk.nwg + sk.ngrp) * sk.P4;
@@ -485,6 +505,8 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   GemmK& k = pl.k;
   k = GemmK{};
   pl.skinny = false;
+  pl.persist = false;
+  pl.wgs = 0;
   const int Nk = g.N + (g.ones_out ? 1 : 0);  // kernel columns (the column-sum column last)
   k.M = g.M; k.N = Nk; k.K = g.K; k.batch = g.batch;
   k.nload = g.N; k.ones_out = g.ones_out; k.ones_stride = (int32_t)g.ones_stride;
@@ -558,6 +580,11 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   // that does not split keeps one summation order under every tile configuration (a B=1 and a
   // B=32 call may pick different tiles: per-sample results stay bit-identical, test_batch_consistency)
   pl.acc2 = !g_bf16 && (best == 0 || best == 2) && splitk > 1 && kchunk > acc2_min_k();
+  // persistent tile loop (gemm_persist_body): no split-K, no column-sum column, fp32, the 64x64 /
+  // 128x32 tiles, enough tiles that a workgroup walks several; the workgroup count is set per
+  // launch (persist_slices)
+  pl.persist = gemm_persist_on() && splitk == 1 && !g.ones_out && !g_bf16 && (best == 0 || best == 2) && g.K > 0 &&
+               (int64_t)blocks >= gemm_persist_min_tiles();
   pl.akc = !g.ak.two && g.ak.s0 == 1;
   pl.bnc = !g.bn.two && g.bn.s0 == 1;
   pl.ktwo = g.ak.two || g.bk.two;
@@ -571,9 +598,9 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   k.nstage = pl.ns;
   if (gemm_log_on()) {
     // one "[gemm]" line per kernel launch (run_gemm_group joins a group's problems with " | ")
-    snprintf(pl.log, sizeof(pl.log), "M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d bf=%d ones=%d acc2=%d",
+    snprintf(pl.log, sizeof(pl.log), "M=%d N=%d K=%d batch=%d cfg=%d splitk=%d akc=%d bnc=%d ktwo=%d blocks=%lld ns=%d va=%d vb=%d bf=%d ones=%d acc2=%d persist=%d",
              g.M, Nk, g.K, g.batch, best, splitk, (int)pl.akc, (int)pl.bnc, (int)pl.ktwo, (long long)blocks * splitk,
-             pl.ns, pl.va, pl.vb, g_bf16, g.ones_out ? 1 : 0, (int)pl.acc2);
+             pl.ns, pl.va, pl.vb, g_bf16, g.ones_out ? 1 : 0, (int)pl.acc2, (int)pl.persist);
   }
   return 0;
 }
@@ -591,10 +618,31 @@ uint32_t make_group(const GemmK* const* ks, const uint32_t* counts, int n, GemmG
   return at;
 }
 
+// the workgroups of each persistent problem of one launch: about kCUs * wpc in all, shared in
+// proportion to the problems' k-tile work, each a multiple of 8 (every XCD walks its eighth of
+// the tile order) and at most the problem's tile count rounded up to 8
+void persist_slices(Plan* const* ps, int n, int ktiles_per_tile0 = -1) {
+  double work[kGroupMax], tot = 0;
+  for (int p = 0; p < n; ++p) {
+    const GemmK& k = ps[p]->k;
+    const int kt = ktiles_per_tile0 > 0 ? ktiles_per_tile0 : (k.K + BKMAX - 1) / BKMAX;
+    work[p] = (double)k.count * std::max(1, kt);
+    tot += work[p];
+  }
+  const double slots = (double)kCUs * gemm_persist_wpc();
+  for (int p = 0; p < n; ++p) {
+    const GemmK& k = ps[p]->k;
+    uint32_t w = (uint32_t)std::max(8.0, slots * work[p] / std::max(tot, 1.0));
+    w = std::min<uint32_t>((w + 7u) & ~7u, (k.count + 7u) & ~7u);
+    ps[p]->wgs = std::max<uint32_t>(8u, w & ~7u);
+  }
+}
+
 void launch_plans(Plan* const* ps, int n, hipStream_t st) {
   const GemmK* ks[kGroupMax];
   uint32_t counts[kGroupMax];
-  for (int p = 0; p < n; ++p) { ks[p] = &ps[p]->k; counts[p] = ps[p]->k.count; }
+  if (ps[0]->persist) persist_slices(ps, n);
+  for (int p = 0; p < n; ++p) { ks[p] = &ps[p]->k; counts[p] = ps[p]->slice(); }
   GemmG gg;
   const uint32_t grid = make_group(ks, counts, n, &gg);
   using Unit = void (*)(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
@@ -603,6 +651,11 @@ void launch_plans(Plan* const* ps, int n, hipStream_t st) {
       {{gemm_c0_k0_bf, gemm_c0_k1_bf}, {gemm_c1_k0_bf, gemm_c1_k1_bf}, {gemm_c2_k0_bf, gemm_c2_k1_bf}},
       {{gemm_c0_k0_a2, gemm_c0_k1_a2}, {nullptr, nullptr}, {gemm_c2_k0_a2, gemm_c2_k1_a2}}};
   const Plan& pl = *ps[0];
+  if (pl.persist) {
+    static const Unit punits[3][2] = {{gemm_p0_k0, gemm_p0_k1}, {nullptr, nullptr}, {gemm_p2_k0, gemm_p2_k1}};
+    punits[pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, false, st);
+    return;
+  }
   const int var = pl.acc2 ? 2 : (g_bf16 ? 1 : 0);
   units[var][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, pl.hot, st);
 }
@@ -728,7 +781,11 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
     }
   }
   GemmG gg{};
-  const uint32_t grid = (plans[0].k.count + 7u) & ~7u;
+  Plan* p0 = &plans[0];
+  int kts = 0;
+  for (int p = 0; p < n; ++p) kts += (gs[p].K + BKMAX - 1) / BKMAX;
+  if (p0->persist) persist_slices(&p0, 1, kts);
+  const uint32_t grid = (p0->slice() + 7u) & ~7u;
   gg.start[0] = (uint32_t)n;  // K-concatenated
   for (int p = 1; p < 4; ++p) gg.start[p] = grid;
   for (int p = 0; p < n; ++p) gg.k[p] = plans[p].k;
@@ -737,7 +794,10 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
       {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}},
       {{gemm_c0_k0_bf, gemm_c0_k1_bf}, {gemm_c1_k0_bf, gemm_c1_k1_bf}, {gemm_c2_k0_bf, gemm_c2_k1_bf}}};
   const Plan& pl = plans[0];
-  units[g_bf16 ? 1 : 0][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, false, st);
+  if (pl.persist)
+    gemm_p2_k0(gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, false, st);
+  else
+    units[g_bf16 ? 1 : 0][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, false, st);
   DS_CHECK_LAUNCH();
   if (gemm_log_on()) {
     fprintf(stderr, "[gemm] kcat %s", plans[0].log);

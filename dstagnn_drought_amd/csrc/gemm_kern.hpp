@@ -3,6 +3,7 @@
 // 32 kernels of a unit compile in parallel with the others) and gemm.hip (host dispatch,
 // split-K fold, profiling).  See gemm.hip for the design.
 #pragma once
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 
@@ -743,6 +744,295 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
 }
 
+// ---------------------------------------------------------------------------------
+// Persistent tile loop (gemm_persist_body).  For GEMMs that do not split K, every output tile
+// of the plain kernel pays a fixed cost the 6-30 k-tiles behind it do not amortise: the
+// argument fetch and tile decode, the first DMA round trip (~1 us under load) with the matrix
+// pipe idle, and the epilogue's stores.  Here a grid of about one workgroup per CU walks the
+// problem's tiles instead: workgroup (XCD x, index r) takes a contiguous run of the XCD's
+// eighth of the tile order (the same XCD-local order as decode_tile), and ONE three-stage
+// DMA / MFMA stream runs over the flattened (tile, k-tile) sequence of the run — the next
+// tile's first k-tiles are in flight while the current tile finishes, and its epilogue stores
+// drain behind the next tile's MFMAs.  The k loop is the pipelined one of gemm_glds_body
+// (PIPE: the barrier that publishes k-tile i+1 sits before k-tile i's last MFMA step, i+1's
+// first fragment steps are read behind it).  K-concatenated problems (run_gemm_kcat) walk
+// their segments in turn inside every tile.  No split-K, no column-sum column, fp32.
+// ---------------------------------------------------------------------------------
+template <int I>
+__device__ __forceinline__ uint32_t gword(const uint32_t (&v)[kGroupVregs]) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v[I >> 6], I & 63);
+}
+// K of problem / segment p (wave-uniform p <= 2)
+__device__ __forceinline__ int seg_k(const uint32_t (&v)[kGroupVregs], int p) {
+  constexpr int NK = (int)(sizeof(GemmK) / 4), OK = (int)(offsetof(GemmK, K) / 4);
+  if constexpr (kGroupMax >= 3) {
+    if (p == 2) return (int)gword<4 + 2 * NK + OK>(v);
+  }
+  if constexpr (kGroupMax >= 2) {
+    if (p == 1) return (int)gword<4 + NK + OK>(v);
+  }
+  return (int)gword<4 + OK>(v);
+}
+
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT>
+__device__ __forceinline__ void gemm_persist_body(const GemmG& gin) {
+  constexpr int BK = 32, NS = 3;
+  constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
+  constexpr int NA = BM * BK / (256 * VA), NB = BN * BK / (256 * VB);
+  constexpr int LA1 = BM * BK / 256, LB1 = BN * BK / 256;
+  constexpr int FT = NA + NB, PT = LA1 + LB1;
+  static_assert(NA + NB < 64 && LA1 % 4 == 0 && LB1 % 4 == 0, "vmcnt range / DMA batches");
+  static_assert((BM + BN) * BK * 4 * NS <= 65536, "persistent loop: three stages within 64 KB");
+  __shared__ __attribute__((aligned(16))) float Asm[NS * BM * BK];
+  __shared__ __attribute__((aligned(16))) float Bsm[NS * BN * BK];
+
+  uint32_t gv[kGroupVregs];
+  load_group_words(gin, gv);
+  uint32_t lbid, lnwg;
+  const GemmK g = pick(gv, group_slot(gv, lbid, lnwg));  // tile geometry + epilogue (problem 0's for kcat)
+  // this workgroup's run [u0, u1) of the tile order
+  const uint32_t T = g.count, xcd = lbid & 7, nx = lnwg >> 3, r = lbid >> 3;
+  const uint32_t X0 = (uint32_t)((uint64_t)T * xcd / 8), X1 = (uint32_t)((uint64_t)T * (xcd + 1) / 8);
+  const uint32_t u0 = X0 + (uint32_t)((uint64_t)(X1 - X0) * r / nx);
+  const uint32_t u1 = X0 + (uint32_t)((uint64_t)(X1 - X0) * (r + 1) / nx);
+  if (u0 >= u1) return;  // uniform, before any barrier
+  const int ntl = (int)(u1 - u0);
+  auto coords = [&](int tl) {
+    const uint32_t u = u0 + (uint32_t)tl;
+    const uint32_t gn = g.tiles_n, gm = g.tiles_m;
+    const uint32_t tf = g.n_fast ? gn : gm, ts = g.n_fast ? gm : gn;
+    const uint32_t f = u % tf, tr = u / tf, sl = tr % ts;
+    TileCoord c;
+    c.n0 = (int)(g.n_fast ? f : sl) * BN;
+    c.m0 = (int)(g.n_fast ? sl : f) * BM;
+    c.zb = (int)(tr / ts);
+    c.sp = 0;
+    return c;
+  };
+  // k-tiles per segment (one segment unless K-concatenated)
+  const int nseg = KCAT ? (int)group_word(gv, 0) : 1;
+  int segk[3] = {0, 0, 0}, skt[3] = {0, 0, 0};
+  segk[0] = KCAT ? seg_k(gv, 0) : g.K;
+  if (KCAT) {
+    if (nseg > 1) segk[1] = seg_k(gv, 1);
+    if (nseg > 2) segk[2] = seg_k(gv, 2);
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p) skt[p] = (segk[p] + BK - 1) / BK;
+  const int kts = skt[0] + skt[1] + skt[2];
+  const int total = ntl * kts;
+  if (kts == 0) return;  // K = 0 never reaches here (the host keeps such problems on the plain kernel)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WGN, wc = wid % WGN;
+  const int lr = lane & 31, lk = lane >> 5;
+  const int arow0 = wr * 32 * WM, bcol0 = wc * 32 * WN;
+
+  // ---- DMA side: the descriptor, tile and row offsets of the k-tile being issued
+  int dtl = -1, dp = -1;
+  GemmK dg = g;
+  TileCoord dtc = coords(0);
+  const float* dA = nullptr;
+  const float* dB = nullptr;
+  int a_kl[NA], b_kl[NB];
+  uint32_t ao[NA], bo[NB];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    int row, k;
+    img_rk<BM, A_KC>(VA == 4 ? 1024 * j + 256 * wid + 4 * lane : 256 * j + 64 * wid + lane, row, k);
+    a_kl[j] = k;
+    ao[j] = 0;
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    int col, k;
+    img_rk<BN, !B_NC>(VB == 4 ? 1024 * j + 256 * wid + 4 * lane : 256 * j + 64 * wid + lane, col, k);
+    b_kl[j] = k;
+    bo[j] = 0;
+  }
+  auto set_dma = [&](int tl, int p) {
+    if (tl != dtl) dtc = coords(tl);
+    if (KCAT && p != dp) dg = pick(gv, p);
+    dtl = tl;
+    dp = p;
+    dA = dg.A + zoff(dg.az, dtc.zb);
+    dB = dg.B + zoff(dg.bz, dtc.zb);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      int row, k;
+      img_rk<BM, A_KC>(VA == 4 ? 1024 * j + 256 * wid + 4 * lane : 256 * j + 64 * wid + lane, row, k);
+      const int m = dtc.m0 + row;
+      ao[j] = (uint32_t)dg.abias + (m < dg.M ? (uint32_t)koff(dg.am, m) : 0u);
+      if (!KTWO) ao[j] += (uint32_t)(k * dg.ak.s0);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      int col, k;
+      img_rk<BN, !B_NC>(VB == 4 ? 1024 * j + 256 * wid + 4 * lane : 256 * j + 64 * wid + lane, col, k);
+      const int n = dtc.n0 + col;
+      bo[j] = (uint32_t)dg.bbias + (n < dg.nload ? (uint32_t)koff(dg.bn, n) : 0u);
+      if (!KTWO) bo[j] += (uint32_t)(k * dg.bk.s0);
+    }
+  };
+  // segment / k-tile of flattened iteration it (within its tile)
+  auto split_it = [&](int it, int& tl, int& p, int& kt) {
+    tl = it / kts;
+    int rr = it - tl * kts;
+    p = 0;
+    if (KCAT) {
+      if (rr >= skt[0]) { rr -= skt[0]; p = 1; if (rr >= skt[1]) { rr -= skt[1]; p = 2; } }
+    }
+    kt = rr;
+  };
+  auto is_partial = [&](int it) {
+    int tl, p, kt;
+    split_it(it, tl, p, kt);
+    const int K = p == 0 ? segk[0] : (p == 1 ? segk[1] : segk[2]);
+    return kt == (K - 1) / BK && K % BK != 0;
+  };
+  auto issue_it = [&](int it, int st) {
+    int tl, p, kt;
+    split_it(it, tl, p, kt);
+    if (tl != dtl || p != dp) set_dma(tl, p);
+    const int kend = dg.K, k0 = kt * BK;
+    const uint32_t sa = lds_addr_of(Asm + st * BM * BK);
+    const uint32_t sb = lds_addr_of(Bsm + st * BN * BK);
+    auto aoff = [&](int j) -> uint32_t {
+      return KTWO ? ao[j] + (uint32_t)koff(dg.ak, k0 + a_kl[j]) : ao[j] + (uint32_t)(k0 * dg.ak.s0);
+    };
+    auto boff = [&](int j) -> uint32_t {
+      return KTWO ? bo[j] + (uint32_t)koff(dg.bk, k0 + b_kl[j]) : bo[j] + (uint32_t)(k0 * dg.bk.s0);
+    };
+    if (k0 + BK <= kend) {
+      if constexpr (VA == 4) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) glds16_saddr(dA, aoff(j) << 2, sa + 4 * (1024 * j + 256 * wid));
+      } else {
+#pragma unroll
+        for (int j = 0; j < NA; j += 4)
+          glds4_saddr(dA - 1024, aoff(j), aoff(j + 1), aoff(j + 2), aoff(j + 3), sa + 4 * (256 * j + 64 * wid));
+      }
+      if constexpr (VB == 4) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) glds16_saddr(dB, boff(j) << 2, sb + 4 * (1024 * j + 256 * wid));
+      } else {
+#pragma unroll
+        for (int j = 0; j < NB; j += 4)
+          glds4_saddr(dB - 1024, boff(j), boff(j + 1), boff(j + 2), boff(j + 3), sb + 4 * (256 * j + 64 * wid));
+      }
+    } else {  // partial k-tile: element by element, zeros past K (as gemm_glds_body)
+      int kt0 = (kend - 1) / BK * BK;
+      asm volatile("" : "+s"(kt0));
+#pragma unroll
+      for (int j = 0; j < LA1; ++j) {
+        int row, k;
+        img_rk<BM, A_KC>(256 * j + 64 * wid + lane, row, k);
+        const int m = dtc.m0 + row;
+        const uint32_t o = (uint32_t)dg.abias + (m < dg.M ? (uint32_t)koff(dg.am, m) : 0u) + (uint32_t)koff(dg.ak, kt0 + k);
+        glds_vaddr(kt0 + k < kend ? reinterpret_cast<const char*>(dA) + (size_t)(o << 2) : (const void*)g_zero_page,
+                   sa + 4 * (256 * j + 64 * wid));
+      }
+#pragma unroll
+      for (int j = 0; j < LB1; ++j) {
+        int col, k;
+        img_rk<BN, !B_NC>(256 * j + 64 * wid + lane, col, k);
+        const int n = dtc.n0 + col;
+        const uint32_t o = (uint32_t)dg.bbias + (n < dg.nload ? (uint32_t)koff(dg.bn, n) : 0u) + (uint32_t)koff(dg.bk, kt0 + k);
+        glds_vaddr(kt0 + k < kend ? reinterpret_cast<const char*>(dB) + (size_t)(o << 2) : (const void*)g_zero_page,
+                   sb + 4 * (256 * j + 64 * wid));
+      }
+    }
+  };
+  // retire every DMA but those of iteration `younger` (still in flight), then barrier
+  auto retire = [&](int younger) {
+    if (younger >= total) wait_vm_barrier<0>();
+    else if (is_partial(younger)) wait_vm_barrier<PT>();
+    else wait_vm_barrier<FT>();
+  };
+
+  // ---- MFMA side
+  floatx16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = zero_acc();
+  float fa[4][WM][4], fb[4][WN][4];
+  auto read_step = [&](int stg, int q) {
+    const float* as = Asm + stg * BM * BK;
+    const float* bs = Bsm + stg * BN * BK;
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      const int m = arow0 + i * 32 + lr;
+      if (A_KC) {
+        const int pq = (lk * 4 + q) ^ ((m >> 1) & 7);
+        const float4 v = *reinterpret_cast<const float4*>(as + m * BK + pq * 4);
+        fa[q][i][0] = v.x; fa[q][i][1] = v.y; fa[q][i][2] = v.z; fa[q][i][3] = v.w;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) fa[q][i][c] = as[(lk * 16 + q * 4 + c) * BM + m];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = bcol0 + j * 32 + lr;
+      if (!B_NC) {
+        const int pq = (lk * 4 + q) ^ ((n >> 1) & 7);
+        const float4 v = *reinterpret_cast<const float4*>(bs + n * BK + pq * 4);
+        fb[q][j][0] = v.x; fb[q][j][1] = v.y; fb[q][j][2] = v.z; fb[q][j][3] = v.w;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) fb[q][j][c] = bs[(lk * 16 + q * 4 + c) * BN + n];
+      }
+    }
+  };
+  auto mfma_step = [&](int q) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][i][c], fb[q][j][c], acc[i][j], 0, 0, 0);
+  };
+
+  issue_it(0, 0);
+  if (total > 1) issue_it(1, 1);
+  retire(1);
+  read_step(0, 0);
+  read_step(0, 1);
+  TileCoord ctc = coords(0);
+  int st = 0, tl = 0, kin = 0;  // compute side: stage, tile of the run, iteration within the tile
+  for (int it = 0; it < total; ++it) {
+    const int st1 = st == 2 ? 0 : st + 1, st2 = st1 == 2 ? 0 : st1 + 1;
+    if (it + 2 < total) issue_it(it + 2, st2);
+    read_step(st, 2);
+    mfma_step(0);
+    read_step(st, 3);
+    mfma_step(1);
+    mfma_step(2);
+    __builtin_amdgcn_sched_barrier(0);
+    if (it + 1 < total) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's fragment reads are complete
+      retire(it + 2);
+      read_step(st1, 0);
+      read_step(st1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    mfma_step(3);
+    st = st1;
+    if (++kin == kts) {  // the tile is complete: its epilogue, then the next tile
+      gemm_epilogue<WM, WN>(g, ctc, arow0, bcol0, lane, acc);
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[i][j] = zero_acc();
+      kin = 0;
+      if (++tl < ntl) ctc = coords(tl);
+    }
+  }
+}
+
 // occupancy target (waves per SIMD) the register allocator works to
 #ifndef DSTAGNN_GEMM_WPE
 #define DSTAGNN_GEMM_WPE 4
@@ -757,7 +1047,40 @@ template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, DSTAGNN_GEMM_WPE))) void gemm_f32_hot_kernel(GemmG g) {
   gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
 }
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void gemm_f32_persist_kernel(GemmG g) {
+  gemm_persist_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, KCAT>(g);
+}
 }  // namespace
+
+// the persistent kernel for one configuration; grid = the sum of the problems' padded slices
+template <int WGM, int WGN, int WM, int WN, bool KTWO>
+void persist_cfg(const GemmG& kk, dim3 grid, bool akc, bool bnc, int va, int vb, hipStream_t st) {
+  if (kk.start[0] > 0) {  // K-concatenated (run_gemm_kcat checked kcat_ok)
+    if constexpr (WGM == 4 && WGN == 1 && WM == 1 && WN == 1 && !KTWO)
+      hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, true, true, KTWO, 4, 4, true>), grid, dim3(256), 0,
+                         st, kk);
+    return;
+  }
+#define DS_PV(AK, BN_)                                                                                          \
+  if (va == 4 && vb == 4)                                                                                     \
+    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4, false>), grid, dim3(256), 0, st, kk); \
+  else if (va == 4)                                                                                           \
+    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1, false>), grid, dim3(256), 0, st, kk); \
+  else if (vb == 4)                                                                                           \
+    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 4, false>), grid, dim3(256), 0, st, kk); \
+  else                                                                                                        \
+    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 1, false>), grid, dim3(256), 0, st, kk);
+  if (akc && bnc) { DS_PV(true, true) }
+  else if (akc)   { DS_PV(true, false) }
+  else if (bnc)   { DS_PV(false, true) }
+  else            { DS_PV(false, false) }
+#undef DS_PV
+}
+#define DS_GEMM_PUNIT(NAME, WGM, WGN, WM, WN, KTWO)                                                    \
+  void NAME(const GemmG& k, dim3 grid, bool akc, bool bnc, int va, int vb, bool, hipStream_t st) {    \
+    persist_cfg<WGM, WGN, WM, WN, KTWO>(k, grid, akc, bnc, va, vb, st);                               \
+  }
 
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool BF, bool KCAT = false,
           bool ACC2 = false>
@@ -821,5 +1144,9 @@ void gemm_c0_k0_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 void gemm_c0_k1_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 void gemm_c2_k0_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 void gemm_c2_k1_a2(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_p0_k0(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_p0_k1(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_p2_k0(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
+void gemm_p2_k1(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
 
 }  // namespace dsgemm
