@@ -357,7 +357,8 @@ unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
 // ---------------------------------------------------------------------------------------
 constexpr int kSmallN = 512;         // <= 16 tiles: <= kSmallTPW per wave
 constexpr int kXs = 36;              // LDS row stride (floats) of a staged (N, 32) operand: 16-B rows
-constexpr int kStripE = 1024;        // sparse entries of one strip staged in LDS (else read from HBM)
+constexpr int kStripE = 512;         // sparse entries of one strip staged in LDS (else read from HBM); 512: the
+                                     // PEMS08 backward fits 3 workgroups per CU (50 KB of LDS each, 54 at 1024)
 
 // forward: lse_j, P and W = T o P on the T support, P on the A_pa support, for one
 // (b, k, 32-column strip).  The strip's P tile goes through LDS ((32 nt) x 33 floats, dynamic).

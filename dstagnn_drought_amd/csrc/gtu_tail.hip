@@ -506,14 +506,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 // parameter vectors — is issued in ONE round at the node's start, into registers; everything
 // after that reads LDS and registers only and ends in stores.
 // ---------------------------------------------------------------------------------------
-template <int C, int T, int NT, int W>  // W: occupancy floor for the register allocator (waves / SIMD)
+// FIRST (compile-time a.first): no uniform branch among the node's loads — a branch there made
+// the compiler wait for every load issued before it (vmcnt(0) at the join), splitting the one
+// round into three dependent ones
+template <int C, int T, int NT, int W, bool FIRST>  // W: occupancy floor for the register allocator (waves / SIMD)
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void gtu_tail_fwd_ct_kernel(GtuTailArgs a) {
   constexpr int S = 3 * T - 12, CT = C * T, C2 = 2 * C, CS = C * S, SP = S + 1, CP = C + 1;
   constexpr int P = T < NT ? NT / T : 1, NRED = P * T > NT ? P * T : NT;
   constexpr int NG = (CS + NT - 1) / NT, NE = (CT + NT - 1) / NT;
   __shared__ float Gs[C * SP], rl[CT], Xs[T * CP], red[NRED], mus[T], rss[T], Wl[T * SP];
   const int tid = threadIdx.x;
-  for (int e = tid; e < T * S; e += NT) Wl[(e / S) * SP + e % S] = a.fcmy_w[e];
+  constexpr int NW = (T * S + NT - 1) / NT;
+  {  // the fcmy weight: every load first, then the LDS stores (one memory round)
+    float wv[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) wv[u] = a.fcmy_w[min(tid + NT * u, T * S - 1)];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int e = tid + NT * u;
+      if (e < T * S) Wl[(e / S) * SP + e % S] = wv[u];
+    }
+  }
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     const int64_t base = bn * CT;
     // every load of the node, one round
@@ -534,11 +547,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
     for (int u = 0; u < NE; ++u) {
       const int e = min(tid + NT * u, CT - 1);
       const int c = e / T, t = e - c * T;
-      Xv[u] = a.first ? 0.f : a.X[base + e];  // (t, c) order, staged below
-      xv[u] = a.first ? a.x[bn * T + t] : a.x[base + e];
+      Xv[u] = FIRST ? 0.f : a.X[base + e];  // (t, c) order, staged below
+      xv[u] = FIRST ? a.x[bn * T + t] : a.x[base + e];
       fb[u] = a.fcmy_b[t];
-      rw[u] = a.first ? a.res_w[c] : 0.f;
-      rb[u] = a.first ? a.res_b[c] : 0.f;
+      rw[u] = FIRST ? a.res_w[c] : 0.f;
+      rb[u] = FIRST ? a.res_b[c] : 0.f;
       lg[u] = a.ln_g[c];
       lb[u] = a.ln_b[c];
     }
@@ -551,7 +564,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
         Gs[c * SP + sidx] = fast_tanh(pv[u]) * fast_sigmoid(qv[u]);
       }
     }
-    if (!a.first) {
+    if (!FIRST) {
 #pragma unroll
       for (int u = 0; u < NE; ++u) {
         const int e = tid + NT * u;
@@ -572,7 +585,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
       for (int sidx = 0; sidx < S; ++sidx) tc = fmaf(gr[sidx], wr[sidx], tc);
       if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(base + e) + a.drop_off, a.drop_p);
       float tco, xres;
-      if (a.first) {
+      if (FIRST) {
         tco = fmaxf(tc, 0.f);
         xres = rw[u] * xv[u] + rb[u];
       } else {
@@ -658,7 +671,7 @@ __device__ __forceinline__ void tail_gate_bwd(float* dconv, int ks, int off, int
   }
 }
 
-template <int C, int T, int NT, int W>
+template <int C, int T, int NT, int W, bool FIRST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void gtu_tail_bwd_ct_kernel(GtuTailArgs a) {
   constexpr int S = 3 * T - 12, CT = C * T, SP = S + 1, CP = C + 1;
   constexpr int P = T < NT ? NT / T : 1, NRED2 = 2 * (P * T > NT ? P * T : NT);
@@ -670,7 +683,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
   float* dXs = sh;  // [t][CP] (dX tile, written to HBM coalesced)
   float* red = sh;
   const int tid = threadIdx.x;
-  for (int e = tid; e < T * S; e += NT) Wl[e] = a.fcmy_w[e];
+  constexpr int NW = (T * S + NT - 1) / NT;
+  {  // the fcmy weight: every load first, then the LDS stores (one memory round)
+    float wv[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) wv[u] = a.fcmy_w[min(tid + NT * u, T * S - 1)];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int e = tid + NT * u;
+      if (e < T * S) Wl[e] = wv[u];
+    }
+  }
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     const int64_t base = bn * CT;
     const bool last = bn == a.BN - 1;
@@ -685,7 +708,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
       muv[u] = a.mu[bn * T + t];
       rsw[u] = a.rs[bn * T + t];
       tcov[u] = a.tco[base + e];
-      xv[u] = a.first ? a.x[bn * T + t] : 0.f;
+      xv[u] = FIRST ? a.x[bn * T + t] : 0.f;
       lg[u] = a.ln_g[c];
     }
     float p3[NQ3], q3[NQ3], p5[NQ5], q5[NQ5], p7[NQ7], q7[NQ7];
@@ -743,7 +766,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
       float dtc = dtco;
       if (a.drop_p > 0.f) dtc *= drop_scale(a.seed, 1, (uint64_t)(base + e) + a.drop_off, a.drop_p);
       a.dtc[base + e] = dtc;
-      if (a.first) {
+      if (FIRST) {
         dXs[t * CP + c] = 0.f;
         if (!a.rpart) {
           a.rcontrib[base + e] = dr * xv[u];
@@ -759,7 +782,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
     __syncthreads();
     for (int e = tid; e < CT; e += NT) a.dX[base + e] = dXs[(e / C) * CP + e % C];  // coalesced
     __syncthreads();  // dXs shares its LDS with dGs
-    if (a.first) {
+    if (FIRST) {
       for (int t = tid; t < T; t += NT) {
         float sum = 0.f;
         for (int c = 0; c < C; ++c) sum += a.res_w[c] * xhl[c * T + t];
@@ -894,8 +917,14 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
   }
   const size_t lds = fwd_lds(a, true);
   if (a.C == 32 && a.T == 12 && tail_ct()) {
-    if (tail_ct() == 2) hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 5>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 1>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
+    const dim3 g(node_grid(a.BN));
+    if (tail_ct() == 2) {
+      if (a.first) hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 5, true>), g, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 5, false>), g, dim3(256), 0, st, a);
+    } else {
+      if (a.first) hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 1, true>), g, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 12, 256, 1, false>), g, dim3(256), 0, st, a);
+    }
     DS_CHECK_LAUNCH();
     return 0;
   }
@@ -930,8 +959,14 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
   }
   const size_t lds = bwd_lds(a, true);
   if (a.C == 32 && a.T == 12 && !generic && tail_ct()) {
-    if (tail_ct() == 2) hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 5>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 1>), dim3(node_grid(a.BN)), dim3(256), 0, st, a);
+    const dim3 g(node_grid(a.BN));
+    if (tail_ct() == 2) {
+      if (a.first) hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 5, true>), g, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 5, false>), g, dim3(256), 0, st, a);
+    } else {
+      if (a.first) hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 1, true>), g, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 1, false>), g, dim3(256), 0, st, a);
+    }
     DS_CHECK_LAUNCH();
     return 0;
   }
