@@ -774,17 +774,32 @@ __device__ __forceinline__ int seg_k(const uint32_t (&v)[kGroupVregs], int p) {
   return (int)gword<4 + OK>(v);
 }
 
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT>
+// retire every DMA but the newest n (a runtime count from a small set of sums of FT / PT)
+template <int FT, int PT>
+__device__ __forceinline__ void wait_vm_barrier_rt(int n) {
+  if (n == 0) wait_vm_barrier<0>();
+  else if (n == FT) wait_vm_barrier<FT>();
+  else if (n == PT) wait_vm_barrier<PT>();
+  else if (n == 2 * FT) wait_vm_barrier<(2 * FT < 64 ? 2 * FT : 0)>();
+  else if (n == FT + PT) wait_vm_barrier<(FT + PT < 64 ? FT + PT : 0)>();
+  else if (n == 2 * PT) wait_vm_barrier<(2 * PT < 64 ? 2 * PT : 0)>();
+  else wait_vm_barrier<0>();  // (never: n is one of the above) the safe over-wait
+}
+
+// PNS: LDS stages (PNS - 1 k-tiles in flight); the stage ring lives in ONE dynamic LDS array
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT, int PNS>
 __device__ __forceinline__ void gemm_persist_body(const GemmG& gin) {
-  constexpr int BK = 32, NS = 3;
+  constexpr int BK = 32, NS = PNS;
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   constexpr int NA = BM * BK / (256 * VA), NB = BN * BK / (256 * VB);
   constexpr int LA1 = BM * BK / 256, LB1 = BN * BK / 256;
   constexpr int FT = NA + NB, PT = LA1 + LB1;
   static_assert(NA + NB < 64 && LA1 % 4 == 0 && LB1 % 4 == 0, "vmcnt range / DMA batches");
-  static_assert((BM + BN) * BK * 4 * NS <= 65536, "persistent loop: three stages within 64 KB");
-  __shared__ __attribute__((aligned(16))) float Asm[NS * BM * BK];
-  __shared__ __attribute__((aligned(16))) float Bsm[NS * BN * BK];
+  static_assert(NS >= 3 && NS <= 4 && (NS - 2) * (FT > PT ? FT : PT) < 64, "two or three stages in flight");
+  static_assert((BM + BN) * BK * 4 * NS <= 160 * 1024, "persistent loop: the ring within the CU's LDS");
+  extern __shared__ __attribute__((aligned(16))) float psmem[];
+  float* const Asm = psmem;
+  float* const Bsm = psmem + NS * BM * BK;
 
   uint32_t gv[kGroupVregs];
   load_group_words(gin, gv);
@@ -944,11 +959,12 @@ __device__ __forceinline__ void gemm_persist_body(const GemmG& gin) {
       }
     }
   };
-  // retire every DMA but those of iteration `younger` (still in flight), then barrier
-  auto retire = [&](int younger) {
-    if (younger >= total) wait_vm_barrier<0>();
-    else if (is_partial(younger)) wait_vm_barrier<PT>();
-    else wait_vm_barrier<FT>();
+  // retire every DMA but those of iterations [first, first + NS - 2) (still in flight), then barrier
+  auto dmas_of = [&](int it) { return it >= total ? 0 : (is_partial(it) ? PT : FT); };
+  auto retire = [&](int first) {
+    int n = dmas_of(first);
+    if constexpr (NS >= 4) n += dmas_of(first + 1);
+    wait_vm_barrier_rt<FT, PT>(n);
   };
 
   // ---- MFMA side
@@ -996,16 +1012,18 @@ __device__ __forceinline__ void gemm_persist_body(const GemmG& gin) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][i][c], fb[q][j][c], acc[i][j], 0, 0, 0);
   };
 
-  issue_it(0, 0);
-  if (total > 1) issue_it(1, 1);
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < total) issue_it(q, q);
   retire(1);
   read_step(0, 0);
   read_step(0, 1);
   TileCoord ctc = coords(0);
   int st = 0, tl = 0, kin = 0;  // compute side: stage, tile of the run, iteration within the tile
   for (int it = 0; it < total; ++it) {
-    const int st1 = st == 2 ? 0 : st + 1, st2 = st1 == 2 ? 0 : st1 + 1;
-    if (it + 2 < total) issue_it(it + 2, st2);
+    const int st1 = st == NS - 1 ? 0 : st + 1;
+    const int stn = st == 0 ? NS - 1 : st - 1;  // the stage of iteration it - 1 = it + NS - 1
+    if (it + NS - 1 < total) issue_it(it + NS - 1, stn);
     read_step(st, 2);
     mfma_step(0);
     read_step(st, 3);
@@ -1047,30 +1065,49 @@ template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, DSTAGNN_GEMM_WPE))) void gemm_f32_hot_kernel(GemmG g) {
   gemm_glds_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, BF, KCAT>(g);
 }
-template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT>
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT, int PNS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void gemm_f32_persist_kernel(GemmG g) {
-  gemm_persist_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, KCAT>(g);
+  gemm_persist_body<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, KCAT, PNS>(g);
 }
 }  // namespace
+
+// LDS stages of the persistent kernel (DSTAGNN_GEMM_PERSIST_NS = 3 or 4)
+inline int persist_ns() {
+  static const int v = getenv("DSTAGNN_GEMM_PERSIST_NS") && atoi(getenv("DSTAGNN_GEMM_PERSIST_NS")) == 4 ? 4 : 3;
+  return v;
+}
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT, int PNS>
+void persist_launch(const GemmG& kk, dim3 grid, hipStream_t st) {
+  constexpr size_t lds = (size_t)(32 * WM * WGM + 32 * WN * WGN) * 32 * 4 * PNS;
+  auto ker = gemm_f32_persist_kernel<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, KCAT, PNS>;
+  if constexpr (lds > 65536) {
+    static bool done = false;  // raise the kernel's dynamic-LDS limit once
+    if (!done) {
+      (void)hipFuncSetAttribute((const void*)ker, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      done = true;
+    }
+  }
+  hipLaunchKernelGGL(ker, grid, dim3(256), lds, st, kk);
+}
+template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT>
+void persist_launch_ns(const GemmG& kk, dim3 grid, hipStream_t st) {
+  if (persist_ns() == 4) persist_launch<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, KCAT, 4>(kk, grid, st);
+  else persist_launch<WGM, WGN, WM, WN, A_KC, B_NC, KTWO, VA, VB, KCAT, 3>(kk, grid, st);
+}
 
 // the persistent kernel for one configuration; grid = the sum of the problems' padded slices
 template <int WGM, int WGN, int WM, int WN, bool KTWO>
 void persist_cfg(const GemmG& kk, dim3 grid, bool akc, bool bnc, int va, int vb, hipStream_t st) {
   if (kk.start[0] > 0) {  // K-concatenated (run_gemm_kcat checked kcat_ok)
     if constexpr (WGM == 4 && WGN == 1 && WM == 1 && WN == 1 && !KTWO)
-      hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, true, true, KTWO, 4, 4, true>), grid, dim3(256), 0,
-                         st, kk);
+      persist_launch_ns<WGM, WGN, WM, WN, true, true, KTWO, 4, 4, true>(kk, grid, st);
     return;
   }
-#define DS_PV(AK, BN_)                                                                                          \
-  if (va == 4 && vb == 4)                                                                                     \
-    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4, false>), grid, dim3(256), 0, st, kk); \
-  else if (va == 4)                                                                                           \
-    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1, false>), grid, dim3(256), 0, st, kk); \
-  else if (vb == 4)                                                                                           \
-    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 4, false>), grid, dim3(256), 0, st, kk); \
-  else                                                                                                        \
-    hipLaunchKernelGGL((gemm_f32_persist_kernel<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 1, false>), grid, dim3(256), 0, st, kk);
+#define DS_PV(AK, BN_)                                                                             \
+  if (va == 4 && vb == 4)  persist_launch_ns<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 4, false>(kk, grid, st); \
+  else if (va == 4)        persist_launch_ns<WGM, WGN, WM, WN, AK, BN_, KTWO, 4, 1, false>(kk, grid, st); \
+  else if (vb == 4)        persist_launch_ns<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 4, false>(kk, grid, st); \
+  else                     persist_launch_ns<WGM, WGN, WM, WN, AK, BN_, KTWO, 1, 1, false>(kk, grid, st);
   if (akc && bnc) { DS_PV(true, true) }
   else if (akc)   { DS_PV(true, false) }
   else if (bnc)   { DS_PV(false, true) }

@@ -43,7 +43,8 @@ for s in "${S[@]}"; do
     sweep1) run gemm_sweep1 300 python tools/gemm_sweep.py --configs auto:auto --iters 50 ;;
     gemmref) run gemm_ref 300 python tools/torch_gemm_ref.py ;;
     knobs)  echo "== knobs ($(date +%T))"; REPS=${KNOB_REPS:-2} timeout -k 10 900 bash tools/knob_sweep.sh "" "DSTAGNN_GEMM_PERSIST=1" \
-              "DSTAGNN_GEMM_PERSIST=1 DSTAGNN_GEMM_PERSIST_WPC=2" "LD_LIBRARY_PATH=$PWD/scratch/pipe3" || exit $? ;;
+              "DSTAGNN_GEMM_PERSIST=1 DSTAGNN_GEMM_PERSIST_NS=4" "DSTAGNN_GEMM_PERSIST=1 DSTAGNN_GEMM_PERSIST_WPC=2" \
+              "LD_LIBRARY_PATH=$PWD/scratch/pipe3" || exit $? ;;
     gemmlab) run gemm_lab 400 python tools/gemm_lab.py --torch-ref --rounds ${LAB_ROUNDS:-3} --variants ${LAB_VARIANTS:-base} \
                --shapes ${LAB_SHAPES:-12288x288x170:nt,12288x170x96:tt,5440x512x384:nt,5440x512x768:nt,5440x512x1536:nt,5440x192x512:tt,54400x64x96:tt,32640x64x224:tt,65280x32x960:tn,5440x512x192:tn,384x5440x512:nt,12288x170x288:tn,4096x4096x2048:tt} ;;
     *) echo "unknown step $s" ;;
