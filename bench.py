@@ -108,7 +108,8 @@ def extras(dev, steps, warmup):
 
     net = D.make_model(dev, 1, 4, 1, K, C, C, 1, tmd, pa, tmd, T, T, N, Dm, dk, dk, h)
     D.set_direct_grads(net).train()
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    from dstagnn_drought_amd.train import make_adam
+    opt = make_adam(net.parameters(), 1e-4)
     crit = torch.nn.SmoothL1Loss().to(dev)
     xm = torch.randn(B, N, 1, T, device=dev, generator=gen)
     ym = torch.randn(B, N, T, device=dev, generator=gen)

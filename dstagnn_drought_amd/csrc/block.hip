@@ -10,6 +10,7 @@
 //   X (B,N,C,T)           conv_g (B*N, 2C, T-k+1)   G (B*N, C, 3T-12)   out (B,N,C,T)
 #include <algorithm>
 #include <atomic>
+#include <vector>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -478,7 +479,17 @@ SideStream* side_stream_for_device() {
   if (!s.ok) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
-    if (hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
+    // DSTAGNN_SIDE_CUMASK=0x<32-bit pattern>: the side stream confined to the CUs the pattern
+    // selects (replicated over every 32-CU word; A/B knob: the side stream's weight-gradient
+    // GEMMs otherwise take CUs from the latency-bound main chain); no priority with a mask
+    const char* cm = getenv("DSTAGNN_SIDE_CUMASK");
+    if (cm && *cm) {
+      const uint32_t pat = (uint32_t)strtoul(cm, nullptr, 0);
+      std::vector<uint32_t> mask(8, pat);  // 256 CUs
+      if (hipExtStreamCreateWithCUMask(&s.side, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+    } else if (hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, lo) != hipSuccess) {
+      return nullptr;
+    }
     for (auto& e : s.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     s.use_flags = !events || atoi(getenv("DSTAGNN_SYNC_EVENTS")) == 2;
@@ -1183,10 +1194,11 @@ struct Bwd {
       g.C = w.dctx; g.cm = idx1(m.HV); g.cn = idx1(1);
       DS_TRY(gemm(g));
     }
+    // d res_att: dS itself (full res_att), or its sum over f (broadcast res_att, folded in the
+    // TAt backward's launch); w.dscore is the scratch either way
     float* dsc = (d.res_mode == DSTAGNN_RES_FULL && dres) ? dres : w.dscore;
-    DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, st));
-    if (d.res_mode == DSTAGNN_RES_BCAST && dres)
-      DS_TRY(op_sum_middle(w.dscore, m.B, m.F, (int64_t)m.h * m.T * m.T, dres, 0.f, st));
+    float* dsum = (d.res_mode == DSTAGNN_RES_BCAST && dres) ? dres : nullptr;
+    DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, dsum, st));
     // --- side: TAt LN gamma / beta, fc and Q|K|V weight grads (one fork)
     DS_TRY(fork());
     if (tat_part()) {
@@ -1209,10 +1221,22 @@ struct Bwd {
       g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.QW;
       g.A = w.dqkv; g.am = idx1(m.QW); g.ak = idx1(1);
       g.B = s.Wqkv; g.bk = idx1(N); g.bn = idx1(1);
-      // dU is only read (the side stream's fc weight grad also reads it): beta input C = dU,
-      // result to Cout = dE
-      g.C = w.dU; g.Cout = w.dE; g.cm = idx1(N); g.cn = idx1(1);
+      // dU is only read (the side stream's fc weight grad also reads it): beta input C = dU
+      g.C = w.dU; g.cm = idx1(N); g.cn = idx1(1);
       g.beta = 1.f;
+      if (m.first) {
+        g.Cout = w.dE;  // -> the EmbedT LayerNorm backward
+      } else if (dE_omap() && m.FT % 32 == 0) {
+        // inner block: E is x transposed, so dE accumulates straight into dx (B,N,F,T) through
+        // the output map (row (b, ft), column n -> b N FT + n FT + ft) once the side stream's
+        // Chebyshev-path gradient is in dx
+        DS_TRY(wait_side(dx_ready));
+        g.Cout = dx; g.omap = true; g.obeta = 1.f;
+        g.om = idx2(m.FT, 1, N * m.FT); g.on = idx1(m.FT);
+        return gemm(g);
+      } else {
+        g.Cout = w.dE;
+      }
       DS_TRY(gemm(g));
     }
     // dE -> dx
@@ -1238,6 +1262,15 @@ struct Bwd {
       DS_TRY(op_transpose(w.dE, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
     }
     return 0;
+  }
+
+  // DSTAGNN_DE_OMAP=1: the inner block's dE accumulated straight into dx by the GEMM's output
+  // map instead of a dE buffer + transpose_kernel.  Opt-in: measured 0.718 vs 0.711 ms/step
+  // (same box, 2 x 100 steps each) — the strided epilogue of that GEMM on the critical path
+  // costs more than the transpose launch it saves.
+  static bool dE_omap() {
+    static const bool on = getenv("DSTAGNN_DE_OMAP") && atoi(getenv("DSTAGNN_DE_OMAP")) != 0;
+    return on;
   }
 
   // [dWq; dWk; dWv] = dqkv^T E — the last product of the backward, issued on the main

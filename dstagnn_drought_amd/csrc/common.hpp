@@ -250,11 +250,15 @@ struct Gemm {
   // where emask <= 0 (a fused ReLU backward: d_pre = d_out * (out > 0))
   const float* emask = nullptr;
   float* Cout = nullptr;
+  // optional: Cout with its OWN index maps (omap; else C's), plus obeta * the old Cout value:
+  // out[om(m) + on(n)] = obeta * out[...] + (alpha AB + beta C[cm(m) + cn(n)]) — e.g. a product
+  // whose beta input is row-major but whose result accumulates into a transposed tensor
+  bool omap = false; Idx2 om, on, oz; float obeta = 0.f;
   int hot = 0;  // 1: launch under the separately named gemm_f32_hot_kernel (profiling tag)
   // optional column sums of A over k: ones_out[m * ones_stride] = alpha * sum_k A[m][k] (a bias
   // gradient folded into its weight-gradient GEMM); plain epilogue only (no beta/bias/relu/emask)
   float* ones_out = nullptr; int64_t ones_stride = 1;
-  Gemm() { am = ak = az = bk = bn = bz = cm = cn = cz = idx1(0); }
+  Gemm() { am = ak = az = bk = bn = bz = cm = cn = cz = om = on = oz = idx1(0); }
 };
 // ws: split-K partial slab scratch (may be null -> no split)
 int run_gemm(const Gemm& g, float* ws, size_t ws_floats, hipStream_t st);

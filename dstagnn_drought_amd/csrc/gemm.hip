@@ -530,6 +530,25 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   k.alpha = g.alpha; k.beta = g.beta; k.bias = g.bias; k.bias_stride = (int32_t)g.bias_stride; k.relu = g.relu;
   k.emask = g.emask ? g.emask + g.c_off : nullptr;
   k.Cout = g.Cout ? g.Cout + g.c_off : nullptr;
+  if (g.omap) {  // Cout's own maps (no c_off: an independent tensor)
+    if (!g.Cout || g.relu || g.emask || g.ones_out) {
+      set_last_error("gemm: an output map needs Cout and no ReLU / mask / column-sum epilogue");
+      return DSTAGNN_E_ARG;
+    }
+    if (g.om.two && g.om.f.d % 32 != 0) {  // gemm_epilogue: 32-row fragments in one map period
+      set_last_error("gemm: a two-level output row map needs a period that is a multiple of 32");
+      return DSTAGNN_E_ARG;
+    }
+    if (!make_kidx(g.om, g.M, &k.om) || !make_kidx(g.on, g.N, &k.on) ||
+        idx_span(g.om, g.M) + idx_span(g.on, g.N) >= (1ll << 31) || idx_min(g.om, g.M) < 0 || idx_min(g.on, g.N) < 0) {
+      set_last_error("gemm: output map offsets exceed int32");
+      return DSTAGNN_E_SHAPE;
+    }
+    k.Cout = g.Cout;
+    k.oz = make_zidx(g.oz);
+    k.omap = 1;
+    k.obeta = g.obeta;
+  }
   k.ws = ws;
 
   // optional overrides for tuning sweeps (tools/gemm_sweep.py)
@@ -547,6 +566,7 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
     else best = 0;
   }
   if (env_cfg >= 0 && env_cfg < (int)(sizeof(kCfgs) / sizeof(kCfgs[0]))) best = env_cfg;
+  if (g.omap) best = 0;  // the output-map epilogue exists in the 64x64 tile's kernels only
   const Cfg cfg = kCfgs[best];
   const int64_t blocks = cdiv64(g.M, cfg.bm()) * cdiv64(Nk, cfg.bn()) * g.batch;
 
@@ -583,7 +603,7 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   // persistent tile loop (gemm_persist_body): no split-K, no column-sum column, fp32, the 64x64 /
   // 128x32 tiles, enough tiles that a workgroup walks several; the workgroup count is set per
   // launch (persist_slices)
-  pl.persist = gemm_persist_on() && splitk == 1 && !g.ones_out && !g_bf16 && (best == 0 || best == 2) && g.K > 0 &&
+  pl.persist = gemm_persist_on() && splitk == 1 && !g.ones_out && !g.omap && !g_bf16 && (best == 0 || best == 2) && g.K > 0 &&
                (int64_t)blocks >= gemm_persist_min_tiles();
   pl.akc = !g.ak.two && g.ak.s0 == 1;
   pl.bnc = !g.bn.two && g.bn.s0 == 1;
@@ -742,7 +762,7 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
   double flops = 0, bytes = 0;
   for (int p = 0; p < n; ++p) {
     const Gemm& g = gs[p];
-    if (g.M != g0.M || g.N != g0.N || g.batch != g0.batch || g.ones_out || g.hot) {
+    if (g.M != g0.M || g.N != g0.N || g.batch != g0.batch || g.ones_out || g.hot || g.omap) {
       set_last_error("gemm kcat: segments must share M, N, batch (no column sums)");
       return DSTAGNN_E_ARG;
     }

@@ -26,6 +26,9 @@ struct GemmK {
   float* ws;  // split partials [batch][splitk][M][N]
   const float* emask;  // optional: zero where emask <= 0 (same maps as C, offset c_off)
   float* Cout;         // optional: destination instead of C (beta still reads C)
+  int omap;            // Cout has its own maps om / on / oz (Gemm::omap), obeta * old Cout added
+  float obeta;
+  KIdx om, on; ZIdx oz;
   int nstage;          // LDS pipeline stages (2 or 3; dynamic LDS)
   // optional column-sum column: N = nload + 1 and column nload of B reads as 1.0, so
   // C[m][nload] = sum_k A[m][k] (a bias gradient folded into its weight-gradient GEMM);
@@ -137,6 +140,11 @@ __device__ __forceinline__ void epilogue_store(const GemmK& g, int zb, int m, in
   if (g.bias) v += g.bias[n * g.bias_stride];
   if (g.relu) v = fmaxf(v, 0.f);
   if (g.emask) v = g.emask[zo + o] > 0.f ? v : 0.f;
+  if (g.omap) {
+    float* d = g.Cout + zoff(g.oz, zb) + koff(g.om, m) + koff(g.on, n);
+    *d = g.obeta != 0.f ? v + g.obeta * *d : v;
+    return;
+  }
   (g.Cout ? g.Cout : g.C)[zo + o] = v;
 }
 
@@ -171,7 +179,9 @@ __device__ __forceinline__ TileCoord decode_tile(const GemmK& g, uint32_t bid, u
 // multiply, one add), instead of a full koff (three 32-bit vector multiplies and a high
 // multiply) per row; split-K slab offsets likewise from one 64-bit base per accumulator.
 __device__ __forceinline__ int rrow(int r) { return (r & 3) + 8 * (r >> 2); }
-template <int WM, int WN>
+// OMAP: the output-map epilogue is compiled into the 64x64 tile's kernels only (the host plans
+// every omap product on that tile): elsewhere its registers would cost occupancy
+template <int WM, int WN, bool OMAP = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmK& g, const TileCoord& c, int wrow0, int wcol0, int lane,
                                               floatx16 (&acc)[WM][WN]) {
   const int lr = lane & 31, lk = lane >> 5;
@@ -205,6 +215,28 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK& g, const TileCoord& c
       const int32_t no = koff(g.cn, n);
       const int32_t mob = cm1 ? mb * g.cm.s0 : 0;
       auto mo = [&](int r) -> int32_t { return cm1 ? mob + rrow(r) * g.cm.s0 : koff(g.cm, mb + rrow(r)); };
+      if (OMAP && g.omap) {
+        // Cout with its own maps (no ReLU / mask here; the host keeps every 32-row fragment
+        // inside one period of a two-level row map, so row r sits at a fixed stride from the
+        // fragment's first row): beta * C and obeta * the old Cout, all loads before the
+        // first store, as below
+        const int64_t ozo = zoff(g.oz, c.zb) + koff(g.on, n) + koff(g.om, c.m0 + wrow0 + i * 32) + 4 * lk * g.om.s0;
+        float cin[16], ob[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = min(mb + rrow(r), g.M - 1);
+          cin[r] = g.beta != 0.f ? g.C[zo + (cm1 ? mob + (m - mb) * g.cm.s0 : koff(g.cm, m)) + no] : 0.f;
+          ob[r] = g.obeta != 0.f && mb + rrow(r) < g.M ? g.Cout[ozo + rrow(r) * g.om.s0] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (mb + rrow(r) >= g.M) continue;
+          float v = acc[i][j][r] * g.alpha + g.beta * cin[r];
+          if (g.bias) v += g.bias[n * g.bias_stride];
+          g.Cout[ozo + rrow(r) * g.om.s0] = v + g.obeta * ob[r];
+        }
+        continue;
+      }
       float* dst = g.Cout ? g.Cout : g.C;
       if (reads) {
         // beta * C and the ReLU mask: all 16 loads issued before the first store (the
@@ -741,7 +773,7 @@ __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   } else {
     kseg(g);
   }
-  gemm_epilogue<WM, WN>(g, tc, arow0, bcol0, lane, acc);
+  gemm_epilogue<WM, WN, WGM == 2 && WGN == 2 && WM == 1 && WN == 1 && !KCAT>(g, tc, arow0, bcol0, lane, acc);
 }
 
 // ---------------------------------------------------------------------------------

@@ -9,6 +9,7 @@
 //   gate_fwd / gate_bwd   GTU gates tanh(p)*sigmoid(q) + concat (:192-197, :242)
 //   tail_fwd / tail_bwd   fcmy dropout + residual + ReLU + LN_C (:243-252)
 //   reductions            deterministic two-stage column sums (bias / gamma / beta grads)
+#include <initializer_list>
 #include <map>
 #include <mutex>
 
@@ -72,7 +73,12 @@ struct TatArgs {
   const float* dctx;     // (B*F*T, h*dv)
   const float* dre;      // (B,F,h,T,T) or null
   float* dqkv;           // (B*F*T, 3 cols blocks)
-  float* dscore;         // (B,F,h,T,T) dS (== d res_att before f-reduction)
+  float* dscore;         // (B,F,h,T,T) dS (== d res_att before f-reduction); scratch when !keep_ds
+  // matrix-core backward only: dres_sum = sum_f dS ((B,1,h,T,T), the broadcast res_att's
+  // gradient) folded in-kernel by tickets cnt[b*h + hd] over partials in dscore
+  float* dres_sum;
+  int* cnt;
+  int keep_ds;           // write the full dS to dscore
 };
 
 // -------------------------------------------------------------------------------------
@@ -936,6 +942,248 @@ __global__ __launch_bounds__(256) void colsum2d_kernel(Colsum2dArgs a) {
   if (t == 0) __hip_atomic_store(cnt2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// =====================================================================================
+// Temporal attention on the matrix cores: T <= 16 with T % 4 == 0, d_k = d_v = 32 — the
+// production TAt (model/DSTAGNN_my.py:27-67 at T = 12, d_k = d_v = 32).  One wave per
+// (b, f, head) problem (four per workgroup); the T x T tile is padded to 16 x 16 and every
+// product is a v_mfma_f32_16x16x4_f32 chain (fragments: A[l&15][k = l>>4], B[k = l>>4][l&15],
+// D[4(l>>4) + r][l&15]) whose operands come from global memory straight into registers.
+// Each product's contraction index is assigned to (k slot q = l>>4, step s) as 4q + s, so an
+// accumulator tile whose ROW index is that contraction index is, register s for register s,
+// the next product's A operand: scores -> P -> ctx in the forward, dA -> dS -> dK / dV in the
+// backward, with one 16 x 16 LDS transpose of dS for dQ.  (The VALU wave kernels above spend
+// ~2 400 VALU and ~700 LDS instructions per problem on index arithmetic and LDS operands.)
+// =====================================================================================
+constexpr int kTmD = 32;  // d_k = d_v of the matrix-core variant
+
+__device__ __forceinline__ float xor_max_16(float v) {
+  v = fmaxf(v, __shfl_xor(v, 1, 64));
+  v = fmaxf(v, __shfl_xor(v, 2, 64));
+  v = fmaxf(v, __shfl_xor(v, 4, 64));
+  return fmaxf(v, __shfl_xor(v, 8, 64));
+}
+__device__ __forceinline__ float xor_sum_16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v + __shfl_xor(v, 8, 64);
+}
+__device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void tat_fwd_mfma_kernel(TatArgs a) {
+  static_assert(T % 4 == 0 && T <= 16, "one 16 x 16 tile, float4 rows");
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, c = l & 15, q = l >> 4;
+  const int id = blockIdx.x * kTatW + w;
+  if (id >= a.B * a.F * a.h) return;  // no barrier in this kernel
+  const int h = a.h, hd = id % h, bf = id / h, b = bf / a.F;
+  const int ld = 3 * h * kTmD;
+  const float* Qp = a.qkv + (int64_t)bf * T * ld + hd * kTmD;
+  const float* Kp = Qp + h * kTmD;
+  const float* Vp = Qp + 2 * h * kTmD;
+  const bool vi = c < T, vj = q < T / 4;
+  // ctx's B operand V[j = 4q + s][d = c + 16t] first: it does not depend on the scores
+  float vv[2][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) vv[t][s] = (4 * q + s < T) ? Vp[(int64_t)(4 * q + s) * ld + c + 16 * t] : 0.f;
+  // S^T = K Q^T: A[m = j][k = d] = K[j = c][8q + s], B[k = d][n = i] = Q[i = c][8q + s]
+  float4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0, q0 = k0, q1 = k0;
+  if (vi) {
+    k0 = *reinterpret_cast<const float4*>(Kp + (int64_t)c * ld + 8 * q);
+    k1 = *reinterpret_cast<const float4*>(Kp + (int64_t)c * ld + 8 * q + 4);
+    q0 = *reinterpret_cast<const float4*>(Qp + (int64_t)c * ld + 8 * q);
+    q1 = *reinterpret_cast<const float4*>(Qp + (int64_t)c * ld + 8 * q + 4);
+  }
+  const int64_t sbase = (int64_t)id * T * T;
+  const float* rp = nullptr;
+  if (a.res_mode == DSTAGNN_RES_BCAST) rp = a.res + ((int64_t)b * h + hd) * T * T;
+  else if (a.res_mode == DSTAGNN_RES_FULL) rp = a.res + sbase;
+  float4 rr = {0.f, 0.f, 0.f, 0.f};
+  if (rp && vi && vj) rr = *reinterpret_cast<const float4*>(rp + c * T + 4 * q);
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = mfma16(k0.x, q0.x, acc);
+  acc = mfma16(k0.y, q0.y, acc);
+  acc = mfma16(k0.z, q0.z, acc);
+  acc = mfma16(k0.w, q0.w, acc);
+  acc = mfma16(k1.x, q1.x, acc);
+  acc = mfma16(k1.y, q1.y, acc);
+  acc = mfma16(k1.z, q1.z, acc);
+  acc = mfma16(k1.w, q1.w, acc);
+  // lane (c, q) holds S[i = c][j = 4q + r]
+  const float rv[4] = {rr.x, rr.y, rr.z, rr.w};
+  float sc[4], p[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    sc[r] = acc[r] * a.scale;
+    sc[r] += rv[r];
+  }
+  if (vi && vj) *reinterpret_cast<float4*>(a.re_at + sbase + c * T + 4 * q) = make_float4(sc[0], sc[1], sc[2], sc[3]);
+  // softmax over the query axis i = the 16 lanes c of this quarter (column j = 4q + r)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float m = xor_max_16(vi ? sc[r] : -INFINITY);
+    const float e = vi ? __expf(sc[r] - m) : 0.f;
+    const float inv = 1.f / xor_sum_16(e);
+    p[r] = vj ? e * inv : 0.f;
+  }
+  if (vi && vj) *reinterpret_cast<float4*>(a.att + sbase + c * T + 4 * q) = make_float4(p[0], p[1], p[2], p[3]);
+  // ctx = P V: A[m = i][k = j] = P[i = c][j = 4q + s] = p[s], B = vv
+  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    c0 = mfma16(p[s], vv[0][s], c0);
+    c1 = mfma16(p[s], vv[1][s], c1);
+  }
+  const int ldc = h * kTmD;
+  float* cb = a.ctx + (int64_t)bf * T * ldc + hd * kTmD + c;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * q + r;
+    if (i < T) {
+      cb[(int64_t)i * ldc] = c0[r];
+      cb[(int64_t)i * ldc + 16] = c1[r];
+    }
+  }
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void tat_bwd_mfma_kernel(TatArgs a) {
+  static_assert(T % 4 == 0 && T <= 16, "one 16 x 16 tile");
+  __shared__ float tr[kTatW][16][17];  // per-wave dS transpose (dQ's A operand)
+  __shared__ float red[kTatW][T * T];  // F-sum: the workgroup's four dS tiles
+  __shared__ int last;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, c = l & 15, q = l >> 4;
+  const int h = a.h, P = a.B * a.F * h;
+  const int nch = a.F / kTatW;
+  int id;
+  if (a.dres_sum) {  // workgroup = (b, head, four consecutive f): wave w takes f = 4 ch + w
+    const int bh = blockIdx.x / nch, ch = blockIdx.x - bh * nch;
+    id = ((bh / h) * a.F + ch * kTatW + w) * h + bh % h;
+  } else {
+    id = blockIdx.x * kTatW + w;
+  }
+  const bool live = id < P;
+  const int hd = id % h, bf = id / h;
+  const int ld = 3 * h * kTmD, ldc = h * kTmD;
+  const float* Qp = a.qkv + (int64_t)bf * T * ld + hd * kTmD;
+  const float* Kp = Qp + h * kTmD;
+  const float* Vp = Qp + 2 * h * kTmD;
+  const float* Cp = a.dctx + (int64_t)bf * T * ldc + hd * kTmD;
+  const int64_t sbase = (int64_t)id * T * T;
+  const bool vj = c < T;  // lane column j = c; rows i = 4q + r
+  // every load up front: dA's operands dC[i = c][8q + s] / V[j = c][8q + s]; the B operands
+  // [4q + s][c + 16t] of dV (dC), dK (Q) and dQ (K); A[i = 4q + r][j = c] and d re_At
+  float4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0, v0 = d0, v1 = d0;
+  float cb[2][4], qb[2][4], kb[2][4], at[4], dr[4];
+  if (live && vj) {
+    d0 = *reinterpret_cast<const float4*>(Cp + (int64_t)c * ldc + 8 * q);
+    d1 = *reinterpret_cast<const float4*>(Cp + (int64_t)c * ldc + 8 * q + 4);
+    v0 = *reinterpret_cast<const float4*>(Vp + (int64_t)c * ld + 8 * q);
+    v1 = *reinterpret_cast<const float4*>(Vp + (int64_t)c * ld + 8 * q + 4);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int i = 4 * q + s;
+    const bool ok = live && i < T;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      cb[t][s] = ok ? Cp[(int64_t)i * ldc + c + 16 * t] : 0.f;
+      qb[t][s] = ok ? Qp[(int64_t)i * ld + c + 16 * t] : 0.f;
+      kb[t][s] = ok ? Kp[(int64_t)i * ld + c + 16 * t] : 0.f;
+    }
+    at[s] = ok && vj ? a.att[sbase + i * T + c] : 0.f;
+    dr[s] = ok && vj && a.dre ? a.dre[sbase + i * T + c] : 0.f;
+  }
+  // dA = dC V^T: D[m = i][n = j], A[m = i][k = d] = dC[i = c][8q + s], B[k = d][n = j] = V[j = c][8q + s]
+  floatx4 dA = {0.f, 0.f, 0.f, 0.f};
+  dA = mfma16(d0.x, v0.x, dA);
+  dA = mfma16(d0.y, v0.y, dA);
+  dA = mfma16(d0.z, v0.z, dA);
+  dA = mfma16(d0.w, v0.w, dA);
+  dA = mfma16(d1.x, v1.x, dA);
+  dA = mfma16(d1.y, v1.y, dA);
+  dA = mfma16(d1.z, v1.z, dA);
+  dA = mfma16(d1.w, v1.w, dA);
+  // column softmax backward over i (this lane's four rows, then the quarters): dS = A (dA - sum_i A dA) + d re_At
+  float cs = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) cs = fmaf(at[r], dA[r], cs);
+  cs = xor_sum_1632(cs);
+  float ds[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ds[r] = at[r] * (dA[r] - cs) + dr[r];
+  if (a.keep_ds && live && vj) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * q + r < T) a.dscore[sbase + (4 * q + r) * T + c] = ds[r];
+  }
+  // dV = A^T dC and dK = dS^T Q: A operand [m = j = c][k = i = 4q + s] = at[s] / ds[s]
+  floatx4 z = {0.f, 0.f, 0.f, 0.f};
+  floatx4 gv0 = z, gv1 = z, gk0 = z, gk1 = z, gq0 = z, gq1 = z;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    gv0 = mfma16(at[s], cb[0][s], gv0);
+    gv1 = mfma16(at[s], cb[1][s], gv1);
+    gk0 = mfma16(ds[s], qb[0][s], gk0);
+    gk1 = mfma16(ds[s], qb[1][s], gk1);
+  }
+  // dQ = dS K: A operand [m = i = c][k = j = 4q + s] = dS[c][4q + s], through LDS
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tr[w][4 * q + r][c] = ds[r];
+  if (a.dres_sum && vj) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * q + r < T) red[w][(4 * q + r) * T + c] = ds[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float x = tr[w][c][4 * q + s];
+    gq0 = mfma16(x, kb[0][s], gq0);
+    gq1 = mfma16(x, kb[1][s], gq1);
+  }
+  if (live) {
+    float* db = a.dqkv + (int64_t)bf * T * ld + hd * kTmD + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * q + r;
+      if (i >= T) continue;
+      float* row = db + (int64_t)i * ld;
+      row[0] = gq0[r] * a.scale;
+      row[16] = gq1[r] * a.scale;
+      row[h * kTmD] = gk0[r] * a.scale;
+      row[h * kTmD + 16] = gk1[r] * a.scale;
+      row[2 * h * kTmD] = gv0[r];
+      row[2 * h * kTmD + 16] = gv1[r];
+    }
+  }
+  if (!a.dres_sum) return;
+  // res_att gradient sum_f dS (deterministic): the four tiles in wave order, one partial per
+  // workgroup (sc1 stores, drained, barrier), a ticket per (b, head); the last of its nch
+  // workgroups acquires and adds the partials in chunk order (colsum2d's hand-off)
+  const int t = threadIdx.x, bh = blockIdx.x / nch, ch = blockIdx.x - bh * nch;
+  float* part = a.dscore + (int64_t)bh * nch * T * T;
+  if (t < T * T) st_agent(part + (int64_t)ch * T * T + t, ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    last = atomicAdd(a.cnt + bh, 1) == nch - 1;
+    if (last) {
+      colsum_acquire();
+      __hip_atomic_store(a.cnt + bh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+  }
+  __syncthreads();
+  if (!last || t >= T * T) return;
+  float v = 0.f;
+  for (int k = 0; k < nch; ++k) v += ld_agent(part + (int64_t)k * T * T + t);
+  a.dres_sum[(int64_t)bh * T * T + t] = v;
+}
+
 // out[a][i] = beta*out + sum_m in[a][m][i]; grid (i blocks, a)
 // out[a][i] = beta*out[a][i] + sum_m in[a][m][i]: a workgroup owns 32 consecutive i of one a;
 // its 8 wave-quarters sum interleaved m (8-way parallel chains per output instead of one
@@ -1268,6 +1516,25 @@ static int allow_lds(const void* kernel, size_t bytes) {
   return 0;
 }
 
+// the matrix-core TAt kernels: T in {4, 8, 12, 16}, d_k = d_v = 32, 16-B aligned operands
+// (float4 rows); DSTAGNN_TAT_MFMA=0 keeps the VALU wave kernels (A/B switch)
+static bool tat_mfma_ok(int T, int dk, int dv, std::initializer_list<const float*> ptrs) {
+  static const bool off = getenv("DSTAGNN_TAT_MFMA") && atoi(getenv("DSTAGNN_TAT_MFMA")) == 0;
+  if (off || dk != kTmD || dv != kTmD || T % 4 != 0 || T < 4 || T > 16) return false;
+  for (const float* p : ptrs)
+    if (reinterpret_cast<uintptr_t>(p) % 16 != 0) return false;
+  return true;
+}
+static void launch_tat_bwd_mfma(const TatArgs& a, dim3 grid, hipStream_t st) {
+  const dim3 blk(64 * kTatW);
+  switch (a.T) {
+    case 4: hipLaunchKernelGGL(tat_bwd_mfma_kernel<4>, grid, blk, 0, st, a); break;
+    case 8: hipLaunchKernelGGL(tat_bwd_mfma_kernel<8>, grid, blk, 0, st, a); break;
+    case 12: hipLaunchKernelGGL(tat_bwd_mfma_kernel<12>, grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(tat_bwd_mfma_kernel<16>, grid, blk, 0, st, a); break;
+  }
+}
+
 static size_t tat_fwd_lds(int T, int dk, int dv) {
   return sizeof(float) * (size_t)(2 * T * (dk + 1) + T * (dv + 1) + T * T);
 }
@@ -1282,6 +1549,17 @@ int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
   a.qkv = qkv; a.res = res; a.res_mode = res ? res_mode : 0; a.scale = 1.f / sqrtf((float)dk);
   a.re_at = re_at; a.att = att; a.ctx = ctx;
   const int P = B * F * h;
+  if (tat_mfma_ok(T, dk, dv, {qkv, res, re_at, att})) {
+    const dim3 grid((unsigned)cdiv64(P, kTatW)), blk(64 * kTatW);
+    switch (T) {
+      case 4: hipLaunchKernelGGL(tat_fwd_mfma_kernel<4>, grid, blk, 0, st, a); break;
+      case 8: hipLaunchKernelGGL(tat_fwd_mfma_kernel<8>, grid, blk, 0, st, a); break;
+      case 12: hipLaunchKernelGGL(tat_fwd_mfma_kernel<12>, grid, blk, 0, st, a); break;
+      default: hipLaunchKernelGGL(tat_fwd_mfma_kernel<16>, grid, blk, 0, st, a); break;
+    }
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   if (T <= 16 && (size_t)kTatW * tat_wave_fwd_floats(T, dk, dv) * sizeof(float) <= 64 * 1024) {
     hipLaunchKernelGGL(tat_fwd_wave_kernel, dim3((unsigned)cdiv64(P, kTatW)), dim3(64 * kTatW),
                        (size_t)kTatW * tat_wave_fwd_floats(T, dk, dv) * sizeof(float), st, a);
@@ -1310,12 +1588,35 @@ int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, con
 }
 
 int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
-               const float* dre, float* dqkv, float* dscore, hipStream_t st) {
+               const float* dre, float* dqkv, float* dscore, float* dres_sum, hipStream_t st) {
+  if (dres_sum) {  // the full dS is scratch; the output is its sum over f
+    if (tat_mfma_ok(T, dk, dv, {qkv, att, dctx, dre}) && F % kTatW == 0) {
+      int* cnt = stream_counters(st, B * h);
+      if (cnt) {
+        TatArgs a{};
+        a.B = B; a.F = F; a.T = T; a.h = h; a.dk = dk; a.dv = dv;
+        a.qkv = qkv; a.att = const_cast<float*>(att); a.scale = 1.f / sqrtf((float)dk);
+        a.dctx = dctx; a.dre = dre; a.dqkv = dqkv; a.dscore = dscore;
+        a.dres_sum = dres_sum; a.cnt = cnt; a.keep_ds = 0;
+        launch_tat_bwd_mfma(a, dim3((unsigned)(B * h * (F / kTatW))), st);
+        DS_CHECK_LAUNCH();
+        return 0;
+      }
+    }
+    DS_TRY(op_tat_bwd(B, F, T, h, dk, dv, qkv, att, dctx, dre, dqkv, dscore, nullptr, st));
+    return op_sum_middle(dscore, B, F, (int64_t)h * T * T, dres_sum, 0.f, st);
+  }
   TatArgs a{};
   a.B = B; a.F = F; a.T = T; a.h = h; a.dk = dk; a.dv = dv;
   a.qkv = qkv; a.att = const_cast<float*>(att); a.scale = 1.f / sqrtf((float)dk);
   a.dctx = dctx; a.dre = dre; a.dqkv = dqkv; a.dscore = dscore;
+  a.keep_ds = 1;
   const int P = B * F * h;
+  if (tat_mfma_ok(T, dk, dv, {qkv, att, dctx, dre})) {
+    launch_tat_bwd_mfma(a, dim3((unsigned)cdiv64(P, kTatW)), st);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   if (T <= 16 && (size_t)kTatW * tat_wave_bwd_floats(T, dk, dv) * sizeof(float) <= 64 * 1024) {
     hipLaunchKernelGGL(tat_bwd_wave_kernel, dim3((unsigned)cdiv64(P, kTatW)), dim3(64 * kTatW),
                        (size_t)kTatW * tat_wave_bwd_floats(T, dk, dv) * sizeof(float), st, a);

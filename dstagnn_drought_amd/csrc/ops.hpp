@@ -231,7 +231,7 @@ int op_transpose(const float* in, float* out, int R, int Cc, int batch, int64_t 
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st);
 int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
-               const float* dre, float* dqkv, float* dscore, hipStream_t st);
+               const float* dre, float* dqkv, float* dscore, float* dres_sum, hipStream_t st);
 int op_ln_fwd(const LnFwd& a, hipStream_t st);
 int op_ln_bwd(const LnBwd& a, hipStream_t st);
 // zero-armed int tickets private to (current device, stream); nullptr if unavailable

@@ -181,12 +181,23 @@ def params_path_of(config, root='myexperiments'):
     return os.path.join(root, config['Data']['dataset_name'], folder_dir)
 
 
+def make_adam(params, lr):
+    """torch.optim.Adam (train_DSTAGNN_my.py:126) — the single-launch fused implementation when
+    every parameter is on the GPU (one kernel over all tensors instead of the multi-tensor
+    foreach chain); DSTAGNN_ADAM_FUSED=0 keeps the default implementation."""
+    params = list(params)
+    fused = os.environ.get("DSTAGNN_ADAM_FUSED", "1") != "0" and params and all(p.is_cuda for p in params)
+    if fused:
+        return torch.optim.Adam(params, lr=lr, fused=True)
+    return torch.optim.Adam(params, lr=lr)
+
+
 def fit(net, train_x, train_y, val_x, val_y, *, epochs, start_epoch=0, batch_size, lr, params_path,
         double_step=True, max_batches=None, log=print):
     """The epoch loop of train_DSTAGNN_my.py:136-178.  Returns (best_epoch, best_val, history)."""
     rank, world = _world()
     criterion = nn.SmoothL1Loss().to(train_x.device)
-    optimizer = torch.optim.Adam(net.parameters(), lr=lr)
+    optimizer = make_adam(net.parameters(), lr)
     reducer = None
     if world > 1:  # block gradients all-reduced beside the backward (attach)
         reducer = GradAllReducer(net.named_parameters(), mask_support=mask_support_of(net)).attach(net)

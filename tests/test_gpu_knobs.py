@@ -1,0 +1,42 @@
+"""GPU: the opt-in / A-B paths that the default run does not take, each held to the fp64 oracle in
+a subprocess (the library reads its switches once per process):
+
+  DSTAGNN_DE_OMAP=1    the inner block's dE accumulated into dx by the GEMM output-map epilogue
+                       (block.hip stage_tat) instead of a dE buffer + transpose_kernel
+  DSTAGNN_TAT_MFMA=0   the VALU wave kernels of the temporal attention instead of the
+                       matrix-core ones (ops.hip tat_*_mfma_kernel)
+  DSTAGNN_SIDE_CUMASK  the side stream confined to a CU subset (scheduling only: same results)
+
+PEMS08 geometry (the bench's default path otherwise), inner block with a broadcast res_att,
+eval and train mode, same bounds as tests/test_gpu_parity.py::test_block_vs_oracle_configs."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+SCRIPT = """
+import sys
+sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
+import test_gpu_parity as T
+T._run_config_vs_oracle("pems08", False, 4)
+T._run_config_vs_oracle("pems08", False, 4, train=True)
+print("KNOB_OK")
+"""
+
+
+@pytest.mark.parametrize("env", ["DSTAGNN_DE_OMAP=1", "DSTAGNN_TAT_MFMA=0", "DSTAGNN_SIDE_CUMASK=0x11111111"])
+def test_knob_path_vs_oracle(env):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    k, v = env.split("=", 1)
+    e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    e[k] = v
+    code = SCRIPT.format(root=ROOT, tests=os.path.join(ROOT, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=e, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0 and "KNOB_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

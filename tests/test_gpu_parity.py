@@ -367,6 +367,9 @@ CONFIGS = {
     # K = 3 at a long series: the aggregate-first backward's LDS image (16 K F T bytes = 221 KB)
     # does not fit, so cheb_agg_ok sends the block down the Theta-first sparse path
     "t144k3": (48, 144, 3, 2, 64, 32, 32),
+    # T = 8 / 16 with d_k = 32: the other tile fills of the matrix-core TAt kernels (T = 12 above)
+    "t8": (40, 8, 3, 2, 64, 32, 32),
+    "t16": (40, 16, 3, 2, 64, 32, 32),
 }
 RELU_EPS = 1e-5  # ReLU decisions may differ from the fp64 oracle's only where |z| <= RELU_EPS * max|z|
 
@@ -522,7 +525,8 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
     # forced on at PEMS07 (N = 883, streamed) and forced off at small and large N, so both
     # paths are held to the oracle everywhere
     ("pems07", False, 2, True), ("pems08", False, 4, False), ("pems08", True, 2, False), ("pems04", False, 2, False),
-    ("t24", False, 2, False), ("gambia", False, 1, False), ("t144k3", False, 2, None), ("t144k3", True, 1, None)])
+    ("t24", False, 2, False), ("gambia", False, 1, False), ("t144k3", False, 2, None), ("t144k3", True, 1, None),
+    ("t8", False, 3, None), ("t16", False, 2, None), ("t16", True, 2, None)])
 def test_block_vs_oracle_configs(name, first, B, flash):
     """Held against the oracle evaluated in float64 (pems08 at B=32: the bench configuration
     itself).  Bound per tensor: the stated 1e-4 (scaled by max(1, max|ref|)), or twice the

@@ -25,7 +25,7 @@ echo "steps: $STEPS"
 IFS=',' read -ra S <<< "$STEPS"
 for s in "${S[@]}"; do
   case $s in
-    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 180 --timeout-method thread ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu --maxfail=8 -q -rf --timeout 180 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
@@ -42,9 +42,10 @@ for s in "${S[@]}"; do
     sweep)  run gemm_sweep 600 python tools/gemm_sweep.py ;;
     sweep1) run gemm_sweep1 300 python tools/gemm_sweep.py --configs auto:auto --iters 50 ;;
     gemmref) run gemm_ref 300 python tools/torch_gemm_ref.py ;;
-    knobs)  echo "== knobs ($(date +%T))"; REPS=${KNOB_REPS:-2} timeout -k 10 900 bash tools/knob_sweep.sh "" "DSTAGNN_GEMM_PERSIST=1" \
-              "DSTAGNN_GEMM_PERSIST=1 DSTAGNN_GEMM_PERSIST_NS=4" "DSTAGNN_GEMM_PERSIST=1 DSTAGNN_GEMM_PERSIST_WPC=2" \
-              "LD_LIBRARY_PATH=$PWD/scratch/pipe3" || exit $? ;;
+    knobs)  echo "== knobs ($(date +%T))"
+            # KNOB_LIST: ';'-separated env sets ("" = default), e.g. ';DSTAGNN_TAT_MFMA=0'
+            IFS=';' read -ra KL <<< "${KNOB_LIST:-;DSTAGNN_TAT_MFMA=0;DSTAGNN_DE_TRANSPOSE=1}"
+            REPS=${KNOB_REPS:-2} timeout -k 10 900 bash tools/knob_sweep.sh "${KL[@]}" || exit $? ;;
     gemmlab) run gemm_lab 400 python tools/gemm_lab.py --torch-ref --rounds ${LAB_ROUNDS:-3} --variants ${LAB_VARIANTS:-base} \
                --shapes ${LAB_SHAPES:-12288x288x170:nt,12288x170x96:tt,5440x512x384:nt,5440x512x768:nt,5440x512x1536:nt,5440x192x512:tt,54400x64x96:tt,32640x64x224:tt,65280x32x960:tn,5440x512x192:tn,384x5440x512:nt,12288x170x288:tn,4096x4096x2048:tt} ;;
     *) echo "unknown step $s" ;;
