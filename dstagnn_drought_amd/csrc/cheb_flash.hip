@@ -356,9 +356,14 @@ unsigned grid_waves(int64_t waves) { return (unsigned)cdiv64(waves, 4); }
 // gradient needs no score recomputation at all.
 // ---------------------------------------------------------------------------------------
 constexpr int kSmallN = 512;         // <= 16 tiles: <= kSmallTPW per wave
-constexpr int kXs = 36;              // LDS row stride (floats) of a staged (N, 32) operand: 16-B rows
+// a staged (N, 32) operand sits in LDS as dense 128-B rows whose 16-B quads are XOR-swizzled by
+// (row & 7): a row-quad read by 8 consecutive rows (the S operand) and a column read of 32
+// lanes in one row (the P X product, the sparse term) are both conflict-free without a pad
+// column (36-float rows took 12 % more LDS: 3 workgroups per CU instead of 5)
+__device__ __forceinline__ int xo(int row, int col) { return row * 32 + ((((col >> 2) ^ row) & 7) << 2) + (col & 3); }
+constexpr int kRedF = 4 * 32 * 33;   // the waves' 32 x 32 partials, aliased on the staged rows after use
 constexpr int kStripE = 512;         // sparse entries of one strip staged in LDS (else read from HBM); 512: the
-                                     // PEMS08 backward fits 3 workgroups per CU (50 KB of LDS each, 54 at 1024)
+                                     // PEMS08 backward fits 5 workgroups per CU (30 KB of LDS each)
 
 // forward: lse_j, P and W = T o P on the T support, P on the A_pa support, for one
 // (b, k, 32-column strip).  The strip's P tile goes through LDS ((32 nt) x 33 floats, dynamic).
@@ -460,14 +465,15 @@ __device__ __forceinline__ void stage_rows(const float* src, int64_t ld, int N, 
 #pragma unroll
   for (int u = 0; u < kIt; ++u) {
     const int e = threadIdx.x + 256 * u, row = e >> 3, c4 = (e & 7) * 4;
-    if (row < NP) *reinterpret_cast<float4*>(X + row * kXs + c4) = v[u];
+    if (row < NP) *reinterpret_cast<float4*>(X + xo(row, c4)) = v[u];
   }
 }
 
-__device__ __forceinline__ void lds16(const float* p, float (&v)[16]) {
+// 16 floats of staged row `row` from column c0 (a multiple of 16)
+__device__ __forceinline__ void lds16(const float* X, int row, int c0, float (&v)[16]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+    const float4 t = *reinterpret_cast<const float4*>(X + xo(row, c0 + 4 * q));
     v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
   }
 }
@@ -479,10 +485,12 @@ __device__ __forceinline__ void lds16(const float* p, float (&v)[16]) {
 // strip's support (CSC for dK', CSR with the CSR-ordered dzs_r for dQ').
 //   dK'_j = s (sum_{i in supp(j)} dzs_ij Q'_i - c_j sum_i P_ij Q'_i)
 //   dQ'_i = s (sum_{j in supp_row(i)} dzs_ij K'_j - sum_j P_ij c_j K'_j)
-template <int kSmallTiles>
-__global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
-  extern __shared__ float X[];  // [(32 nt)][kXs] operand rows, then lse [32 nt], c [32 nt] (dQ)
-  __shared__ float red[4][32][33];
+// WPE: the register budget as waves per SIMD (4: no spill; 5: 5 workgroups per CU — the PEMS08
+// grid of 1 152 workgroups in one round — at ~22 spilled dwords per lane; DSTAGNN_FLASH_DQK_WPE);
+// 1 (no constraint) for 3 / 4 tiles per wave
+template <int kSmallTiles, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void flash_small_dqk_kernel(ChebFl a) {
+  extern __shared__ float X[];  // [(32 nt)][32] operand rows (>= kRedF floats), then lse [32 nt], c [32 nt] (dQ)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const int nt = (a.N + 31) >> 5, NP = nt * 32;
   const int64_t half = (int64_t)a.B * a.K * nt;
@@ -496,7 +504,8 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
   const float* lseb = a.lse + (int64_t)bk * a.N;
   const float* cb = a.cc + (int64_t)bk * a.N;
   const int64_t zb = (int64_t)bk * a.nnz;
-  float* Ls = X + NP * kXs;
+  float* Ls = X + max(NP * 32, kRedF);
+  float (*red)[32][33] = reinterpret_cast<float (*)[32][33]>(X);  // after the last read of the rows
   float* Cs = Ls + NP;
   float* Ed = Cs + NP;                            // the strip's sparse entries: dzs values ...
   int* Ec = reinterpret_cast<int*>(Ed + kStripE);  // ... and their staged-row indices
@@ -573,7 +582,7 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
     const int tt = w + 4 * q;  // the contraction's tile: columns j (dQ) / rows i (dK)
     if (tt >= nt) break;
     float av[16];
-    lds16(X + (tt * 32 + l32) * kXs + h * 16, av);
+    lds16(X, tt * 32 + l32, h * 16, av);
     floatx16 S = zero16();
 #pragma unroll
     for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], S, 0, 0, 0);
@@ -592,8 +601,24 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
     // O[m = strip row][n = d] += sum over the tile's 32 entries of pv x (staged row)[d]
 #pragma unroll
     for (int s = 0; s < 16; ++s)
-      O = __builtin_amdgcn_mfma_f32_32x32x2f32(pv[s], X[(tt * 32 + frag_row(s, h)) * kXs + l32], O, 0, 0, 0);
+      O = __builtin_amdgcn_mfma_f32_32x32x2f32(pv[s], X[xo(tt * 32 + frag_row(s, h), l32)], O, 0, 0, 0);
   }
+  // the sparse term (the last reads of the staged rows), then the partials over the rows
+  float sp[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = st * 32 + (threadIdx.x >> 5) + 8 * u;
+    float v = 0.f;
+    if (row < a.N) {
+      if (staged) {
+        for (int p = pb[u] - sbeg; p < pe[u] - sbeg; ++p) v = fmaf(Ed[p], X[xo(Ec[p], d)], v);
+      } else {
+        for (int p = pb[u]; p < pe[u]; ++p) v = fmaf(edz[p], X[xo(eidx[p], d)], v);
+      }
+    }
+    sp[u] = v;
+  }
+  __syncthreads();
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[w][frag_row(r, h)][l32] = O[r];
   __syncthreads();
@@ -602,14 +627,8 @@ __global__ __launch_bounds__(256) void flash_small_dqk_kernel(ChebFl a) {
     const int rl = (threadIdx.x >> 5) + 8 * u, row = st * 32 + rl;
     if (row >= a.N) continue;
     const float dense = (red[0][rl][d] + red[1][rl][d]) + (red[2][rl][d] + red[3][rl][d]);
-    float sp = 0.f;
-    if (staged) {
-      for (int p = pb[u] - sbeg; p < pe[u] - sbeg; ++p) sp = fmaf(Ed[p], X[Ec[p] * kXs + d], sp);
-    } else {
-      for (int p = pb[u]; p < pe[u]; ++p) sp = fmaf(edz[p], X[eidx[p] * kXs + d], sp);
-    }
-    if (dq) a.dqk[((int64_t)b * a.N + row) * a.ld + k * 32 + d] = (sp - dense) * a.scale;
-    else a.dqk[((int64_t)b * a.N + row) * a.ld + a.kd + k * 32 + d] = (sp - cb[row] * dense) * a.scale;
+    if (dq) a.dqk[((int64_t)b * a.N + row) * a.ld + k * 32 + d] = (sp[u] - dense) * a.scale;
+    else a.dqk[((int64_t)b * a.N + row) * a.ld + a.kd + k * 32 + d] = (sp[u] - cb[row] * dense) * a.scale;
   }
 }
 
@@ -756,13 +775,24 @@ int op_flash_colc(const ChebFl& a, hipStream_t st) {
 int op_flash_dqk(const ChebFl& a, hipStream_t st) {
   const int nt = (a.N + 31) >> 5;
   if (a.am) {  // small graphs (flash_small): dK' and dQ' strips in one launch
-    const size_t lds = ((size_t)nt * 32 * kXs + 2 * (size_t)nt * 32 + 2 * (size_t)kStripE) * sizeof(float);
+    const size_t lds = (std::max<size_t>((size_t)nt * 32 * 32, kRedF) + 2 * (size_t)nt * 32 + 2 * (size_t)kStripE) *
+                       sizeof(float);
     const dim3 grid((unsigned)(2 * (int64_t)a.B * a.K * nt));
+    static const bool wpe5 = getenv("DSTAGNN_FLASH_DQK_WPE") && atoi(getenv("DSTAGNN_FLASH_DQK_WPE")) == 5;
     switch ((nt + 3) / 4) {  // tiles per wave
-#define DS_DQK(T) case T: DS_TRY(allow_lds(flash_small_dqk_kernel<T>, lds)); \
-      hipLaunchKernelGGL(flash_small_dqk_kernel<T>, grid, dim3(256), lds, st, a); break;
-      DS_DQK(1) DS_DQK(2) DS_DQK(3) DS_DQK(4)
+#define DS_DQK(T) case T: \
+      if (wpe5) { DS_TRY(allow_lds(flash_small_dqk_kernel<T, 5>, lds)); \
+                  hipLaunchKernelGGL((flash_small_dqk_kernel<T, 5>), grid, dim3(256), lds, st, a); } \
+      else { DS_TRY(allow_lds(flash_small_dqk_kernel<T, 4>, lds)); \
+             hipLaunchKernelGGL((flash_small_dqk_kernel<T, 4>), grid, dim3(256), lds, st, a); } \
+      break;
+      DS_DQK(1) DS_DQK(2)
 #undef DS_DQK
+      // 3 / 4 tiles per wave (N > 256): the register budget of 4 or 5 waves would spill
+      case 3: DS_TRY(allow_lds(flash_small_dqk_kernel<3, 1>, lds));
+        hipLaunchKernelGGL((flash_small_dqk_kernel<3, 1>), grid, dim3(256), lds, st, a); break;
+      case 4: DS_TRY(allow_lds(flash_small_dqk_kernel<4, 1>, lds));
+        hipLaunchKernelGGL((flash_small_dqk_kernel<4, 1>), grid, dim3(256), lds, st, a); break;
       default: set_last_error("flash: graph too large for the small-graph kernels"); return DSTAGNN_E_SHAPE;
     }
     DS_CHECK_LAUNCH();

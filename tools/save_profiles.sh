@@ -32,7 +32,11 @@ for c in GAMBIA SYN; do
   t=$(ls gpurun_out/trace_cfg_$c/*kernel_trace.csv gpurun_out/trace_cfg_$c/*/*kernel_trace.csv 2>/dev/null | head -1)
   [ -n "$f" ] && cp "$f" "profiles/${R}_${lc}_kernel_stats.csv"
   [ -n "$t" ] && { hdr; python3 tools/trace_by_grid.py "$t" 30; } > "profiles/${R}_${lc}_kernels_by_grid.txt"
+  # one step of the normal two-stream run: which stream ends the step
+  [ -n "$t" ] && { hdr; python3 tools/step_timeline.py "$t" 1; } > "profiles/${R}_${lc}_step_timeline.txt" 2>&1
 done
+[ -f gpurun_out/prof/run_kernel_trace.csv ] && { hdr; python3 tools/step_timeline.py gpurun_out/prof/run_kernel_trace.csv; } \
+  > "profiles/${R}_step_timeline_under_rocprof.txt" 2>&1
 [ -f gpurun_out/trace_final/step_kernels.txt ] && { hdr; cat gpurun_out/trace_final/step_kernels.txt; } > "profiles/${R}_step_kernels.txt"
 if [ -f gpurun_out/pmcb_summary.txt ]; then
   { echo "# build (measured): $(cat gpurun_out/pmcb/build.json 2>/dev/null)  git: $HEAD"; cat gpurun_out/pmcb_summary.txt; } > "profiles/${R}_step_sq_pmc.txt"
