@@ -80,9 +80,12 @@ constexpr int gather_wpe() {
   return kNQ >= 12 ? 2 : (agg_prefetch<kNQ>() ? 2 : 1) * kE * kNQ + KM * kNQ + 40 <= 110 ? 4
        : ((agg_prefetch<kNQ>() ? 2 : 1) * kE * kNQ + KM * kNQ + 40 <= 125 ? 3 : 2);
 }
-template <int kNQ, int KM>
+template <int kNQ, int KM, bool PF = agg_prefetch<kNQ>()>
 constexpr int sddmm_wpe() {
-  return KM <= 3 && (agg_prefetch<kNQ>() ? 2 : 1) * kE * kNQ + 16 + KM * kNQ + 64 <= 150 ? 3 : 2;
+  // without the batch prefetch (PF false, DSTAGNN_SDDMM_NOPF=1): one batch of rows fewer in
+  // registers -> PEMS08's <6, 3> fits 4 waves (more resident waves instead of the prefetch)
+  return !PF && kNQ <= 6 && KM <= 3 ? 4
+       : (KM <= 3 && (PF ? 2 : 1) * kE * kNQ + 16 + KM * kNQ + 64 <= 150 ? 3 : 2);
 }
 constexpr int kAs = 33;    // LDS row stride of a 32 x 32 operand tile
 
@@ -203,8 +206,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<
 // with all K: dW_k[i, j] = <x_i, dagg_k> (flash path: the softmax backward's support terms
 // dzs = P T dW and c_j instead, as cheb_sparse.hip).
 // ---------------------------------------------------------------------------------------
-template <int kNQ, int KM>  // kNQ >= min(F*T, 1024) / 64
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<kNQ, KM>(), 8))) void cheb_agg_sddmm_kernel(ChebAg a) {
+template <int kNQ, int KM, bool PF = agg_prefetch<kNQ>()>  // kNQ >= min(F*T, 1024) / 64
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<kNQ, KM, PF>(), 8))) void cheb_agg_sddmm_kernel(ChebAg a) {
   extern __shared__ float Dg[];  // [waves][K][F * T]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
@@ -272,10 +275,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<k
       }
     };
     float v[kE][kNQ];
-    if constexpr (agg_prefetch<kNQ>()) gather(0, 0, v);
+    if constexpr (PF) gather(0, 0, v);
     for (int e0 = 0; e0 < nc; e0 += kE) {
       float vn[kE][kNQ];
-      if constexpr (agg_prefetch<kNQ>()) gather(e0 + kE, 0, vn);  // the next batch's first element range, in flight meanwhile
+      if constexpr (PF) gather(e0 + kE, 0, vn);  // the next batch's first element range, in flight meanwhile
       else gather(e0, 0, v);
       float sf[NV];  // dot products, value k kE + e (zero padded to NV: reduced in place)
 #pragma unroll
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<k
           a.dW[((int64_t)b * a.K + kl) * NN + (int64_t)a.csc_row[p] * a.N + j] = sv;
         }
       }
-      if constexpr (agg_prefetch<kNQ>()) {
+      if constexpr (PF) {
 #pragma unroll
         for (int e = 0; e < kE; ++e)
 #pragma unroll
@@ -486,6 +489,21 @@ struct SddmmL {
         (void)hipFuncSetAttribute((const void*)cheb_agg_sddmm_kernel<NQ, KM>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
         done = true;
+      }
+    }
+    static const bool nopf = getenv("DSTAGNN_SDDMM_NOPF") && atoi(getenv("DSTAGNN_SDDMM_NOPF")) != 0;
+    if constexpr (NQ <= 6 && KM <= 3) {
+      if (nopf) {
+        if (l.lds > (64u << 10)) {
+          static bool done2 = false;
+          if (!done2) {
+            (void)hipFuncSetAttribute((const void*)cheb_agg_sddmm_kernel<NQ, KM, false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+            done2 = true;
+          }
+        }
+        hipLaunchKernelGGL((cheb_agg_sddmm_kernel<NQ, KM, false>), l.grid, dim3(256), l.lds, l.st, l.a);
+        return;
       }
     }
     hipLaunchKernelGGL((cheb_agg_sddmm_kernel<NQ, KM>), l.grid, dim3(256), l.lds, l.st, l.a);

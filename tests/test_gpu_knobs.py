@@ -6,6 +6,7 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_TAT_MFMA=0   the VALU wave kernels of the temporal attention instead of the
                        matrix-core ones (ops.hip tat_*_mfma_kernel)
   DSTAGNN_SIDE_CUMASK  the side stream confined to a CU subset (scheduling only: same results)
+  DSTAGNN_SDDMM_NOPF=1 the aggregate-first SDDMM without its batch prefetch (4 waves per SIMD)
 
 PEMS08 geometry (the bench's default path otherwise), inner block with a broadcast res_att,
 eval and train mode, same bounds as tests/test_gpu_parity.py::test_block_vs_oracle_configs."""
@@ -29,7 +30,8 @@ print("KNOB_OK")
 """
 
 
-@pytest.mark.parametrize("env", ["DSTAGNN_DE_OMAP=1", "DSTAGNN_TAT_MFMA=0", "DSTAGNN_SIDE_CUMASK=0x11111111"])
+@pytest.mark.parametrize("env", ["DSTAGNN_DE_OMAP=1", "DSTAGNN_TAT_MFMA=0", "DSTAGNN_SIDE_CUMASK=0x11111111",
+                                 "DSTAGNN_SDDMM_NOPF=1"])
 def test_knob_path_vs_oracle(env):
     import torch
     if not torch.cuda.is_available():

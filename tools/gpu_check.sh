@@ -29,6 +29,7 @@ for s in "${S[@]}"; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    mstep)  run mstep 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mstep -o run --output-format csv -- python3 tools/model_step_prof.py --steps 5 ;;
     dp2)    DSTAGNN_DIST_BACKEND=gloo DSTAGNN_DEVICE_MOD=1 run dp2 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-extras ;;
     pmcs)   echo "== pmcs ($(date +%T))"; bash tools/pmc_step.sh || exit $? ;;
     pmcs_gambia) echo "== pmcs GAMBIA ($(date +%T))"; PMC_CONFIG=GAMBIA bash tools/pmc_step.sh || exit $? ;;
