@@ -60,10 +60,43 @@ __device__ __forceinline__ float apa_term(const ChebFl& a, const float* Mk, int 
   return a.apa[o] * Mk[o];
 }
 
+// The A_pa o M_k term of a tile is a dependent global load wherever the tile's bit word has a
+// bit in the lane's 16 fragment rows (at SYN, N = 4096 with 4 A_pa entries per row: ~60 % of
+// the tiles have one in some lane, so the whole wave waited on it).  The large-graph kernels
+// therefore carry it one tile ahead: the next tile's bit word and the term of its FIRST set bit
+// in the lane's rows are loaded while the current tile is multiplied; further set bits (rare:
+// ~2 % of the lanes' tiles) still load in place.  Same additions in the same order: identical
+// results.  Lane half h holds fragment rows (r & 3) + 8 (r >> 2) + 4 h.
+__device__ __forceinline__ uint32_t half_rows(int h) { return h ? 0xF0F0F0F0u : 0x0F0F0F0Fu; }
+struct ApaNext {
+  int f = -1;      // the first set fragment row of the lane's half, or -1
+  float v = 0.f;   // its A_pa o M_k term
+};
+// row-major walk (flash_dq): fixed row i, tile columns j0 + [0, 32)
+__device__ __forceinline__ ApaNext apa_first_row(const ChebFl& a, const float* Mk, uint32_t bits, int h, int i, int j0) {
+  ApaNext n;
+  const uint32_t b = bits & half_rows(h);
+  if (b) {
+    n.f = __builtin_ctz(b);
+    n.v = apa_term(a, Mk, i, j0 + n.f);
+  }
+  return n;
+}
+// column walk (flash_stats / flash_dk): fixed column j, tile rows i0 + [0, 32)
+__device__ __forceinline__ ApaNext apa_first_col(const ChebFl& a, const float* Mk, uint32_t bits, int h, int i0, int j) {
+  ApaNext n;
+  const uint32_t b = bits & half_rows(h);
+  if (b) {
+    n.f = __builtin_ctz(b);
+    n.v = apa_term(a, Mk, i0 + n.f, j);
+  }
+  return n;
+}
+
 // ---------------------------------------------------------------------------------------
 // forward: column statistics.  One wave per (b, k, 32 columns); waves independent.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void flash_stats_kernel(ChebFl a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flash_stats_kernel(ChebFl a) {
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const int nt = (a.N + 31) >> 5;
   const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -79,19 +112,23 @@ __global__ __launch_bounds__(256) void flash_stats_kernel(ChebFl a) {
   float m = -INFINITY, l = 0.f;
   float aq[16];
   load16(Q + (int64_t)min(l32, a.N - 1) * a.ld + h * 16, aq);
+  uint32_t bits = (uint32_t)bt[0];
+  ApaNext cur = apa_first_col(a, Mk, bits, h, 0, jc);
+  uint32_t bnext = nt > 1 ? (uint32_t)bt[1] : 0u;
   for (int it = 0; it < nt; ++it) {
     floatx16 acc = zero16();
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[s], bkv[s], acc, 0, 0, 0);
     if (it + 1 < nt) load16(Q + (int64_t)min((it + 1) * 32 + l32, a.N - 1) * a.ld + h * 16, aq);
-    const uint32_t bits = (uint32_t)bt[it];
+    const ApaNext nxt = it + 1 < nt ? apa_first_col(a, Mk, bnext, h, (it + 1) * 32, jc) : ApaNext{};
+    const uint32_t bnn = it + 2 < nt ? (uint32_t)bt[it + 2] : 0u;
     const int i0 = it * 32;
     float z[16], tmax = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int il = frag_row(r, h), i = i0 + il;
       float v = acc[r] * a.scale;
-      if ((bits >> il) & 1u) v += apa_term(a, Mk, i, jc);
+      if ((bits >> il) & 1u) v += il == cur.f ? cur.v : apa_term(a, Mk, i, jc);
       v = i < a.N ? v : -INFINITY;
       z[r] = v;
       tmax = fmaxf(tmax, v);
@@ -104,6 +141,9 @@ __global__ __launch_bounds__(256) void flash_stats_kernel(ChebFl a) {
       l = l * __expf(m - mn) + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
       m = mn;
     }
+    bits = bnext;
+    cur = nxt;
+    bnext = bnn;
   }
   const float m2 = __shfl_xor(m, 32, 64), l2 = __shfl_xor(l, 32, 64);
   const float M = fmaxf(m, m2);
@@ -167,7 +207,7 @@ __global__ __launch_bounds__(256) void flash_colc_kernel(ChebFl a) {
 }
 
 // backward: dQ'.  One wave per (b, k, 32 rows i), independent (own LDS slice).
-__global__ __launch_bounds__(256) void flash_dq_kernel(ChebFl a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flash_dq_kernel(ChebFl a) {
   __shared__ float Kt[4][32][33];
   __shared__ float lse_t[4][32], c_t[4][32];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
@@ -187,6 +227,9 @@ __global__ __launch_bounds__(256) void flash_dq_kernel(ChebFl a) {
   floatx16 O = zero16();
   float ak[16];
   load16(Kp + (int64_t)min(l32, a.N - 1) * a.ld + h * 16, ak);
+  uint32_t bits = (uint32_t)br[0];
+  ApaNext cur = apa_first_row(a, Mk, bits, h, ic, 0);
+  uint32_t bnext = nt > 1 ? (uint32_t)br[1] : 0u;
   for (int jt = 0; jt < nt; ++jt) {
     const int j0 = jt * 32;
 #pragma unroll
@@ -200,20 +243,24 @@ __global__ __launch_bounds__(256) void flash_dq_kernel(ChebFl a) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(ak[s], bq[s], S, 0, 0, 0);
     if (jt + 1 < nt) load16(Kp + (int64_t)min(j0 + 32 + l32, a.N - 1) * a.ld + h * 16, ak);
-    const uint32_t bits = (uint32_t)br[jt];
+    const ApaNext nxt = jt + 1 < nt ? apa_first_row(a, Mk, bnext, h, ic, j0 + 32) : ApaNext{};
+    const uint32_t bnn = jt + 2 < nt ? (uint32_t)br[jt + 2] : 0u;
     wave_lds_sync();
     float pa[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jl = frag_row(r, h);
       float v = S[r] * a.scale;
-      if ((bits >> jl) & 1u) v += apa_term(a, Mk, ic, j0 + jl);
+      if ((bits >> jl) & 1u) v += jl == cur.f ? cur.v : apa_term(a, Mk, ic, j0 + jl);
       pa[r] = __expf(v - lse_t[w][jl]) * c_t[w][jl];  // P_ij c_j (0 past N: lse = +inf)
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s)
       O = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], Kt[w][frag_row(s, h)][l32], O, 0, 0, 0);
     wave_lds_sync();
+    bits = bnext;
+    cur = nxt;
+    bnext = bnn;
   }
   const int64_t zb = (int64_t)bk * a.nnz;
 #pragma unroll
@@ -247,6 +294,9 @@ __global__ __launch_bounds__(256) void flash_dk_kernel(ChebFl a) {
   floatx16 U = zero16();
   float aq[16];
   load16(Q + (int64_t)min(l32, a.N - 1) * a.ld + h * 16, aq);
+  uint32_t bits = (uint32_t)bt[0];
+  ApaNext cur = apa_first_col(a, Mk, bits, h, 0, jc);
+  uint32_t bnext = nt > 1 ? (uint32_t)bt[1] : 0u;
   for (int it = 0; it < nt; ++it) {
     const int i0 = it * 32;
 #pragma unroll
@@ -255,20 +305,24 @@ __global__ __launch_bounds__(256) void flash_dk_kernel(ChebFl a) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[s], bkv[s], S, 0, 0, 0);
     if (it + 1 < nt) load16(Q + (int64_t)min(i0 + 32 + l32, a.N - 1) * a.ld + h * 16, aq);
-    const uint32_t bits = (uint32_t)bt[it];
+    const ApaNext nxt = it + 1 < nt ? apa_first_col(a, Mk, bnext, h, i0 + 32, jc) : ApaNext{};
+    const uint32_t bnn = it + 2 < nt ? (uint32_t)bt[it + 2] : 0u;
     wave_lds_sync();
     float pr[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int il = frag_row(r, h), i = i0 + il;
       float v = S[r] * a.scale;
-      if ((bits >> il) & 1u) v += apa_term(a, Mk, i, jc);
+      if ((bits >> il) & 1u) v += il == cur.f ? cur.v : apa_term(a, Mk, i, jc);
       pr[r] = i < a.N ? __expf(v - lse) : 0.f;
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s)
       U = __builtin_amdgcn_mfma_f32_32x32x2f32(pr[s], Qt[w][frag_row(s, h)][l32], U, 0, 0, 0);
     wave_lds_sync();
+    bits = bnext;
+    cur = nxt;
+    bnext = bnn;
   }
   const int64_t zb = (int64_t)bk * a.nnz;
   const float* cb = a.cc + (int64_t)bk * a.N;

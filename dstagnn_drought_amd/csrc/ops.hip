@@ -607,6 +607,109 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd a) {
   }
 }
 
+// Long rows (L > 1024: the TAt / EmbedT LayerNorm over N nodes at GAMBIA N = 2139 and SYN
+// N = 4096): a 256-thread WORKGROUP per row, element e = tid + 256 q (VPT <= 16 values per
+// thread, all loads in one round as above), the sums over the row by a wave reduction and the
+// four waves' partials through LDS in a fixed order.  The wave-per-row kernel needed 64 values
+// per lane there (~210-256 VGPRs + AGPR spills of the gradient: one wave per SIMD, ~25 % of
+// HBM bandwidth).
+__device__ __forceinline__ float wg_sum4(float v, float* red4) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red4[w] = v;
+  __syncthreads();
+  const float t = (red4[0] + red4[1]) + (red4[2] + red4[3]);
+  __syncthreads();  // red4 reused by the next reduction
+  return t;
+}
+
+template <int VPT, int NSRC>
+__global__ __launch_bounds__(256) void ln_fwd_wg_kernel(LnFwd a) {
+  __shared__ float red4[4];
+  const int tid = threadIdx.x, row = blockIdx.x, L = a.L;
+  float xs[NSRC][VPT], gv[VPT], bv[VPT], v[VPT];
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int e = min(tid + 256 * q, L - 1);
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s) xs[s][q] = a.src[s].p[ioff(a.src[s].row, row) + (int64_t)e * a.src[s].es];
+    gv[q] = a.g[e];
+    bv[q] = a.b[e];
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    float u = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s) u += xs[s][q];
+    v[q] = tid + 256 * q < L ? u : 0.f;
+    sum += v[q];
+  }
+  const float mean = wg_sum4(sum, red4) / L;
+  float var = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q)
+    if (tid + 256 * q < L) { const float d = v[q] - mean; var += d * d; }
+  var = wg_sum4(var, red4) / L;
+  const float rs = rsqrtf(var + a.eps);
+  if (tid == 0) { a.mu[row] = mean; a.rs[row] = rs; }
+  const int64_t yo = ioff(a.yrow, row);
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int e = tid + 256 * q;
+    if (e >= L) continue;
+    if (a.u) a.u[(int64_t)row * L + e] = v[q];
+    float y = (v[q] - mean) * rs * gv[q] + bv[q];
+    if (a.drop_p > 0.f) y *= drop_scale(a.seed, a.which, (uint64_t)row * L + e + a.drop_off, a.drop_p);
+    a.y[yo + (int64_t)e * a.yes] = y;
+  }
+}
+
+// backward of the above (per-element gamma / beta contributions: the partial-slab form needs
+// L <= 1024)
+template <int VPT>
+__global__ __launch_bounds__(256) void ln_bwd_wg_kernel(LnBwd a) {
+  __shared__ float red4[4];
+  const int tid = threadIdx.x, row = blockIdx.x, L = a.L;
+  const int64_t yo = ioff(a.dyrow, row), xo = ioff(a.dxrow, row);
+  float dyl[VPT], ul[VPT], gl[VPT], xin[VPT];
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int e = min(tid + 256 * q, L - 1);
+    dyl[q] = a.dy[yo + (int64_t)e * a.dyes];
+    ul[q] = a.u[(int64_t)row * L + e];
+    gl[q] = a.g[e];
+    xin[q] = a.beta != 0.f ? a.dx[xo + (int64_t)e * a.dxes] : 0.f;
+  }
+  const float mean = a.mu[row], rs = a.rs[row];
+  float dyv[VPT], xh[VPT], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int e = tid + 256 * q;
+    dyv[q] = 0.f; xh[q] = 0.f;
+    if (e < L) {
+      float dy = dyl[q];
+      if (a.drop_p > 0.f) dy *= drop_scale(a.seed, a.which, (uint64_t)row * L + e + a.drop_off, a.drop_p);
+      const float x = (ul[q] - mean) * rs;
+      dyv[q] = dy; xh[q] = x;
+      const float dxh = dy * gl[q];
+      s1 += dxh; s2 += dxh * x;
+      if (a.gcontrib) a.gcontrib[(int64_t)row * L + e] = dy * x;
+      if (a.bcontrib) a.bcontrib[(int64_t)row * L + e] = dy;
+    }
+  }
+  s1 = wg_sum4(s1, red4) / L;
+  s2 = wg_sum4(s2, red4) / L;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int e = tid + 256 * q;
+    if (e >= L) continue;
+    float dx = rs * (dyv[q] * gl[q] - s1 - xh[q] * s2);
+    if (a.beta != 0.f) dx += a.beta * xin[q];
+    a.dx[xo + (int64_t)e * a.dxes] = dx;
+  }
+}
+
 // PART: gamma / beta gradient partial sums per workgroup instead of per-element contribution
 // tensors: a wave takes kLnRowsPerWave consecutive rows, keeps the sums over them in
 // registers, and the 4 waves combine through LDS into one row of the (blocks, L) slabs
@@ -1652,6 +1755,12 @@ static void launch_ln_fwd(const LnFwd& a, dim3 grid, hipStream_t st) {
   else hipLaunchKernelGGL((ln_fwd_kernel<VPT, 3>), grid, dim3(256), 0, st, a);
 }
 
+// DSTAGNN_LN_WG=0: long rows keep the wave-per-row kernels (A/B)
+static bool ln_wg_rows() {
+  static const bool on = !getenv("DSTAGNN_LN_WG") || atoi(getenv("DSTAGNN_LN_WG")) != 0;
+  return on;
+}
+
 int op_ln_fwd(const LnFwd& a, hipStream_t st) {
   if (a.nsrc < 1 || a.nsrc > 3 || a.L < 1) { set_last_error("ln_fwd: 1..3 sources, L >= 1"); return DSTAGNN_E_ARG; }
   dim3 grid((unsigned)cdiv64(a.R, 4));
@@ -1661,6 +1770,16 @@ int op_ln_fwd(const LnFwd& a, hipStream_t st) {
   else if (vpt <= 4) launch_ln_fwd<4>(a, grid, st);
   else if (vpt <= 8) launch_ln_fwd<8>(a, grid, st);
   else if (vpt <= 16) launch_ln_fwd<16>(a, grid, st);
+  else if (ln_wg_rows() && a.L <= 4096) {  // a workgroup per row (ln_fwd_wg_kernel)
+    const dim3 g((unsigned)a.R);
+    const int v = (int)cdiv64(a.L, 256);
+#define DS_LNW(V) \
+  if (a.nsrc == 1) hipLaunchKernelGGL((ln_fwd_wg_kernel<V, 1>), g, dim3(256), 0, st, a); \
+  else if (a.nsrc == 2) hipLaunchKernelGGL((ln_fwd_wg_kernel<V, 2>), g, dim3(256), 0, st, a); \
+  else hipLaunchKernelGGL((ln_fwd_wg_kernel<V, 3>), g, dim3(256), 0, st, a);
+    if (v <= 8) { DS_LNW(8) } else { DS_LNW(16) }
+#undef DS_LNW
+  }
   else if (vpt <= 64) launch_ln_fwd<64>(a, grid, st);
   else { set_last_error("ln_fwd: row too long"); return DSTAGNN_E_SHAPE; }
   DS_CHECK_LAUNCH();
@@ -1686,6 +1805,10 @@ int op_ln_bwd(const LnBwd& a, hipStream_t st) {
   else if (vpt <= 4) hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, st, a);
   else if (vpt <= 8) hipLaunchKernelGGL((ln_bwd_kernel<8, false>), grid, dim3(256), 0, st, a);
   else if (vpt <= 16) hipLaunchKernelGGL((ln_bwd_kernel<16, false>), grid, dim3(256), 0, st, a);
+  else if (ln_wg_rows() && a.L <= 4096) {
+    if (a.L <= 2048) hipLaunchKernelGGL((ln_bwd_wg_kernel<8>), dim3((unsigned)a.R), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((ln_bwd_wg_kernel<16>), dim3((unsigned)a.R), dim3(256), 0, st, a);
+  }
   else if (vpt <= 64) hipLaunchKernelGGL((ln_bwd_kernel<64, false>), grid, dim3(256), 0, st, a);
   else { set_last_error("ln_bwd: row too long"); return DSTAGNN_E_SHAPE; }
   DS_CHECK_LAUNCH();

@@ -688,6 +688,51 @@ std::vector<Tensor> head_bwd(at::TensorList outs, const Tensor& w1, const Tensor
 }
 
 // -------------------------------------------------------------------------------------
+// optimiser: one Adam step over the listed tensors (optim.hip); the segment / chunk tables
+// go through a pinned host buffer and an asynchronous copy on the current stream (the
+// caching host allocator keeps the buffer alive until the copy has run)
+// -------------------------------------------------------------------------------------
+void adam_step(at::TensorList params, at::TensorList grads, at::TensorList exp_avgs, at::TensorList exp_avg_sqs,
+               double beta1, double beta2, double eps, double step_size, double bc2_sqrt) {
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n && exp_avgs.size() == n && exp_avg_sqs.size() == n, "adam_step: list lengths differ");
+  if (n == 0) return;
+  c10::DeviceGuard guard(params[0].device());
+  const int64_t ce = dstagnn_adam_chunk_elems();
+  std::vector<dstagnn_adam_seg> segs(n);
+  int64_t nchunk = 0;
+  for (size_t i = 0; i < n; ++i) {
+    for (const Tensor* t : {&params[i], &grads[i], &exp_avgs[i], &exp_avg_sqs[i]}) {
+      check_dev(*t, at::kFloat, "adam_step tensor");
+      TORCH_CHECK(t->device() == params[0].device(), "adam_step: tensors on different devices");
+      TORCH_CHECK(t->numel() == params[i].numel(), "adam_step: param / grad / state sizes differ");
+    }
+    segs[i] = {params[i].data_ptr<float>(), grads[i].data_ptr<float>(), exp_avgs[i].data_ptr<float>(),
+               exp_avg_sqs[i].data_ptr<float>(), params[i].numel()};
+    nchunk += (params[i].numel() + ce - 1) / ce;
+  }
+  TORCH_CHECK(nchunk < (1ll << 31), "adam_step: too many chunks");
+  const size_t sb = n * sizeof(dstagnn_adam_seg), cb = (size_t)nchunk * 2 * sizeof(int64_t);
+  Tensor host = at::empty({(int64_t)(sb + cb)}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  uint8_t* hp = host.data_ptr<uint8_t>();
+  std::memcpy(hp, segs.data(), sb);
+  int64_t* ch = reinterpret_cast<int64_t*>(hp + sb);
+  int64_t k = 0;
+  for (size_t i = 0; i < n; ++i)
+    for (int64_t off = 0; off < segs[i].n; off += ce) {
+      ch[2 * k] = (int64_t)i;
+      ch[2 * k + 1] = off;
+      ++k;
+    }
+  Tensor dev = host.to(params[0].device(), /*non_blocking=*/true);
+  const uint8_t* dp = dev.data_ptr<uint8_t>();
+  check_rc(dstagnn_adam_step(reinterpret_cast<const dstagnn_adam_seg*>(dp), reinterpret_cast<const int64_t*>(dp + sb),
+                             (int)nchunk, (float)beta1, (float)beta2, (float)eps, (float)step_size, (float)bc2_sqrt,
+                             stream_of(params[0])),
+           "dstagnn_adam_step");
+}
+
+// -------------------------------------------------------------------------------------
 // graph builders (fp64)
 // -------------------------------------------------------------------------------------
 // data (T,N,F) -> (xhat (N,T,F), p (N,T), psum (N))
@@ -810,6 +855,8 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("colsum(Tensor x, int O, int I) -> Tensor");
   m.def("head_fwd(Tensor[] outs, Tensor w1, Tensor b1, Tensor w2, Tensor b2) -> (Tensor, Tensor)");
   m.def("head_bwd(Tensor[] outs, Tensor w1, Tensor w2, Tensor h, Tensor dy, int[] need) -> Tensor[]");
+  m.def("adam_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avgs, Tensor(c!)[] exp_avg_sqs, "
+        "float beta1, float beta2, float eps, float step_size, float bc2_sqrt) -> ()");
   m.def("stag_prep(Tensor data) -> (Tensor, Tensor, Tensor)");
   m.def("stag_emd_pairs(Tensor xhat, Tensor p, Tensor psum, Tensor pairs, bool with_pivots) -> (Tensor, Tensor, Tensor)");
   m.def("stag_emd_lds_bytes(int T, int F) -> int", stag_emd_lds_bytes);
@@ -839,6 +886,7 @@ TORCH_LIBRARY_IMPL(dstagnn, CUDA, m) {
   m.impl("colsum", colsum);
   m.impl("head_fwd", head_fwd);
   m.impl("head_bwd", head_bwd);
+  m.impl("adam_step", adam_step);
   m.impl("stag_prep", stag_prep);
   m.impl("stag_emd_pairs", stag_emd_pairs);
   m.impl("emd_dense", emd_dense);

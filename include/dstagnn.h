@@ -259,6 +259,25 @@ int dstagnn_head_backward(int B, int N, int C, int T, int nb, int O, int P, cons
                           size_t scratch_bytes, dstagnn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Optimiser step of the training driver (optim.hip): torch.optim.Adam as the reference builds
+ * it (train_DSTAGNN_my.py:126: `optim.Adam(net.parameters(), lr=learning_rate)` — betas
+ * (0.9, 0.999), eps 1e-8, no weight decay, no amsgrad) over many fp32 tensors in ONE launch.
+ * segs: device array of {param, grad, exp_avg, exp_avg_sq, n}; chunks: device array of nchunk
+ * (segment index, element offset) pairs, one per dstagnn_adam_chunk_elems() elements of a
+ * segment.  step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t) for step t.
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+} dstagnn_adam_seg;
+int dstagnn_adam_chunk_elems(void);
+int dstagnn_adam_step(const dstagnn_adam_seg* segs, const int64_t* chunks, int nchunk, float beta1, float beta2,
+                      float eps, float step_size, float bc2_sqrt, dstagnn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Graph builders (stag.hip).  fp64 throughout, like the reference's numpy/scipy code.
  * ------------------------------------------------------------------------------------- */
 
