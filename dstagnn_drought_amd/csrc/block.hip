@@ -761,10 +761,25 @@ struct Fwd {
     return g;
   }
 
+  // DSTAGNN_GTU_GCONV=0: the forward convolutions as the grouped implicit-im2col GEMM (A/B)
+  static bool gconv_on() {
+    static const bool on = !getenv("DSTAGNN_GTU_GCONV") || atoi(getenv("DSTAGNN_GTU_GCONV")) != 0;
+    return on;
+  }
+
   int stage_tail(bool /*split*/) {
     // the three independent convolutions (kernel widths 3, 5, 7) as ONE grouped launch
-    const Gemm convs[3] = {gtu_conv(0), gtu_conv(1), gtu_conv(2)};
-    DS_TRY(run_gemm_group(convs, 3, w.gemm_ws, kGemmWs, st));
+    if (gconv_on() && gtu_conv_fwd_ok(m.C, m.T, m.ks, 3)) {  // sliding-window kernel (gtu_tconv.hip)
+      GconvArgs gc{};
+      gc.X = s.X; gc.BN = m.BN; gc.T = m.T;
+      for (int q = 0; q < 3; ++q) {
+        gc.wf[q] = s.Wgf[q]; gc.bias[q] = p.gtu_b[q]; gc.conv[q] = s.conv[q]; gc.ks[q] = m.ks[q];
+      }
+      DS_TRY(op_gtu_conv_fwd(gc, st));
+    } else {
+      const Gemm convs[3] = {gtu_conv(0), gtu_conv(1), gtu_conv(2)};
+      DS_TRY(run_gemm_group(convs, 3, w.gemm_ws, kGemmWs, st));
+    }
     GtuTailArgs t;  // gates + fcmy + dropout + residual + LN, one workgroup per node
     t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
     for (int q = 0; q < 3; ++q) t.conv[q] = s.conv[q];
@@ -955,7 +970,16 @@ struct Bwd {
       }
       segs[0].beta = 1.f;
       segs[0].Cout = w.gpre; segs[0].emask = s.X;  // fused ReLU backward of the cheb output
-      DS_TRY(run_gemm_kcat(segs, 3, st));
+      if (tconv_on() && gtu_tconv_ok(m.C, m.ks, 3)) {
+        // the same product as one sliding-window kernel: each tile stages the union of its
+        // rows' windows once (gtu_tconv.hip)
+        TconvArgs tc;
+        for (int q = 0; q < 3; ++q) { tc.dconv[q] = w.dconv[q]; tc.wflip[q] = s.Wgb[q]; tc.ks[q] = m.ks[q]; }
+        tc.dX = w.dX; tc.X = s.X; tc.gpre = w.gpre; tc.M = m.BN * m.T;
+        DS_TRY(op_gtu_tconv(tc, st));
+      } else {
+        DS_TRY(run_gemm_kcat(segs, 3, st));
+      }
     }
     return 0;
   }
@@ -1262,6 +1286,13 @@ struct Bwd {
       DS_TRY(op_transpose(w.dE, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
     }
     return 0;
+  }
+
+  // DSTAGNN_GTU_TCONV=0: the GTU input gradient as the K-concatenated GEMM (run_gemm_kcat)
+  // instead of the sliding-window kernel (A/B)
+  static bool tconv_on() {
+    static const bool on = !getenv("DSTAGNN_GTU_TCONV") || atoi(getenv("DSTAGNN_GTU_TCONV")) != 0;
+    return on;
   }
 
   // DSTAGNN_DE_OMAP=1: the inner block's dE accumulated straight into dx by the GEMM's output

@@ -271,6 +271,9 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st);
 // GEMM-family profiling (gemm.hip): while on, the block runs on ONE stream (no side-stream
 // overlap) so every recorded GEMM duration is its own
 bool gemm_prof_on();
+// a GEMM-family product computed by another kernel, timed into the same records (or null)
+void* gemm_prof_begin(double flops, double bytes, hipStream_t st);
+void gemm_prof_end(void* rec, hipStream_t st);
 int gemm_prof_start(int capacity);
 int gemm_prof_stop(dstagnn_prof_stats* out);
 int gemm_set_splitk_target(int target);

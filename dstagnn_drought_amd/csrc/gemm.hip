@@ -353,6 +353,24 @@ int g_bf16 = 0;
 
 bool gemm_prof_on() { return g_prof.on; }
 
+// the same event pair around a non-GEMM kernel that computes a GEMM-family product (the
+// sliding-window GTU input gradient, gtu_tconv.hip): counted with its algorithmic FLOP / bytes
+void* gemm_prof_begin(double flops, double bytes, hipStream_t st) {
+  if (!g_prof.on) return nullptr;
+  if (g_prof.n >= g_prof.cap) {
+    ++g_prof.dropped;
+    return nullptr;
+  }
+  ProfRec* r = &g_prof.rec[g_prof.n++];
+  r->flops = flops;
+  r->bytes = bytes;
+  (void)hipEventRecord(r->e0, st);
+  return r;
+}
+void gemm_prof_end(void* rec, hipStream_t st) {
+  if (rec) (void)hipEventRecord(static_cast<ProfRec*>(rec)->e1, st);
+}
+
 int gemm_set_splitk_target(int target) {
   const int prev = g_splitk_target;
   if (target > 0) g_splitk_target = target;

@@ -228,6 +228,32 @@ int op_cheb_spmm_t_bwd(const ChebSp& a, hipStream_t st);
 int op_pack_theta(const PackTheta& a, hipStream_t st);
 int op_transpose(const float* in, float* out, int R, int Cc, int batch, int64_t in_bs, int64_t out_bs, float beta,
                  hipStream_t st);
+// the GTU convolutions' input gradient as one sliding-window kernel (gtu_tconv.hip)
+struct TconvArgs {
+  const float* dconv[3];  // zero-padded gate-gradient rows (M + ks - 1, 2C) per GTU
+  const float* wflip[3];  // flipped weights (ks, 2C, C) per GTU
+  int ks[3];
+  const float* dX;        // (M, C) the tail's gradient of the GTU block input (beta input)
+  const float* X;         // (M, C) the Chebyshev output (ReLU mask)
+  float* gpre;            // (M, C) result
+  int64_t M;              // rows B*N*T
+};
+bool gtu_tconv_ok(int C, const int* ks, int n);
+// the three GTU convolutions (forward) by the same sliding window (gtu_tconv.hip)
+struct GconvArgs {
+  const float* X;        // (BN, T, C) Chebyshev output
+  const float* wf[3];    // (2C, ks, C) re-laid weights (o, j, c)
+  const float* bias[3];  // (2C) or null
+  float* conv[3];        // (BN * Tg, 2C)
+  int ks[3];
+  int Tg[3];             // set by the launcher
+  int start[4];          // first workgroup of each GTU (set by the launcher)
+  int64_t BN;
+  int T;
+};
+bool gtu_conv_fwd_ok(int C, int T, const int* ks, int n);
+int op_gtu_conv_fwd(GconvArgs a, hipStream_t st);
+int op_gtu_tconv(const TconvArgs& a, hipStream_t st);
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st);
 int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
