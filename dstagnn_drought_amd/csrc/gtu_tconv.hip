@@ -14,8 +14,9 @@
 // staged row r + j: the same products, k_q× less operand traffic, MFMA-bound.
 //
 // MFMA v_mfma_f32_32x32x2_f32, wave w owns rows [32w, 32w + 32) of the tile and all C = 32
-// columns; step s of tap j contracts o = 2s + h (lane half h), i.e. the flattened index
-// j·2C + 2s + h (the same products as the K-concatenated GEMM, summed in this fixed order).
+// columns; step s of tap j contracts o = s + 32h (lane half h: the two halves read columns 32
+// apart, so the 64 lanes of an A-fragment read hit 64 distinct banks with the 65-float rows) —
+// the same products as the K-concatenated GEMM, summed in this fixed order.
 // The weight fragments (≤ 57 KB per GTU, L2-resident) come from global memory one tap ahead.
 #include <algorithm>
 
@@ -34,54 +35,78 @@ constexpr int kTcStageF4 = (kTcRowsMax * kTcCin / 4 + 255) / 256;  // float4 loa
 
 __device__ __forceinline__ int tc_frow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// the 15 taps of the three GTUs as one flat sequence: tap i -> (GTU, offset j)
+struct TcTap {
+  int q, j;
+};
+__device__ __forceinline__ TcTap tc_tap(const TconvArgs& a, int i) {
+  const int k0 = a.ks[0], k1 = a.ks[1];
+  if (i < k0) return {0, i};
+  if (i < k0 + k1) return {1, i - k0};
+  return {2, i - k0 - k1};
+}
+// B fragments of a tap: B[kk = s + 32h][n = l32] = Wflip[(j 2C + s + 32h) C + l32]
+__device__ __forceinline__ void tc_load_b(const TconvArgs& a, TcTap t, int h, int l32, float (&b)[32]) {
+  const float* wq = a.wflip[t.q] + ((int64_t)t.j * kTcCin + 32 * h) * kTcC + l32;
+#pragma unroll
+  for (int s = 0; s < 32; ++s) b[s] = wq[s * kTcC];
+}
+// the tile's window rows of GTU q, one round of 16-B loads into registers
+__device__ __forceinline__ void tc_load_a(const TconvArgs& a, int q, int64_t m0, float4 (&v)[kTcStageF4]) {
+  const int ks = a.ks[q], rows = kTcBM + ks - 1;
+  const int64_t avail = a.M + ks - 1 - m0;
+  const float* src = a.dconv[q] + m0 * kTcCin;
+#pragma unroll
+  for (int u = 0; u < kTcStageF4; ++u) {
+    const int e4 = threadIdx.x + 256 * u, row = e4 >> 4;
+    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < rows && row < avail) v[u] = *reinterpret_cast<const float4*>(src + (int64_t)e4 * 4);
+  }
+}
+
+// One workgroup per 128 output rows; the taps of all three GTUs run as one sequence with the
+// weight fragments loaded two taps ahead and the next GTU's window rows loaded during the
+// current GTU's last tap (the grid gives ~2 waves per SIMD at PEMS08, so the registers are
+// spent on keeping loads in flight instead of on occupancy).
 __global__ __launch_bounds__(256) void gtu_tconv_kernel(TconvArgs a) {
   __shared__ float As[kTcRowsMax * kTcRow];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int64_t m0 = (int64_t)blockIdx.x * kTcBM;
+  const int ntap = a.ks[0] + a.ks[1] + a.ks[2];
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (int q = 0; q < 3; ++q) {
-    const int ks = a.ks[q], rows = kTcBM + ks - 1;
-    const int64_t avail = a.M + ks - 1 - m0;  // window rows present in the buffer from m0 on
-    const float* src = a.dconv[q] + m0 * kTcCin;
-    // the tile's window rows, one round of 16-B loads (all issued before the first LDS store)
-    float4 v[kTcStageF4];
+  float4 v[kTcStageF4];
+  tc_load_a(a, 0, m0, v);
+  float b0[32], b1[32];
+  tc_load_b(a, tc_tap(a, 0), h, l32, b0);
+  tc_load_b(a, tc_tap(a, min(1, ntap - 1)), h, l32, b1);
+  const float* arow = As + (32 * w + l32) * kTcRow + 32 * h;
+  for (int i = 0; i < ntap; ++i) {
+    const TcTap t = tc_tap(a, i);
+    if (t.j == 0) {  // a GTU's first tap: its window rows (loaded earlier) into LDS
+      const int rows = kTcBM + a.ks[t.q] - 1;
+      __syncthreads();  // the previous GTU's reads of As are done
 #pragma unroll
-    for (int u = 0; u < kTcStageF4; ++u) {
-      const int e4 = tid + 256 * u, row = e4 >> 4;
-      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (row < rows && row < avail) v[u] = *reinterpret_cast<const float4*>(src + (int64_t)e4 * 4);
+      for (int u = 0; u < kTcStageF4; ++u) {
+        const int e4 = tid + 256 * u, row = e4 >> 4, c = (e4 & 15) * 4;
+        if (row < rows) {
+          float* d = As + row * kTcRow + c;
+          d[0] = v[u].x; d[1] = v[u].y; d[2] = v[u].z; d[3] = v[u].w;
+        }
+      }
+      __syncthreads();
     }
-    // first tap's weight fragments: B[kk = 2s + h][n = l32] = Wflip[(j 2C + 2s + h) C + l32]
-    const float* wq = a.wflip[q];
-    float bc[32];
+    float b2[32];  // two taps ahead
+    if (i + 2 < ntap) tc_load_b(a, tc_tap(a, i + 2), h, l32, b2);
+    if (t.j == a.ks[t.q] - 1 && t.q < 2) tc_load_a(a, t.q + 1, m0, v);  // the next GTU's rows
+    const float* ar = arow + t.j * kTcRow;
 #pragma unroll
-    for (int s = 0; s < 32; ++s) bc[s] = wq[(2 * s + h) * kTcC + l32];
-    __syncthreads();  // the previous GTU's reads of As are done
+    for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[s], b0[s], acc, 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < kTcStageF4; ++u) {
-      const int e4 = tid + 256 * u, row = e4 >> 4, c = (e4 & 15) * 4;
-      if (row < rows) {
-        float* d = As + row * kTcRow + c;
-        d[0] = v[u].x; d[1] = v[u].y; d[2] = v[u].z; d[3] = v[u].w;
-      }
-    }
-    __syncthreads();
-    const float* arow = As + (32 * w + l32) * kTcRow + h;
-    for (int j = 0; j < ks; ++j) {
-      float bn[32];  // the next tap's fragments, in flight during this tap
-      if (j + 1 < ks) {
-#pragma unroll
-        for (int s = 0; s < 32; ++s) bn[s] = wq[((j + 1) * kTcCin + 2 * s + h) * kTcC + l32];
-      }
-      const float* ar = arow + j * kTcRow;
-#pragma unroll
-      for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * s], bc[s], acc, 0, 0, 0);
-      if (j + 1 < ks) {
-#pragma unroll
-        for (int s = 0; s < 32; ++s) bc[s] = bn[s];
-      }
+    for (int s = 0; s < 32; ++s) {
+      b0[s] = b1[s];
+      b1[s] = b2[s];
     }
   }
   // epilogue: gpre = (X > 0) ? dX + acc : 0, row m = m0 + 32 w + frow(r, h), column l32;
@@ -97,8 +122,8 @@ __global__ __launch_bounds__(256) void gtu_tconv_kernel(TconvArgs a) {
   for (int r = 0; r < 16; ++r) {
     const int64_t m = m0 + 32 * w + tc_frow(r, h);
     if (m >= a.M) continue;
-    const float v = acc[r] * 1.f + 1.f * dx[r];
-    a.gpre[m * kTcC + l32] = xm[r] > 0.f ? v : 0.f;
+    const float v2 = acc[r] * 1.f + 1.f * dx[r];
+    a.gpre[m * kTcC + l32] = xm[r] > 0.f ? v2 : 0.f;
   }
 }
 
@@ -110,7 +135,7 @@ __global__ __launch_bounds__(256) void gtu_tconv_kernel(TconvArgs a) {
 // ONE contiguous range (a node's last rows are followed by the next node's first), staged once
 // into LDS; the A fragment of tap j for row m is staged row in(m) - in(m0) + j.  Wave w owns
 // rows 32 (w & 1) and output channels 32 (w >> 1) of the tile; step s of tap j contracts
-// c = 2s + h, the GEMM's (j, c) order.  Output: conv_q[m][o] = bias[o] + sum.
+// c = s + 16h (the halves read columns 16 apart: fewer bank conflicts than c = 2s + h).  Output: conv_q[m][o] = bias[o] + sum.
 // ---------------------------------------------------------------------------------------
 constexpr int kGcBM = 64, kGcRowsMax = 320, kGcRow = kTcC + 1;
 constexpr int kGcStageF4 = kGcRowsMax * kTcC / 4 / 256;  // float4 loads per thread (10)
@@ -139,10 +164,10 @@ __global__ __launch_bounds__(256) void gtu_conv_fwd_kernel(GconvArgs a) {
   const int64_t m = min(m0 + 32 * (w & 1) + l32, mlast);
   const int ar = (int)(in_row(m) - r0);
   const int o = 32 * (w >> 1) + l32;
-  const float* wo = a.wf[q] + (int64_t)o * ks * kTcC;  // (o, j, c)
+  const float* wo = a.wf[q] + o;  // (j, c, o): B[kk = j C + c][n = o], lanes along o (coalesced)
   float bc[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) bc[s] = wo[2 * s + h];
+  for (int s = 0; s < 16; ++s) bc[s] = wo[(s + 16 * h) * (2 * kTcC)];
 #pragma unroll
   for (int u = 0; u < kGcStageF4; ++u) {
     const int e4 = tid + 256 * u, row = e4 >> 3, c = (e4 & 7) * 4;
@@ -159,11 +184,11 @@ __global__ __launch_bounds__(256) void gtu_conv_fwd_kernel(GconvArgs a) {
     float bn[16];
     if (j + 1 < ks) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) bn[s] = wo[(j + 1) * kTcC + 2 * s + h];
+      for (int s = 0; s < 16; ++s) bn[s] = wo[((j + 1) * kTcC + s + 16 * h) * (2 * kTcC)];
     }
-    const float* xr = Xs + (ar + j) * kGcRow + h;
+    const float* xr = Xs + (ar + j) * kGcRow + 16 * h;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[2 * s], bc[s], acc, 0, 0, 0);
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[s], bc[s], acc, 0, 0, 0);
     if (j + 1 < ks) {
 #pragma unroll
       for (int s = 0; s < 16; ++s) bc[s] = bn[s];

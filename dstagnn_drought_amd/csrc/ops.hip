@@ -1549,6 +1549,11 @@ __global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
         o = (oc * g.p1 + j) * g.p0 + c;
         break;
       }
+      case 7: {  // src (o, c, j) -> dst (j, c, o): the forward convolution's B operand, o fastest
+        const int64_t j = i % g.p1, r = i / g.p1, c = r % g.p0, oc = r / g.p0;
+        o = (j * g.p0 + c) * 2 * g.p0 + oc;
+        break;
+      }
       case 4: {  // src (o, c, j) -> dst (ks-1-j, o, c)
         const int64_t j = i % g.p1, r = i / g.p1, c = r % g.p0, oc = r / g.p0;
         o = ((g.p1 - 1 - j) * 2 * g.p0 + oc) * g.p0 + c;

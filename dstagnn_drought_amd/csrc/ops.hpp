@@ -242,7 +242,7 @@ bool gtu_tconv_ok(int C, const int* ks, int n);
 // the three GTU convolutions (forward) by the same sliding window (gtu_tconv.hip)
 struct GconvArgs {
   const float* X;        // (BN, T, C) Chebyshev output
-  const float* wf[3];    // (2C, ks, C) re-laid weights (o, j, c)
+  const float* wf[3];    // (ks, C, 2C) re-laid weights (j, c, o)
   const float* bias[3];  // (2C) or null
   float* conv[3];        // (BN * Tg, 2C)
   int ks[3];

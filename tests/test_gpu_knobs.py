@@ -8,7 +8,7 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_SIDE_CUMASK  the side stream confined to a CU subset (scheduling only: same results)
   DSTAGNN_SDDMM_NOPF=1 the aggregate-first SDDMM without its batch prefetch (4 waves per SIMD)
   DSTAGNN_GTU_TCONV=0  the GTU input gradient as the K-concatenated GEMM (run_gemm_kcat)
-  DSTAGNN_GTU_GCONV=0  the GTU forward convolutions as the grouped implicit-im2col GEMM
+  DSTAGNN_GTU_GCONV=1  the GTU forward convolutions by the sliding-window kernel (gtu_tconv.hip)
 
 PEMS08 geometry (the bench's default path otherwise), inner block with a broadcast res_att,
 eval and train mode, same bounds as tests/test_gpu_parity.py::test_block_vs_oracle_configs."""
@@ -33,7 +33,7 @@ print("KNOB_OK")
 
 
 @pytest.mark.parametrize("env", ["DSTAGNN_DE_OMAP=1", "DSTAGNN_TAT_MFMA=0", "DSTAGNN_SIDE_CUMASK=0x11111111",
-                                 "DSTAGNN_SDDMM_NOPF=1", "DSTAGNN_GTU_TCONV=0", "DSTAGNN_GTU_GCONV=0"])
+                                 "DSTAGNN_SDDMM_NOPF=1", "DSTAGNN_GTU_TCONV=0", "DSTAGNN_GTU_GCONV=1"])
 def test_knob_path_vs_oracle(env):
     import torch
     if not torch.cuda.is_available():
