@@ -861,12 +861,20 @@ int rows_gemm(const float* A, int lda, const float* B, Idx2 bk, Idx2 bn, float* 
 // (measured: SYN T=24 step 60.9 -> 57.7 ms split; PEMS08 T=12 0.91 fused vs 0.99 split);
 // DSTAGNN_TAIL_SPLIT_T overrides the threshold (0 = always split, used by the parity runs)
 constexpr int kTailSplitT = 20;
+// DSTAGNN_TAIL_CT24=1: the compile-time tail kernels also at C = 32, T = 24 (the synthetic
+// N = 4096 config) instead of the split path (A/B)
+static bool tail_ct24(const GtuTailArgs& a) {
+  static const bool on = getenv("DSTAGNN_TAIL_CT24") && atoi(getenv("DSTAGNN_TAIL_CT24")) != 0;
+  return on && a.C == 32 && a.T == 24;
+}
 bool tail_split_fwd(const GtuTailArgs& a) {
   static const int split_t = getenv("DSTAGNN_TAIL_SPLIT_T") ? atoi(getenv("DSTAGNN_TAIL_SPLIT_T")) : kTailSplitT;
+  if (tail_ct24(a) && split_t > 0) return false;
   return fwd_lds(a, true) > 32 * 1024 || a.T >= split_t;
 }
 bool tail_split_bwd(const GtuTailArgs& a) {
   static const int split_t = getenv("DSTAGNN_TAIL_SPLIT_T") ? atoi(getenv("DSTAGNN_TAIL_SPLIT_T")) : kTailSplitT;
+  if (tail_ct24(a) && split_t > 0) return false;
   return bwd_lds(a, true) > 32 * 1024 || a.T >= split_t;
 }
 
@@ -916,6 +924,13 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
     return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, false, 2, 256>, fwd_lds(a, false, false, 256), a, st, 256);
   }
   const size_t lds = fwd_lds(a, true);
+  if (tail_ct24(a)) {
+    const dim3 g(node_grid(a.BN));
+    if (a.first) hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 24, 256, 1, true>), g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gtu_tail_fwd_ct_kernel<32, 24, 256, 1, false>), g, dim3(256), 0, st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   if (a.C == 32 && a.T == 12 && tail_ct()) {
     const dim3 g(node_grid(a.BN));
     if (tail_ct() == 2) {
@@ -958,6 +973,13 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
     return 0;
   }
   const size_t lds = bwd_lds(a, true);
+  if (tail_ct24(a) && !generic) {
+    const dim3 g(node_grid(a.BN));
+    if (a.first) hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 24, 256, 1, true>), g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 24, 256, 1, false>), g, dim3(256), 0, st, a);
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   if (a.C == 32 && a.T == 12 && !generic && tail_ct()) {
     const dim3 g(node_grid(a.BN));
     if (tail_ct() == 2) {

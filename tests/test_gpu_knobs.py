@@ -9,9 +9,11 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_SDDMM_NOPF=1 the aggregate-first SDDMM without its batch prefetch (4 waves per SIMD)
   DSTAGNN_GTU_TCONV=0  the GTU input gradient as the K-concatenated GEMM (run_gemm_kcat)
   DSTAGNN_GTU_GCONV=1  the GTU forward convolutions by the sliding-window kernel (gtu_tconv.hip)
+  DSTAGNN_TAIL_CT24=1  the compile-time GTU tail kernels at T = 24 instead of the split path
 
-PEMS08 geometry (the bench's default path otherwise), inner block with a broadcast res_att,
-eval and train mode, same bounds as tests/test_gpu_parity.py::test_block_vs_oracle_configs."""
+PEMS08 geometry (the bench's default path otherwise; t24 for the T = 24 switches), inner block
+with a broadcast res_att in eval and train mode plus the first block, same bounds as
+tests/test_gpu_parity.py::test_block_vs_oracle_configs."""
 import os
 import subprocess
 import sys
@@ -26,21 +28,25 @@ SCRIPT = """
 import sys
 sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
 import test_gpu_parity as T
-T._run_config_vs_oracle("pems08", False, 4)
-T._run_config_vs_oracle("pems08", False, 4, train=True)
+T._run_config_vs_oracle({cfg!r}, False, {B})
+T._run_config_vs_oracle({cfg!r}, False, {B}, train=True)
+T._run_config_vs_oracle({cfg!r}, True, 2)
 print("KNOB_OK")
 """
 
 
-@pytest.mark.parametrize("env", ["DSTAGNN_DE_OMAP=1", "DSTAGNN_TAT_MFMA=0", "DSTAGNN_SIDE_CUMASK=0x11111111",
-                                 "DSTAGNN_SDDMM_NOPF=1", "DSTAGNN_GTU_TCONV=0", "DSTAGNN_GTU_GCONV=1"])
-def test_knob_path_vs_oracle(env):
+@pytest.mark.parametrize("env,cfg,B", [("DSTAGNN_DE_OMAP=1", "pems08", 4), ("DSTAGNN_TAT_MFMA=0", "pems08", 4),
+                                       ("DSTAGNN_SIDE_CUMASK=0x11111111", "pems08", 4),
+                                       ("DSTAGNN_SDDMM_NOPF=1", "pems08", 4), ("DSTAGNN_GTU_TCONV=0", "pems08", 4),
+                                       ("DSTAGNN_GTU_GCONV=1", "pems08", 4), ("DSTAGNN_GTU_GCONV=1", "t24", 2),
+                                       ("DSTAGNN_TAIL_CT24=1", "t24", 2)])
+def test_knob_path_vs_oracle(env, cfg, B):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     k, v = env.split("=", 1)
     e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
     e[k] = v
-    code = SCRIPT.format(root=ROOT, tests=os.path.join(ROOT, "tests"))
+    code = SCRIPT.format(root=ROOT, tests=os.path.join(ROOT, "tests"), cfg=cfg, B=B)
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=e, capture_output=True, text=True, timeout=170)
     assert r.returncode == 0 and "KNOB_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

@@ -29,6 +29,12 @@ for s in "${S[@]}"; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    cfgab)  # same-box A/B of one env knob on BASELINE configs: CFGAB_ENV="K=V", CFGAB_CONFIGS="SYN GAMBIA"
+            for r in 1 2; do
+              BENCH_CONFIGS_STEPS=5 run cfgab_base_$r 300 python tools/bench_configs.py ${CFGAB_CONFIGS:-SYN}
+              env ${CFGAB_ENV:-DSTAGNN_TAIL_CT24=1} BENCH_CONFIGS_STEPS=5 timeout -k 10 300 python tools/bench_configs.py ${CFGAB_CONFIGS:-SYN} > gpurun_out/cfgab_knob_$r.log 2>&1 || exit $?
+              grep -h "ms_per_step" gpurun_out/cfgab_base_$r.log gpurun_out/cfgab_knob_$r.log | grep configs
+            done ;;
     mstep)  run mstep 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mstep -o run --output-format csv -- python3 tools/model_step_prof.py --steps 5 ;;
     dp2)    DSTAGNN_DIST_BACKEND=gloo DSTAGNN_DEVICE_MOD=1 run dp2 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-extras ;;
     pmcs)   echo "== pmcs ($(date +%T))"; bash tools/pmc_step.sh || exit $? ;;
