@@ -861,10 +861,11 @@ int rows_gemm(const float* A, int lda, const float* B, Idx2 bk, Idx2 bn, float* 
 // (measured: SYN T=24 step 60.9 -> 57.7 ms split; PEMS08 T=12 0.91 fused vs 0.99 split);
 // DSTAGNN_TAIL_SPLIT_T overrides the threshold (0 = always split, used by the parity runs)
 constexpr int kTailSplitT = 20;
-// DSTAGNN_TAIL_CT24=1: the compile-time tail kernels also at C = 32, T = 24 (the synthetic
-// N = 4096 config) instead of the split path (A/B)
+// The compile-time tail kernels also at C = 32, T = 24 (the synthetic N = 4096 config) instead
+// of the split path: SYN B=32 40.2 -> 37.4-37.7 ms/step same box (2 x 2 runs,
+// tools/gpu_check.sh cfgab); DSTAGNN_TAIL_CT24=0 keeps the split path (A/B)
 static bool tail_ct24(const GtuTailArgs& a) {
-  static const bool on = getenv("DSTAGNN_TAIL_CT24") && atoi(getenv("DSTAGNN_TAIL_CT24")) != 0;
+  static const bool on = !getenv("DSTAGNN_TAIL_CT24") || atoi(getenv("DSTAGNN_TAIL_CT24")) != 0;
   return on && a.C == 32 && a.T == 24;
 }
 bool tail_split_fwd(const GtuTailArgs& a) {

@@ -9,7 +9,7 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_SDDMM_NOPF=1 the aggregate-first SDDMM without its batch prefetch (4 waves per SIMD)
   DSTAGNN_GTU_TCONV=0  the GTU input gradient as the K-concatenated GEMM (run_gemm_kcat)
   DSTAGNN_GTU_GCONV=1  the GTU forward convolutions by the sliding-window kernel (gtu_tconv.hip)
-  DSTAGNN_TAIL_CT24=1  the compile-time GTU tail kernels at T = 24 instead of the split path
+  DSTAGNN_TAIL_CT24=0  the split GTU tail path at T = 24 instead of the compile-time kernels
 
 PEMS08 geometry (the bench's default path otherwise; t24 for the T = 24 switches), inner block
 with a broadcast res_att in eval and train mode plus the first block, same bounds as
@@ -39,7 +39,7 @@ print("KNOB_OK")
                                        ("DSTAGNN_SIDE_CUMASK=0x11111111", "pems08", 4),
                                        ("DSTAGNN_SDDMM_NOPF=1", "pems08", 4), ("DSTAGNN_GTU_TCONV=0", "pems08", 4),
                                        ("DSTAGNN_GTU_GCONV=1", "pems08", 4), ("DSTAGNN_GTU_GCONV=1", "t24", 2),
-                                       ("DSTAGNN_TAIL_CT24=1", "t24", 2)])
+                                       ("DSTAGNN_TAIL_CT24=0", "t24", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
     import torch
     if not torch.cuda.is_available():

@@ -38,6 +38,9 @@ for s in "${S[@]}"; do
     mstep)  run mstep 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mstep -o run --output-format csv -- python3 tools/model_step_prof.py --steps 5 ;;
     dp2)    DSTAGNN_DIST_BACKEND=gloo DSTAGNN_DEVICE_MOD=1 run dp2 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-extras ;;
     pmcs)   echo "== pmcs ($(date +%T))"; bash tools/pmc_step.sh || exit $? ;;
+    pmcsum) # summarise the PMC passes on the box so the bench below reads this build's traffic
+            python3 tools/pmc_step_summary.py gpurun_out/pmcs profiles/block_pmc.json > gpurun_out/pmcsum.log 2>&1 \
+              && cp profiles/block_pmc.json gpurun_out/block_pmc.json || exit $? ;;
     pmcs_gambia) echo "== pmcs GAMBIA ($(date +%T))"; PMC_CONFIG=GAMBIA bash tools/pmc_step.sh || exit $? ;;
     pmcs_syn)    echo "== pmcs SYN ($(date +%T))"; PMC_CONFIG=SYN bash tools/pmc_step.sh || exit $? ;;
     pmcb)   echo "== pmcb ($(date +%T))"; bash tools/pmc_block.sh || exit $?; python3 tools/pmc_block_summary.py gpurun_out/pmcb > gpurun_out/pmcb_summary.txt ;;
