@@ -463,7 +463,65 @@ struct SideStream {
   std::atomic<uint32_t> fnext{0};
   bool use_flags = true;
   bool side_flags = false;  // DSTAGNN_SYNC_EVENTS=2: flags for the side stream's signals too
+  bool ksig = true;         // fork flags written by the next main-stream kernel (DSTAGNN_KSIG=0: off)
   bool ok = false;
+};
+
+}  // namespace
+
+// the pending kernel-written signal of this host thread (common.hpp); one at a time: a fork
+// flushes the previous one first
+namespace {
+struct PendingSig {
+  hipStream_t st = nullptr;    // the writer's (main) stream
+  hipStream_t side = nullptr;  // the waiting stream
+  uint32_t* p = nullptr;
+  uint32_t v = 0;
+};
+thread_local PendingSig t_sig;
+}  // namespace
+
+StreamSig peek_stream_sig(hipStream_t st) {
+  StreamSig s;
+  if (t_sig.p && t_sig.st == st) { s.p = t_sig.p; s.v = t_sig.v; }
+  return s;
+}
+static int sig_wait(const PendingSig& s) {
+  const hipError_t r = hipStreamWaitValue32(s.side, s.p, s.v, hipStreamWaitValueGte, 0xffffffffu);
+  if (r != hipSuccess) {
+    set_last_error(std::string("side stream: ") + hipGetErrorString(r));
+    return (int)r;
+  }
+  return 0;
+}
+int stream_sig_sent(hipStream_t st, const StreamSig& s) {
+  if (!(t_sig.p && t_sig.st == st && t_sig.p == s.p && t_sig.v == s.v)) return 0;
+  const PendingSig q = t_sig;
+  t_sig = PendingSig{};
+  return sig_wait(q);  // the writer is queued: now the side's wait
+}
+static void set_stream_sig(hipStream_t st, hipStream_t side, uint32_t* p, uint32_t v) {
+  t_sig.st = st;
+  t_sig.side = side;
+  t_sig.p = p;
+  t_sig.v = v;
+}
+int flush_stream_sig() {
+  if (!t_sig.p) return 0;
+  const PendingSig s = t_sig;
+  t_sig = PendingSig{};
+  const hipError_t r = hipStreamWriteValue32(s.st, s.p, s.v, 0);
+  if (r != hipSuccess) {
+    set_last_error(std::string("side stream: ") + hipGetErrorString(r));
+    return (int)r;
+  }
+  return sig_wait(s);
+}
+
+namespace {
+// every exit of a block op (errors included) releases a side-stream wait still queued
+struct SigFlushGuard {
+  ~SigFlushGuard() { (void)flush_stream_sig(); }
 };
 
 SideStream* side_stream_for_device() {
@@ -494,6 +552,7 @@ SideStream* side_stream_for_device() {
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     s.use_flags = !events || atoi(getenv("DSTAGNN_SYNC_EVENTS")) == 2;
     s.side_flags = events && atoi(getenv("DSTAGNN_SYNC_EVENTS")) == 2;
+    s.ksig = s.use_flags && (!getenv("DSTAGNN_KSIG") || atoi(getenv("DSTAGNN_KSIG")) != 0);
     if (s.use_flags) {
       if (hipMalloc(&s.flags, sizeof(uint32_t) * SideStream::kSlots) != hipSuccess ||
           hipMemset(s.flags, 0, sizeof(uint32_t) * SideStream::kSlots) != hipSuccess ||
@@ -527,6 +586,13 @@ struct SyncTok {
 // stream waits for it.  Flag words rotate over kSlots; numbers only grow, so a wait can only
 // be released by its own write or a later one issued behind it.  DSTAGNN_SYNC_EVENTS=1: events
 // both ways; =2: flags both ways.
+// Kernel-written fork flags (fork_k; default, DSTAGNN_KSIG=0 for the hipStreamWriteValue32
+// above): the flag is stored by workgroup 0 of the next kernel the main stream launches that
+// carries the signal (common.hpp) — every earlier kernel of the stream has completed when it
+// starts — and the side's wait is queued right after that launch, before the side's work: the
+// writer always precedes the wait in host order (a first version queued the wait at the fork
+// and hung with a CU-masked side stream).  tools/flag_sync_probe.hip modes 4 / 5: 0 stale
+// reads in 300 rounds each way.
 struct Streams {
   hipStream_t st = nullptr, sd = nullptr;
   SideStream* ss = nullptr;
@@ -553,6 +619,9 @@ struct Streams {
     return r == hipSuccess ? 0 : fail(r);
   }
   int wait(hipStream_t to, const SyncTok& t) {
+    // the main stream about to wait for the side: a signal the side may be waiting for goes
+    // out first (else both would wait for each other)
+    if (to == st) DS_TRY(flush_stream_sig());
     hipError_t r = hipSuccess;
     if (t.slot >= 0)
       r = hipStreamWaitValue32(to, ss->flags + t.slot, t.seq, hipStreamWaitValueGte, 0xffffffffu);
@@ -567,6 +636,17 @@ struct Streams {
     return wait(to, t);
   }
   int fork() { return event_pair(st, sd); }  // side sees everything the main chain issued so far
+  // the same dependency, its flag carried by the NEXT kernel launched on the main stream (if it
+  // can carry one; else flushed).  The caller issues that main-stream launch BEFORE any side
+  // work that depends on the fork: the side's wait is queued when the signal goes out.
+  int fork_k() {
+    if (!(ss && ss->ksig && st != sd)) return fork();
+    DS_TRY(flush_stream_sig());
+    const int slot = (int)(ss->fnext.fetch_add(1, std::memory_order_relaxed) % SideStream::kSlots);
+    const uint32_t seq = ss->gseq.fetch_add(1, std::memory_order_relaxed) + 1;
+    set_stream_sig(st, sd, ss->flags + slot, seq);
+    return 0;
+  }
   int join() { return event_pair(sd, st); }  // main waits for everything issued on the side
 };
 
@@ -797,6 +877,7 @@ struct Fwd {
     static const bool prof = getenv("DSTAGNN_HOST_PROFILE") != nullptr;
     static const bool conc = !getenv("DSTAGNN_FWD_CONCURRENT") || atoi(getenv("DSTAGNN_FWD_CONCURRENT")) != 0;
     HostTimer ht(prof, "fwd");
+    SigFlushGuard sig_guard;
     ks.init(st);
     const bool split = conc && ks.sd != st && !params_forked;
     DS_TRY(stage_params());
@@ -854,6 +935,7 @@ struct Bwd {
   Streams ks;
   hipStream_t sd = nullptr;  // side stream (== st when disabled)
   ChebFl fl;
+  bool defer_mask = false;  // stage_cheb forked the mask gradient; stage_sat issues it
   ChebFl flash_args() {
     ChebFl f = make_fl(m, p, gr, s);
     f.dzs = w.dzs; f.dzs_r = w.dzs_r; f.cc = w.cc; f.dqk = w.dqk;
@@ -861,6 +943,9 @@ struct Bwd {
     return f;
   }
   int fork() { return ks.fork(); }
+  int fork_k() { return ks.fork_k(); }
+  // a fork_k's signal went out (or was flushed): side work may be issued
+  int fork_k_done() { return flush_stream_sig(); }
   int join() { return ks.join(); }
   // a point on the side stream that the main stream can wait for later (wait_side)
   SyncTok dx_ready;
@@ -917,8 +1002,39 @@ struct Bwd {
     t.gpart = w.gcon_t; t.bpart = w.gcon_t + m.BN * m.C;
     if (m.first) { t.rpart = w.bcon_t; t.dpart = w.bcon_t + m.BN * m.C; }
     DS_TRY(op_gtu_tail_bwd(t, st));
-    // --- side: LN / residual / fcmy / GTU parameter gradients (one fork)
-    DS_TRY(fork());
+    DS_TRY(fork_k());
+    {
+      // gpre = (X > 0) * (dX + sum_q sum_{(j',o)} dconv_pad_q[bn,t+j',o] W_q[o,c,ks-1-j']): the three
+      // transposed convolutions as ONE K-concatenated product (K = 2C (3 + 5 + 7)), with the
+      // tail's dX as the beta input and the ReLU backward of the Chebyshev output in the epilogue
+      Gemm segs[3];
+      for (int q = 0; q < 3; ++q) {
+        const int ks = m.ks[q];
+        const int64_t C2 = 2 * (int64_t)m.C;
+        Gemm& g = segs[q];
+        g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
+        // row (bn, t) of the padded layout sits at (bn T + t) C2 (node stride T C2): a
+        // single-level row map (cheap prologue / epilogue row offsets)
+        g.A = w.dconv[q]; g.am = idx1(C2); g.ak = idx1(1);
+        g.B = s.Wgb[q]; g.bk = idx1(m.C); g.bn = idx1(1);  // flipped (j', o, c)
+        g.C = w.dX; g.cm = idx1(m.C); g.cn = idx1(1);
+      }
+      segs[0].beta = 1.f;
+      segs[0].Cout = w.gpre; segs[0].emask = s.X;  // fused ReLU backward of the cheb output
+      if (tconv_on() && gtu_tconv_ok(m.C, m.ks, 3)) {
+        // the same product as one sliding-window kernel: each tile stages the union of its
+        // rows' windows once (gtu_tconv.hip)
+        TconvArgs tc;
+        for (int q = 0; q < 3; ++q) { tc.dconv[q] = w.dconv[q]; tc.wflip[q] = s.Wgb[q]; tc.ks[q] = m.ks[q]; }
+        tc.dX = w.dX; tc.X = s.X; tc.gpre = w.gpre; tc.M = m.BN * m.T;
+        DS_TRY(op_gtu_tconv(tc, st));
+      } else {
+        DS_TRY(run_gemm_kcat(segs, 3, st));
+      }
+    }
+    // --- side: LN / residual / fcmy / GTU parameter gradients (one fork; its flag rides on
+    // the GTU input-gradient launch, issued first)
+    DS_TRY(fork_k_done());
     DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + m.BN * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
                     {w.bcon_t + m.BN * m.C, m.first ? gd.res_b : nullptr}}, m.BN, m.C, 1));
     // the bias gradients ride on their weight-gradient GEMMs as a column-sum column
@@ -955,35 +1071,6 @@ struct Bwd {
       }
       if (nw) DS_TRY(run_gemm_group(dws, nw, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd));
     }
-    {
-      // gpre = (X > 0) * (dX + sum_q sum_{(j',o)} dconv_pad_q[bn,t+j',o] W_q[o,c,ks-1-j']): the three
-      // transposed convolutions as ONE K-concatenated product (K = 2C (3 + 5 + 7)), with the
-      // tail's dX as the beta input and the ReLU backward of the Chebyshev output in the epilogue
-      Gemm segs[3];
-      for (int q = 0; q < 3; ++q) {
-        const int ks = m.ks[q];
-        const int64_t C2 = 2 * (int64_t)m.C;
-        Gemm& g = segs[q];
-        g.M = (int)(m.BN * m.T); g.N = m.C; g.K = (int)C2 * ks;
-        // row (bn, t) of the padded layout sits at (bn T + t) C2 (node stride T C2): a
-        // single-level row map (cheap prologue / epilogue row offsets)
-        g.A = w.dconv[q]; g.am = idx1(C2); g.ak = idx1(1);
-        g.B = s.Wgb[q]; g.bk = idx1(m.C); g.bn = idx1(1);  // flipped (j', o, c)
-        g.C = w.dX; g.cm = idx1(m.C); g.cn = idx1(1);
-      }
-      segs[0].beta = 1.f;
-      segs[0].Cout = w.gpre; segs[0].emask = s.X;  // fused ReLU backward of the cheb output
-      if (tconv_on() && gtu_tconv_ok(m.C, m.ks, 3)) {
-        // the same product as one sliding-window kernel: each tile stages the union of its
-        // rows' windows once (gtu_tconv.hip)
-        TconvArgs tc;
-        for (int q = 0; q < 3; ++q) { tc.dconv[q] = w.dconv[q]; tc.wflip[q] = s.Wgb[q]; tc.ks[q] = m.ks[q]; }
-        tc.dX = w.dX; tc.X = s.X; tc.gpre = w.gpre; tc.M = m.BN * m.T;
-        DS_TRY(op_gtu_tconv(tc, st));
-      } else {
-        DS_TRY(run_gemm_kcat(segs, 3, st));
-      }
-    }
     return 0;
   }
 
@@ -994,14 +1081,18 @@ struct Bwd {
     if (m.agg) {
       // aggregate-first (cheb_agg.hip).  Side stream: dx += the Chebyshev path's gradient
       // (transposed SpMM of g, Theta on the matrix cores) and dTheta_k = agg_k^T g, both from g
-      // alone; main: the SDDMM dW = <x_i, Theta_k g_j^T> (flash: dzs and c) for the softmax backward
+      // alone; main: the SDDMM dW = <x_i, Theta_k g_j^T> (flash: dzs and c) for the softmax backward.
+      // (One fork after the SDDMM for the side's SpMM, dTheta and mask gradient together
+      // measured 0.705 vs 0.703 ms/step, same box: the SpMM then starts later.)
       ChebAg a = make_ag(B, N, K, F, C, m.T, &gr);
       a.x = x; a.thcat = s.thcat; a.P = s.P; a.agg = s.xth; a.g = w.gpre; a.dW = w.dW; a.dx = dx; a.dx_beta = 1.f;
       if (m.flash) {
         a.nnz = (int)m.nnz; a.wsupp = s.wsupp; a.psupp = s.psupp; a.tsupp = gr.tsupp; a.dzs = w.dzs; a.cc = w.cc;
         if (m.fsmall) { a.csc2csr = gr.csc2csr; a.dzs_r = w.dzs_r; }
       }
-      DS_TRY(fork());
+      DS_TRY(fork_k());  // its flag rides on the SDDMM, issued before the side's work
+      DS_TRY(op_cheb_agg_sddmm(a, st));
+      DS_TRY(fork_k_done());
       DS_TRY(op_cheb_agg_spmm_t(a, sd));
       DS_TRY(mark_side(&dx_ready));
       {
@@ -1019,7 +1110,6 @@ struct Bwd {
         DS_TRY(sgemm(g));
         if (!adjacent) DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sd));
       }
-      DS_TRY(op_cheb_agg_sddmm(a, st));
     } else if (m.sparse) {
       // dW is written on the support only; the softmax backward reads it only where
       // T_k != 0 (no memset)
@@ -1066,6 +1156,11 @@ struct Bwd {
       DS_TRY(op_cheb_softmax_bwd(sm, st));
     }
     // --- side: mask and Theta gradients
+    if (m.flash && m.agg) {  // the flag rides on the flash dQ'/dK' launch (stage_sat), issued first
+      DS_TRY(fork_k());
+      defer_mask = true;
+      return 0;
+    }
     DS_TRY(fork());
     if (m.flash) DS_TRY(op_flash_mask_grad(fl, sd));
     else DS_TRY(op_cheb_mask_grad(sm, sd));
@@ -1106,6 +1201,11 @@ struct Bwd {
     const float sc = 1.f / sqrtf((float)m.dk);
     const int64_t ld = 2 * m.KD;
     if (m.flash) DS_TRY(op_flash_dqk(fl, st));  // dQ' | dK' with P tiles recomputed, no dense dz
+    if (defer_mask) {  // side: the mask gradient (stage_cheb's fork_k)
+      defer_mask = false;
+      DS_TRY(fork_k_done());
+      DS_TRY(op_flash_mask_grad(fl, sd));
+    }
     if (!m.flash) {  // dQ'[b,i,k,:] = sum_j dz[b,k,i,j] K'[b,j,k,:] / sqrt(dk)
       Gemm g;
       g.M = m.N; g.N = m.dk; g.K = m.N; g.batch = m.B * m.K;
@@ -1149,8 +1249,11 @@ struct Bwd {
       }
       DS_TRY(op_ln_bwd(a, st));
     }
-    // --- side: SAt projection, EmbedS gamma / beta / pos-embedding, pre_conv bias and weight grads
-    DS_TRY(fork());
+    // --- side: SAt projection, EmbedS gamma / beta / pos-embedding, pre_conv bias and weight
+    // grads; the fork's flag rides on the pre_conv data-gradient GEMM, issued first
+    DS_TRY(fork_k());
+    DS_TRY(stage_preconv());
+    DS_TRY(fork_k_done());
     if (gd.sat_wq || gd.sat_wk) {  // side: [dW_Q'; dW_K'] = dqk^T Zd, then split
       Gemm g;
       g.M = (int)ld; g.N = m.D; g.K = (int)m.BN;
@@ -1226,23 +1329,21 @@ struct Bwd {
     float* dsc = (d.res_mode == DSTAGNN_RES_FULL && dres) ? dres : w.dscore;
     float* dsum = (d.res_mode == DSTAGNN_RES_BCAST && dres) ? dres : nullptr;
     DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, dsum, st));
-    // --- side: TAt LN gamma / beta, fc and Q|K|V weight grads (one fork)
-    DS_TRY(fork());
-    if (tat_part()) {
-      const int64_t pb = ln_bwd_part_blocks(m.BFT);
-      DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1));
-    } else {
-      DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
-    }
-    if (gd.tat_fc) {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
-      Gemm g;
-      g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
-      g.A = w.dU; g.am = idx1(1); g.ak = idx1(N);
-      g.B = s.ctx; g.bk = idx1(m.HV); g.bn = idx1(1);
-      g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
-      DS_TRY(sgemm(g));
-    }
-    if (wqkv_side()) DS_TRY(tat_wqkv_grad(true));
+    // --- side: TAt LN gamma / beta, fc and Q|K|V weight grads (one fork; its flag rides on the
+    // dE GEMM, issued first)
+    DS_TRY(fork_k());
+    auto side_work = [&]() -> int {
+      DS_TRY(fork_k_done());
+      if (tat_part()) {
+        const int64_t pb = ln_bwd_part_blocks(m.BFT);
+        DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1));
+      } else {
+        DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
+      }
+      if (gd.tat_fc && fc_side()) DS_TRY(sgemm(fc_grad_gemm()));
+      if (wqkv_side()) DS_TRY(tat_wqkv_grad(true));
+      return 0;
+    };
     {  // dE = dU + dqkv [Wq; Wk; Wv]
       Gemm g;
       g.M = (int)m.BFT; g.N = m.N; g.K = (int)m.QW;
@@ -1257,15 +1358,17 @@ struct Bwd {
         // inner block: E is x transposed, so dE accumulates straight into dx (B,N,F,T) through
         // the output map (row (b, ft), column n -> b N FT + n FT + ft) once the side stream's
         // Chebyshev-path gradient is in dx
-        DS_TRY(wait_side(dx_ready));
+        DS_TRY(wait_side(dx_ready));  // (flushes the fork_k's signal first)
         g.Cout = dx; g.omap = true; g.obeta = 1.f;
         g.om = idx2(m.FT, 1, N * m.FT); g.on = idx1(m.FT);
-        return gemm(g);
+        DS_TRY(gemm(g));
+        return side_work();
       } else {
         g.Cout = w.dE;
       }
       DS_TRY(gemm(g));
     }
+    DS_TRY(side_work());
     // dE -> dx
     if (m.first) {
       LnBwd a;
@@ -1317,8 +1420,25 @@ struct Bwd {
     static const bool on = getenv("DSTAGNN_WQKV_SIDE") && atoi(getenv("DSTAGNN_WQKV_SIDE")) != 0;
     return on;
   }
+  // the TAt fc weight gradient on the side stream (DSTAGNN_FC_SIDE=1) or, by default, on the
+  // main stream with the Q|K|V weight gradient as one grouped launch at the step's end: with the
+  // main chain's fork flags kernel-written the side stream's tail set the step (two-stream
+  // timeline: main ended ~48 us before the side)
+  static bool fc_side() {
+    static const bool on = getenv("DSTAGNN_FC_SIDE") && atoi(getenv("DSTAGNN_FC_SIDE")) != 0;
+    return on;
+  }
+  Gemm fc_grad_gemm() {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
+    Gemm g;
+    g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
+    g.A = w.dU; g.am = idx1(1); g.ak = idx1(m.N);
+    g.B = s.ctx; g.bk = idx1(m.HV); g.bn = idx1(1);
+    g.C = gd.tat_fc; g.cm = idx1(m.HV); g.cn = idx1(1);
+    return g;
+  }
   int tat_wqkv_grad(bool side) {
-    if (!(gd.tat_wq || gd.tat_wk || gd.tat_wv)) return 0;
+    const bool fc_here = !side && !fc_side() && gd.tat_fc;
+    if (!(gd.tat_wq || gd.tat_wk || gd.tat_wv)) return fc_here ? gemm(fc_grad_gemm()) : 0;
     hipStream_t q = side ? sd : st;
     const int64_t N = m.N;
     Gemm g;
@@ -1327,7 +1447,12 @@ struct Bwd {
     g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
     const bool adjacent = gd.tat_wq && gd.tat_wk == gd.tat_wq + m.HQ * N && gd.tat_wv == gd.tat_wk + m.HQ * N;
     g.C = adjacent ? gd.tat_wq : w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
-    DS_TRY(side ? sgemm(g) : gemm(g));
+    if (fc_here) {
+      const Gemm gs[2] = {g, fc_grad_gemm()};
+      DS_TRY(run_gemm_group(gs, 2, w.gemm_ws, kGemmWs, st));
+    } else {
+      DS_TRY(side ? sgemm(g) : gemm(g));
+    }
     if (!adjacent) {
       PackRows pk;
       pk.n = 3; pk.cols = m.N; pk.unpack = 1;
@@ -1341,6 +1466,7 @@ struct Bwd {
   int run() {
     static const bool prof = getenv("DSTAGNN_HOST_PROFILE") != nullptr;
     HostTimer ht(prof, "bwd");
+    SigFlushGuard sig_guard;
     ks.init(st);
     sd = ks.sd;
     ht.lap("init");
@@ -1348,13 +1474,12 @@ struct Bwd {
     ht.lap("tail");
     DS_TRY(stage_cheb());
     ht.lap("cheb");
-    DS_TRY(stage_sat());
+    DS_TRY(stage_sat());  // + stage_preconv
     ht.lap("sat");
-    DS_TRY(stage_preconv());
-    ht.lap("preconv");
     DS_TRY(stage_tat());
     ht.lap("tat");
-    if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));
+    if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));  // (+ the fc weight gradient)
+    else if (!fc_side() && gd.tat_fc) DS_TRY(gemm(fc_grad_gemm()));
     DS_TRY(join());
     ht.lap("join");
     return 0;

@@ -209,6 +209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<
 template <int kNQ, int KM, bool PF = agg_prefetch<kNQ>()>  // kNQ >= min(F*T, 1024) / 64
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<kNQ, KM, PF>(), 8))) void cheb_agg_sddmm_kernel(ChebAg a) {
   extern __shared__ float Dg[];  // [waves][K][F * T]
+  stream_sig_store(a.sig, a.sig_v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
   if (wv >= (int64_t)a.B * a.N) return;
@@ -549,11 +550,15 @@ int op_cheb_agg_fwd(const ChebAg& a0, hipStream_t st) {
 
 int op_cheb_agg_sddmm(const ChebAg& a0, hipStream_t st) {
   DS_TRY(check(a0));
-  const ChebAg a = with_order(a0);
+  ChebAg a = with_order(a0);
+  const StreamSig sg = peek_stream_sig(st);  // carries a pending stream signal (common.hpp)
+  a.sig = sg.p;
+  a.sig_v = sg.v;
   const int FT = a.F * a.T;
   const size_t lds = sddmm_lds_bytes(a.K, a.F, a.T);
   dispatch<SddmmL>(nq_of(std::min(FT, 1024)), km_of(a.K), Launch{a, dim3(grid_rows((int64_t)a.B * a.N)), lds, st});
   DS_CHECK_LAUNCH();
+  if (sg.p) DS_TRY(stream_sig_sent(st, sg));
   return 0;
 }
 

@@ -208,6 +208,7 @@ __global__ __launch_bounds__(256) void flash_colc_kernel(ChebFl a) {
 
 // backward: dQ'.  One wave per (b, k, 32 rows i), independent (own LDS slice).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flash_dq_kernel(ChebFl a) {
+  stream_sig_store(a.sig, a.sig_v);
   __shared__ float Kt[4][32][33];
   __shared__ float lse_t[4][32], c_t[4][32];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
@@ -544,6 +545,7 @@ __device__ __forceinline__ void lds16(const float* X, int row, int c0, float (&v
 // 1 (no constraint) for 3 / 4 tiles per wave
 template <int kSmallTiles, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void flash_small_dqk_kernel(ChebFl a) {
+  stream_sig_store(a.sig, a.sig_v);
   extern __shared__ float X[];  // [(32 nt)][32] operand rows (>= kRedF floats), then lse [32 nt], c [32 nt] (dQ)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const int nt = (a.N + 31) >> 5, NP = nt * 32;
@@ -826,7 +828,11 @@ int op_flash_colc(const ChebFl& a, hipStream_t st) {
   return 0;
 }
 
-int op_flash_dqk(const ChebFl& a, hipStream_t st) {
+int op_flash_dqk(const ChebFl& a0, hipStream_t st) {
+  ChebFl a = a0;  // the first launch carries a pending stream signal (common.hpp)
+  const StreamSig sg = peek_stream_sig(st);
+  a.sig = sg.p;
+  a.sig_v = sg.v;
   const int nt = (a.N + 31) >> 5;
   if (a.am) {  // small graphs (flash_small): dK' and dQ' strips in one launch
     const size_t lds = (std::max<size_t>((size_t)nt * 32 * 32, kRedF) + 2 * (size_t)nt * 32 + 2 * (size_t)kStripE) *
@@ -850,11 +856,13 @@ int op_flash_dqk(const ChebFl& a, hipStream_t st) {
       default: set_last_error("flash: graph too large for the small-graph kernels"); return DSTAGNN_E_SHAPE;
     }
     DS_CHECK_LAUNCH();
+    if (sg.p) DS_TRY(stream_sig_sent(st, sg));
     return 0;
   }
   hipLaunchKernelGGL(flash_dq_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
   DS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(flash_dk_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a);
+  if (sg.p) DS_TRY(stream_sig_sent(st, sg));
+  hipLaunchKernelGGL(flash_dk_kernel, dim3(grid_waves((int64_t)a.B * a.K * nt)), dim3(256), 0, st, a0);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -236,6 +236,35 @@ void set_last_error(const std::string& s);
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ---------------------------------------------------------------------------------
+// kernel-written stream signals (block.hip Streams::fork_k): a fork from the block's main
+// stream to its side stream leaves the flag write PENDING for the next kernel launched on the
+// main stream that can carry it (the GEMMs, the GTU input-gradient kernel, the aggregate-first
+// SDDMM, the flash dQ / dK kernels): that kernel's workgroup 0 stores the flag as it starts —
+// every earlier kernel of the stream has completed by then — instead of a
+// hipStreamWriteValue32 (a ~4.5 us ROCclr kernel plus its dispatch gap on the critical path).
+// A launcher reads the pending signal (peek_stream_sig), passes it to its kernel and, once the
+// launch succeeded, calls stream_sig_sent, which queues the side stream's wait for the flag —
+// so the writer is always queued BEFORE the wait (no dependence on how streams map to hardware
+// queues, nor on whether a wait can block the host).  A signal nobody consumed is written by
+// flush_stream_sig() (write on main, then the side's wait), which runs before the main stream
+// waits for the side stream and when the block's op returns (also on its error paths).  The
+// block issues no side-stream work between a fork_k and the launch that carries its signal.
+// ---------------------------------------------------------------------------------
+struct StreamSig {
+  uint32_t* p = nullptr;
+  uint32_t v = 0;
+};
+StreamSig peek_stream_sig(hipStream_t st);  // the pending signal for st, or {}
+int stream_sig_sent(hipStream_t st, const StreamSig& s);  // a launch on st carried s: queue the wait
+int flush_stream_sig();  // a pending signal nobody consumed: hipStreamWriteValue32, then the wait
+
+// workgroup 0, thread 0: a vector store (system scope, release) of the signal, if any
+__device__ __forceinline__ void stream_sig_store(uint32_t* p, uint32_t v) {
+  if (p != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ---------------------------------------------------------------------------------
 // internal GEMM entry (gemm.hip)
 // ---------------------------------------------------------------------------------
 struct Gemm {

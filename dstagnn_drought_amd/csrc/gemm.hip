@@ -31,7 +31,9 @@ namespace {
 
 // out[zb][m][n] = epilogue( sum_s ws[zb][s][m][n] ).  A workgroup takes 256/G outputs and
 // G split groups per output (G = power of two ~ splitk/8, per problem), combined by an LDS
-// tree.  Grouped like the GEMM: problem p owns workgroups [start[p], start[p+1]).
+// tree.  Consecutive threads take consecutive outputs of one split group (thread = q per + c),
+// so one load instruction of a wave touches 64 / per slab rows (per contiguous floats each)
+// instead of G slab rows of 64 / G floats.  Same sums in the same order.  Grouped like the GEMM: problem p owns workgroups [start[p], start[p+1]).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmG gin) {
   __shared__ float red[256];
   uint32_t lbid, lnwg;
@@ -40,7 +42,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmG gin) {
   const int64_t MN = (int64_t)g.M * g.N;
   const int64_t total = (int64_t)g.batch * MN;
   const int per = 256 / G;
-  const int c = threadIdx.x / G, q = threadIdx.x % G;
+  const int c = threadIdx.x % per, q = threadIdx.x / per;
   const int64_t idx = (int64_t)lbid * per + c;
   float s = 0.f;
   if (idx < total) {
@@ -59,10 +61,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmG gin) {
     for (; sp < g.splitk; sp += G) s += p[(int64_t)sp * MN];
     s = (s + s1) + (s2 + s3);
   }
-  red[threadIdx.x] = s;
+  red[threadIdx.x] = s;  // = red[q per + c]
   __syncthreads();
   for (int w = G / 2; w > 0; w >>= 1) {
-    if (q < w) red[threadIdx.x] += red[threadIdx.x + w];
+    if (q < w) red[threadIdx.x] += red[threadIdx.x + w * per];
     __syncthreads();
   }
   if (q == 0 && idx < total) {
@@ -676,13 +678,16 @@ void persist_slices(Plan* const* ps, int n, int ktiles_per_tile0 = -1) {
   }
 }
 
-void launch_plans(Plan* const* ps, int n, hipStream_t st) {
+int launch_plans(Plan* const* ps, int n, hipStream_t st) {
   const GemmK* ks[kGroupMax];
   uint32_t counts[kGroupMax];
   if (ps[0]->persist) persist_slices(ps, n);
   for (int p = 0; p < n; ++p) { ks[p] = &ps[p]->k; counts[p] = ps[p]->slice(); }
   GemmG gg;
   const uint32_t grid = make_group(ks, counts, n, &gg);
+  const StreamSig sg = peek_stream_sig(st);
+  gg.sig = sg.p;
+  gg.sig_v = sg.v;
   using Unit = void (*)(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
   static const Unit units[3][3][2] = {
       {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}},
@@ -692,10 +697,13 @@ void launch_plans(Plan* const* ps, int n, hipStream_t st) {
   if (pl.persist) {
     static const Unit punits[3][2] = {{gemm_p0_k0, gemm_p0_k1}, {nullptr, nullptr}, {gemm_p2_k0, gemm_p2_k1}};
     punits[pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, false, st);
-    return;
+  } else {
+    const int var = pl.acc2 ? 2 : (g_bf16 ? 1 : 0);
+    units[var][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, pl.hot, st);
   }
-  const int var = pl.acc2 ? 2 : (g_bf16 ? 1 : 0);
-  units[var][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, pl.hot, st);
+  DS_CHECK_LAUNCH();
+  if (sg.p) DS_TRY(stream_sig_sent(st, sg));
+  return 0;
 }
 
 }  // namespace
@@ -737,7 +745,7 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
     int j = i + 1;
     while (j < nl && j - i < kGroupMax && live[j]->same_kernel(*live[i])) ++j;
     if (live[i]->skinny) launch_skinny(live[i]->sk, st);
-    else launch_plans(live + i, j - i, st);
+    else DS_TRY(launch_plans(live + i, j - i, st));
     DS_CHECK_LAUNCH();
     if (gemm_log_on()) {
       fprintf(stderr, "[gemm] %s", live[i]->log);
@@ -827,6 +835,9 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
   gg.start[0] = (uint32_t)n;  // K-concatenated
   for (int p = 1; p < 4; ++p) gg.start[p] = grid;
   for (int p = 0; p < n; ++p) gg.k[p] = plans[p].k;
+  const StreamSig sg = peek_stream_sig(st);
+  gg.sig = sg.p;
+  gg.sig_v = sg.v;
   using Unit = void (*)(const GemmG&, dim3, bool, bool, int, int, bool, hipStream_t);
   static const Unit units[2][3][2] = {
       {{gemm_c0_k0, gemm_c0_k1}, {gemm_c1_k0, gemm_c1_k1}, {gemm_c2_k0, gemm_c2_k1}},
@@ -837,6 +848,7 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
   else
     units[g_bf16 ? 1 : 0][pl.best][pl.ktwo ? 1 : 0](gg, dim3(grid), pl.akc, pl.bnc, pl.va, pl.vb, false, st);
   DS_CHECK_LAUNCH();
+  if (sg.p) DS_TRY(stream_sig_sent(st, sg));
   if (gemm_log_on()) {
     fprintf(stderr, "[gemm] kcat %s", plans[0].log);
     for (int q = 1; q < n; ++q) fprintf(stderr, " + %s", plans[q].log);

@@ -56,6 +56,8 @@ struct GemmG {
   // with problem 0's epilogue.
   uint32_t start[4];
   GemmK k[kGroupMax];
+  uint32_t* sig;  // kernel-written stream signal (common.hpp), read by workgroup 0 only
+  uint32_t sig_v, sig_pad;
 };
 
 namespace {
@@ -385,6 +387,7 @@ template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int
           bool ACC2 = false>
 __device__ __forceinline__ void gemm_glds_body(const GemmG& gin) {
   constexpr int BK = 32;
+  stream_sig_store(gin.sig, gin.sig_v);
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   constexpr int NA = BM * BK / (256 * VA), NB = BN * BK / (256 * VB);  // DMA instructions per thread per k-tile
   constexpr int LA1 = BM * BK / 256, LB1 = BN * BK / 256;              // element DMAs of the partial tile
@@ -822,6 +825,7 @@ __device__ __forceinline__ void wait_vm_barrier_rt(int n) {
 template <int WGM, int WGN, int WM, int WN, bool A_KC, bool B_NC, bool KTWO, int VA, int VB, bool KCAT, int PNS>
 __device__ __forceinline__ void gemm_persist_body(const GemmG& gin) {
   constexpr int BK = 32, NS = PNS;
+  stream_sig_store(gin.sig, gin.sig_v);
   constexpr int BM = 32 * WM * WGM, BN = 32 * WN * WGN;
   constexpr int NA = BM * BK / (256 * VA), NB = BN * BK / (256 * VB);
   constexpr int LA1 = BM * BK / 256, LB1 = BN * BK / 256;

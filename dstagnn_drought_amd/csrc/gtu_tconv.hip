@@ -69,6 +69,7 @@ __device__ __forceinline__ void tc_load_a(const TconvArgs& a, int q, int64_t m0,
 // current GTU's last tap (the grid gives ~2 waves per SIMD at PEMS08, so the registers are
 // spent on keeping loads in flight instead of on occupancy).
 __global__ __launch_bounds__(256) void gtu_tconv_kernel(TconvArgs a) {
+  stream_sig_store(a.sig, a.sig_v);
   __shared__ float As[kTcRowsMax * kTcRow];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int64_t m0 = (int64_t)blockIdx.x * kTcBM;
@@ -276,9 +277,14 @@ int op_gtu_tconv(const TconvArgs& a, hipStream_t st) {
     flops += 2.0 * a.M * kTcC * (double)(kTcCin * a.ks[q]);
     bytes += 4.0 * ((double)(a.M + a.ks[q] - 1) * kTcCin + (double)kTcCin * a.ks[q] * kTcC);
   }
+  TconvArgs b = a;  // carries a pending stream signal (common.hpp)
+  const StreamSig sg = peek_stream_sig(st);
+  b.sig = sg.p;
+  b.sig_v = sg.v;
   void* rec = gemm_prof_begin(flops, bytes, st);
-  hipLaunchKernelGGL(gtu_tconv_kernel, dim3((unsigned)cdiv64(a.M, kTcBM)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(gtu_tconv_kernel, dim3((unsigned)cdiv64(a.M, kTcBM)), dim3(256), 0, st, b);
   DS_CHECK_LAUNCH();
+  if (sg.p) DS_TRY(stream_sig_sent(st, sg));
   gemm_prof_end(rec, st);
   return 0;
 }

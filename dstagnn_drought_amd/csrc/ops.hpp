@@ -185,6 +185,7 @@ struct ChebAg {
   float* dzs = nullptr; float* dzs_r = nullptr; const int* csc2csr = nullptr; float* cc = nullptr;  // support terms
   float* dx = nullptr; float dx_beta = 1.f;  // spmm_t: dx = dx_beta dx + (the Chebyshev path's gradient)
   int xcd_order = 0;
+  uint32_t* sig = nullptr; uint32_t sig_v = 0;  // kernel-written stream signal (SDDMM; common.hpp)
 };
 bool cheb_agg_ok(int F, int C, int K, int T);
 int op_cheb_agg_fwd(const ChebAg& a, hipStream_t st);
@@ -215,6 +216,7 @@ struct ChebFl {
   const int* apa_idx = nullptr;            // (N,N) A_pa-CSC index or -1
   const int* apa2t = nullptr;              // (apa_nnz) union-support CSC position or -1
   float* dzs_r = nullptr;                  // (B,K,nnz) dzs in CSR order (the SDDMM writes it)
+  uint32_t* sig = nullptr; uint32_t sig_v = 0;  // kernel-written stream signal (common.hpp)
 };
 bool flash_small(int N);  // the LDS-staged small-graph kernels (N <= 512)
 int op_flash_forward(const ChebFl& a, hipStream_t st);   // lse, psupp, wsupp
@@ -237,6 +239,7 @@ struct TconvArgs {
   const float* X;         // (M, C) the Chebyshev output (ReLU mask)
   float* gpre;            // (M, C) result
   int64_t M;              // rows B*N*T
+  uint32_t* sig = nullptr; uint32_t sig_v = 0;  // kernel-written stream signal (common.hpp)
 };
 bool gtu_tconv_ok(int C, const int* ks, int n);
 // the three GTU convolutions (forward) by the same sliding window (gtu_tconv.hip)

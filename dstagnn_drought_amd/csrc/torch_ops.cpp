@@ -700,14 +700,21 @@ void adam_step(at::TensorList params, at::TensorList grads, at::TensorList exp_a
   c10::DeviceGuard guard(params[0].device());
   const int64_t ce = dstagnn_adam_chunk_elems();
   std::vector<dstagnn_adam_seg> segs(n);
+  std::vector<Tensor> gcopy;  // contiguous copies of strided gradients, alive until the launch is queued
+  gcopy.reserve(n);
   int64_t nchunk = 0;
   for (size_t i = 0; i < n; ++i) {
-    for (const Tensor* t : {&params[i], &grads[i], &exp_avgs[i], &exp_avg_sqs[i]}) {
+    const Tensor* g = &grads[i];
+    if (g->defined() && g->is_cuda() && !g->is_contiguous()) {
+      gcopy.push_back(g->contiguous());
+      g = &gcopy.back();
+    }
+    for (const Tensor* t : {&params[i], g, &exp_avgs[i], &exp_avg_sqs[i]}) {
       check_dev(*t, at::kFloat, "adam_step tensor");
       TORCH_CHECK(t->device() == params[0].device(), "adam_step: tensors on different devices");
       TORCH_CHECK(t->numel() == params[i].numel(), "adam_step: param / grad / state sizes differ");
     }
-    segs[i] = {params[i].data_ptr<float>(), grads[i].data_ptr<float>(), exp_avgs[i].data_ptr<float>(),
+    segs[i] = {params[i].data_ptr<float>(), g->data_ptr<float>(), exp_avgs[i].data_ptr<float>(),
                exp_avg_sqs[i].data_ptr<float>(), params[i].numel()};
     nchunk += (params[i].numel() + ce - 1) / ce;
   }

@@ -192,6 +192,45 @@ class HipAdam(torch.optim.Optimizer):
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        # per group, after a step whose gradient-carrying parameters all shared one step count:
+        # (params list, which params had a gradient, those params, their state dicts,
+        # exp_avgs, exp_avg_sqs, step).  The per-parameter grouping below costs ~2 us per
+        # Parameter in Python (~0.3 ms at nb_block=4, with the GPU idle); the cached path
+        # gathers the gradients and launches while the same parameters carry gradients.
+        self._plans = {}
+
+    def load_state_dict(self, state_dict):
+        self._plans = {}
+        super().load_state_dict(state_dict)
+
+    def zero_grad(self, set_to_none=True):
+        """torch's zero_grad(set_to_none=True) spends ~1 us per parameter in profiler /
+        foreach bookkeeping (~0.15 ms at nb_block=4, before the forward can start); dropping
+        the references is all it does here."""
+        if not set_to_none:
+            return super().zero_grad(set_to_none=False)
+        for group in self.param_groups:
+            for p in group["params"]:
+                p.grad = None
+
+    def _fast_step(self, ops, group):
+        plan = self._plans.get(id(group))
+        params = group["params"]
+        if plan is None or plan[0] is not params or len(plan[1]) != len(params):
+            return False
+        grads = [p.grad for p in params]
+        if [g is not None for g in grads] != plan[1]:
+            return False
+        _, present, ps, states, ms, vs, t = plan
+        gs = [g for g in grads if g is not None]
+        t += 1
+        b1, b2 = group["betas"]
+        ops.adam_step(ps, gs, ms, vs, b1, b2, group["eps"], group["lr"] / (1.0 - b1 ** t),
+                      math.sqrt(1.0 - b2 ** t))
+        for st in states:
+            st["step"] = t
+        self._plans[id(group)] = plan[:6] + (t,)
+        return True
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -202,6 +241,9 @@ class HipAdam(torch.optim.Optimizer):
         from . import _lib
         ops = _lib.load()
         for group in self.param_groups:
+            if self._fast_step(ops, group):
+                continue
+            self._plans.pop(id(group), None)
             b1, b2 = group["betas"]
             lr, eps = group["lr"], group["eps"]
             by_step = {}
@@ -219,7 +261,7 @@ class HipAdam(torch.optim.Optimizer):
                 st["step"] += 1
                 lists = by_step.setdefault(st["step"], ([], [], [], []))
                 lists[0].append(p if p.is_contiguous() else p.data)
-                lists[1].append(g if g.is_contiguous() else g.contiguous())
+                lists[1].append(g)  # a strided gradient is copied contiguous by the op
                 lists[2].append(st["exp_avg"])
                 lists[3].append(st["exp_avg_sq"])
             for t, (ps, gs, ms, vs) in by_step.items():
@@ -228,6 +270,10 @@ class HipAdam(torch.optim.Optimizer):
                 step_size = lr / (1.0 - b1 ** t)
                 bc2_sqrt = math.sqrt(1.0 - b2 ** t)
                 ops.adam_step(ps, gs, ms, vs, b1, b2, eps, step_size, bc2_sqrt)
+            if len(by_step) == 1:
+                (t, (ps, _, ms, vs)), = by_step.items()
+                present = [p.grad is not None for p in group["params"]]
+                self._plans[id(group)] = (group["params"], present, ps, [self.state[p] for p in ps], ms, vs, t)
         return loss
 
 

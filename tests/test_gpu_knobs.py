@@ -10,6 +10,11 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_GTU_TCONV=0  the GTU input gradient as the K-concatenated GEMM (run_gemm_kcat)
   DSTAGNN_GTU_GCONV=1  the GTU forward convolutions by the sliding-window kernel (gtu_tconv.hip)
   DSTAGNN_TAIL_CT24=0  the split GTU tail path at T = 24 instead of the compile-time kernels
+  DSTAGNN_KSIG=0       main -> side stream forks signalled by hipStreamWriteValue32 instead of
+                       by the next main-stream kernel's prologue store (block.hip Streams::fork;
+                       the default path is held by every other GPU test)
+  DSTAGNN_FC_SIDE=1    the TAt fc weight gradient on the side stream instead of grouped with the
+                       Q|K|V weight gradient on the main stream
 
 PEMS08 geometry (the bench's default path otherwise; t24 for the T = 24 switches), inner block
 with a broadcast res_att in eval and train mode plus the first block, same bounds as
@@ -28,9 +33,9 @@ SCRIPT = """
 import sys
 sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
 import test_gpu_parity as T
-T._run_config_vs_oracle({cfg!r}, False, {B})
-T._run_config_vs_oracle({cfg!r}, False, {B}, train=True)
-T._run_config_vs_oracle({cfg!r}, True, 2)
+T._run_config_vs_oracle({cfg!r}, False, {B}, flash={flash!r})
+T._run_config_vs_oracle({cfg!r}, False, {B}, train=True, flash={flash!r})
+T._run_config_vs_oracle({cfg!r}, True, 2, flash={flash!r})
 print("KNOB_OK")
 """
 
@@ -39,7 +44,8 @@ print("KNOB_OK")
                                        ("DSTAGNN_SIDE_CUMASK=0x11111111", "pems08", 4),
                                        ("DSTAGNN_SDDMM_NOPF=1", "pems08", 4), ("DSTAGNN_GTU_TCONV=0", "pems08", 4),
                                        ("DSTAGNN_GTU_GCONV=1", "pems08", 4), ("DSTAGNN_GTU_GCONV=1", "t24", 2),
-                                       ("DSTAGNN_TAIL_CT24=0", "t24", 2)])
+                                       ("DSTAGNN_TAIL_CT24=0", "t24", 2), ("DSTAGNN_KSIG=0", "pems08", 4),
+                                       ("DSTAGNN_KSIG=0", "pems07+flash", 2), ("DSTAGNN_FC_SIDE=1", "pems08", 4)])
 def test_knob_path_vs_oracle(env, cfg, B):
     import torch
     if not torch.cuda.is_available():
@@ -47,6 +53,8 @@ def test_knob_path_vs_oracle(env, cfg, B):
     k, v = env.split("=", 1)
     e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
     e[k] = v
-    code = SCRIPT.format(root=ROOT, tests=os.path.join(ROOT, "tests"), cfg=cfg, B=B)
+    flash = True if cfg.endswith("+flash") else None  # "+flash": the streamed (large-graph) kernels forced on
+    cfg = cfg.split("+")[0]
+    code = SCRIPT.format(root=ROOT, tests=os.path.join(ROOT, "tests"), cfg=cfg, B=B, flash=flash)
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=e, capture_output=True, text=True, timeout=170)
     assert r.returncode == 0 and "KNOB_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

@@ -49,6 +49,11 @@ for s in "${S[@]}"; do
     trace_cfg) for c in GAMBIA SYN; do
                  BENCH_CONFIGS_STEPS=3 BENCH_CONFIGS_WARMUP=1 run trace_$c 300 rocprofv3 --kernel-trace --stats -d gpurun_out/trace_cfg_$c -o run --output-format csv -- python3 tools/bench_configs.py $c
                done ;;
+    serial_cfg) # serialised (one stream) trace + GEMM launch log of SERIAL_CFG (default GAMBIA)
+               c=${SERIAL_CFG:-GAMBIA}
+               DSTAGNN_SIDE_STREAM=0 DSTAGNN_GEMM_LOG=1 BENCH_CONFIGS_STEPS=2 BENCH_CONFIGS_WARMUP=1 \
+                 run serial_$c 300 rocprofv3 --kernel-trace -d gpurun_out/serial_$c -o run --output-format csv -- \
+                 python3 tools/bench_configs.py $c ;;
     sweep)  run gemm_sweep 600 python tools/gemm_sweep.py ;;
     sweep1) run gemm_sweep1 300 python tools/gemm_sweep.py --configs auto:auto --iters 50 ;;
     gemmref) run gemm_ref 300 python tools/torch_gemm_ref.py ;;
