@@ -670,6 +670,21 @@ struct Fwd {
   bool e_side = false;           // E = x transposed is issued on the side stream (token e_ready)
   SyncTok e_ready;
   ChebFl fl;
+  // the forward's side work (E, x Theta), forked by fork_k in run() and issued right after the
+  // Q|K|V GEMM, which carries the fork's flag
+  bool side_pending = false, side_xth_pending = false;
+  ChebIO side_io{};
+  int issue_fwd_side() {
+    if (!side_pending) return 0;
+    side_pending = false;
+    DS_TRY(flush_stream_sig());  // (no-op when the GEMM carried the flag)
+    if (!m.first) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
+      DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, (int64_t)m.N * m.FT, m.FT * m.N, 0.f, ks.sd));
+      DS_TRY(ks.signal(ks.sd, &e_ready));
+    }
+    if (side_xth_pending) DS_TRY(cheb_xtheta(side_io, w.gemm_ws_side, ks.sd));
+    return 0;
+  }
 
   int stage_tat() {
     const int64_t N = m.N;
@@ -701,6 +716,7 @@ struct Fwd {
       g.C = s.qkv; g.cm = idx1(m.QW); g.cn = idx1(1);
       DS_TRY(run_gemm(g, w.gemm_ws, kGemmWs, st));
     }
+    DS_TRY(issue_fwd_side());
     DS_TRY(op_tat_fwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, res, d.res_mode, re_at, s.att, s.ctx, st));
     // fc (:99)
     {
@@ -887,13 +903,11 @@ struct Fwd {
     // E = x transposed, which the main chain awaits by its own token (e_ready)
     const bool side_xth = split && !m.agg;
     if (split && (side_xth || !m.first)) {  // x Theta needs only x and Theta: it runs beside the whole attention chain
-      DS_TRY(ks.fork());
-      if (!m.first) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
-        DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, (int64_t)m.N * m.FT, m.FT * m.N, 0.f, ks.sd));
-        DS_TRY(ks.signal(ks.sd, &e_ready));
-        e_side = true;
-      }
-      if (side_xth) DS_TRY(cheb_xtheta(c, w.gemm_ws_side, ks.sd));
+      DS_TRY(ks.fork_k());  // issued after the Q|K|V GEMM (issue_fwd_side), which carries the flag
+      side_pending = true;
+      side_xth_pending = side_xth;
+      side_io = c;
+      e_side = !m.first;
     }
     DS_TRY(stage_tat());
     ht.lap("tat");
@@ -974,15 +988,18 @@ struct Bwd {
     float* part = q == st ? w.part : w.part_side;
     return op_colsum(in, A, O, I, out, 1, 0.f, part, kPart, q);
   }
-  // several same-shape column sums in one launch pair (side stream); null outputs skipped
-  int colsums(std::initializer_list<std::pair<const float*, float*>> io, int64_t A, int O, int I) {
+  // several same-shape column sums in one launch pair (side stream unless q is given); null
+  // outputs skipped
+  int colsums(std::initializer_list<std::pair<const float*, float*>> io, int64_t A, int O, int I,
+              hipStream_t q = nullptr) {
+    if (!q) q = sd;
     const float* ins[4];
     float* outs[4];
     int n = 0;
     for (const auto& q : io)
       if (q.second && n < 4) { ins[n] = q.first; outs[n] = q.second; ++n; }
     if (!n) return 0;
-    return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, sd == st ? w.part : w.part_side, kPart, sd);
+    return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, q == st ? w.part : w.part_side, kPart, q);
   }
   int gemm(const Gemm& g) { return run_gemm(g, w.gemm_ws, kGemmWs, st); }
   int sgemm(const Gemm& g) { return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd); }
@@ -1331,15 +1348,12 @@ struct Bwd {
     DS_TRY(op_tat_bwd(m.B, m.F, m.T, m.h, m.dk, m.dv, s.qkv, s.att, w.dctx, dre, w.dqkv, dsc, dsum, st));
     // --- side: TAt LN gamma / beta, fc and Q|K|V weight grads (one fork; its flag rides on the
     // dE GEMM, issued first)
-    DS_TRY(fork_k());
+    const bool side_any = tatln_side() || (gd.tat_fc && fc_side()) || wqkv_side();
+    if (side_any) DS_TRY(fork_k());
     auto side_work = [&]() -> int {
+      if (!side_any) return 0;
       DS_TRY(fork_k_done());
-      if (tat_part()) {
-        const int64_t pb = ln_bwd_part_blocks(m.BFT);
-        DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1));
-      } else {
-        DS_TRY(colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1));
-      }
+      if (tatln_side()) DS_TRY(tat_ln_colsums(sd));
       if (gd.tat_fc && fc_side()) DS_TRY(sgemm(fc_grad_gemm()));
       if (wqkv_side()) DS_TRY(tat_wqkv_grad(true));
       return 0;
@@ -1428,6 +1442,19 @@ struct Bwd {
     static const bool on = getenv("DSTAGNN_FC_SIDE") && atoi(getenv("DSTAGNN_FC_SIDE")) != 0;
     return on;
   }
+  // the TAt LayerNorm gamma / beta column sums: likewise on the main stream at the end by default
+  // (then the TAt stage forks nothing: no side-stream wait at the step's end); DSTAGNN_TATLN_SIDE=1
+  static bool tatln_side() {
+    static const bool on = getenv("DSTAGNN_TATLN_SIDE") && atoi(getenv("DSTAGNN_TATLN_SIDE")) != 0;
+    return on;
+  }
+  int tat_ln_colsums(hipStream_t q) {
+    if (tat_part()) {
+      const int64_t pb = ln_bwd_part_blocks(m.BFT);
+      return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1, q);
+    }
+    return colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1, q);
+  }
   Gemm fc_grad_gemm() {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
     Gemm g;
     g.M = m.N; g.N = (int)m.HV; g.K = (int)m.BFT;
@@ -1480,6 +1507,7 @@ struct Bwd {
     ht.lap("tat");
     if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));  // (+ the fc weight gradient)
     else if (!fc_side() && gd.tat_fc) DS_TRY(gemm(fc_grad_gemm()));
+    if (!tatln_side()) DS_TRY(tat_ln_colsums(st));
     DS_TRY(join());
     ht.lap("join");
     return 0;

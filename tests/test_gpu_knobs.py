@@ -15,6 +15,7 @@ a subprocess (the library reads its switches once per process):
                        the default path is held by every other GPU test)
   DSTAGNN_FC_SIDE=1    the TAt fc weight gradient on the side stream instead of grouped with the
                        Q|K|V weight gradient on the main stream
+  DSTAGNN_TATLN_SIDE=1 the TAt LayerNorm gamma / beta column sums on the side stream
 
 PEMS08 geometry (the bench's default path otherwise; t24 for the T = 24 switches), inner block
 with a broadcast res_att in eval and train mode plus the first block, same bounds as
@@ -45,7 +46,8 @@ print("KNOB_OK")
                                        ("DSTAGNN_SDDMM_NOPF=1", "pems08", 4), ("DSTAGNN_GTU_TCONV=0", "pems08", 4),
                                        ("DSTAGNN_GTU_GCONV=1", "pems08", 4), ("DSTAGNN_GTU_GCONV=1", "t24", 2),
                                        ("DSTAGNN_TAIL_CT24=0", "t24", 2), ("DSTAGNN_KSIG=0", "pems08", 4),
-                                       ("DSTAGNN_KSIG=0", "pems07+flash", 2), ("DSTAGNN_FC_SIDE=1", "pems08", 4)])
+                                       ("DSTAGNN_KSIG=0", "pems07+flash", 2), ("DSTAGNN_FC_SIDE=1", "pems08", 4),
+                                       ("DSTAGNN_TATLN_SIDE=1", "pems08", 4)])
 def test_knob_path_vs_oracle(env, cfg, B):
     import torch
     if not torch.cuda.is_available():
