@@ -988,11 +988,12 @@ struct Bwd {
     float* part = q == st ? w.part : w.part_side;
     return op_colsum(in, A, O, I, out, 1, 0.f, part, kPart, q);
   }
-  // several same-shape column sums in one launch pair (side stream unless q is given); null
+  // several same-shape column sums in one launch pair (side stream, or the main stream with
+  // on_main: the caller's stream may be the null stream, so no stream-valued sentinel); null
   // outputs skipped
   int colsums(std::initializer_list<std::pair<const float*, float*>> io, int64_t A, int O, int I,
-              hipStream_t q = nullptr) {
-    if (!q) q = sd;
+              bool on_main = false) {
+    const hipStream_t q = on_main ? st : sd;
     const float* ins[4];
     float* outs[4];
     int n = 0;
@@ -1353,7 +1354,7 @@ struct Bwd {
     auto side_work = [&]() -> int {
       if (!side_any) return 0;
       DS_TRY(fork_k_done());
-      if (tatln_side()) DS_TRY(tat_ln_colsums(sd));
+      if (tatln_side()) DS_TRY(tat_ln_colsums(false));
       if (gd.tat_fc && fc_side()) DS_TRY(sgemm(fc_grad_gemm()));
       if (wqkv_side()) DS_TRY(tat_wqkv_grad(true));
       return 0;
@@ -1448,12 +1449,12 @@ struct Bwd {
     static const bool on = getenv("DSTAGNN_TATLN_SIDE") && atoi(getenv("DSTAGNN_TATLN_SIDE")) != 0;
     return on;
   }
-  int tat_ln_colsums(hipStream_t q) {
+  int tat_ln_colsums(bool on_main) {
     if (tat_part()) {
       const int64_t pb = ln_bwd_part_blocks(m.BFT);
-      return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1, q);
+      return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1, on_main);
     }
-    return colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1, q);
+    return colsums({{w.gcon_a, gd.tat_ln_g}, {w.dO, gd.tat_ln_b}}, m.BFT, m.N, 1, on_main);
   }
   Gemm fc_grad_gemm() {  // dWfc[n,c] = sum_r dU[r,n] ctx[r,c]
     Gemm g;
@@ -1507,7 +1508,7 @@ struct Bwd {
     ht.lap("tat");
     if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));  // (+ the fc weight gradient)
     else if (!fc_side() && gd.tat_fc) DS_TRY(gemm(fc_grad_gemm()));
-    if (!tatln_side()) DS_TRY(tat_ln_colsums(st));
+    if (!tatln_side()) DS_TRY(tat_ln_colsums(true));
     DS_TRY(join());
     ht.lap("join");
     return 0;
