@@ -519,6 +519,31 @@ int flush_stream_sig() {
 }
 
 namespace {
+// Race probes (tests/test_gpu_knobs.py): DSTAGNN_DEBUG_MAIN_DELAY_US / DSTAGNN_DEBUG_SIDE_DELAY_US
+// put a bounded busy-wait kernel (<= 20 ms, one wave) on the main stream before every stage /
+// on the side stream after every fork, so a cross-stream read issued without its dependency
+// reads stale data instead of winning the race by timing (a missing fork once went unnoticed
+// because the side stream happened to reach the read late).
+__global__ void debug_delay_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+int debug_delay(hipStream_t q, bool on_main) {
+  static const int us_main = getenv("DSTAGNN_DEBUG_MAIN_DELAY_US") ? atoi(getenv("DSTAGNN_DEBUG_MAIN_DELAY_US")) : 0;
+  static const int us_side = getenv("DSTAGNN_DEBUG_SIDE_DELAY_US") ? atoi(getenv("DSTAGNN_DEBUG_SIDE_DELAY_US")) : 0;
+  const int us = std::min(on_main ? us_main : us_side, 20000);
+  if (us <= 0) return 0;
+  static const int rate_khz = [] {
+    int dev = 0, r = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&r, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+      r = 0;
+    return r > 0 ? r : 100000;
+  }();
+  hipLaunchKernelGGL(debug_delay_kernel, dim3(1), dim3(64), 0, q, (uint64_t)us * (uint64_t)rate_khz / 1000u);
+  DS_CHECK_LAUNCH();
+  return 0;
+}
+
 // every exit of a block op (errors included) releases a side-stream wait still queued
 struct SigFlushGuard {
   ~SigFlushGuard() { (void)flush_stream_sig(); }
@@ -635,7 +660,10 @@ struct Streams {
     DS_TRY(signal(from, &t));
     return wait(to, t);
   }
-  int fork() { return event_pair(st, sd); }  // side sees everything the main chain issued so far
+  int fork() {  // side sees everything the main chain issued so far
+    DS_TRY(event_pair(st, sd));
+    return sd != st ? debug_delay(sd, false) : 0;
+  }
   // the same dependency, its flag carried by the NEXT kernel launched on the main stream (if it
   // can carry one; else flushed).  The caller issues that main-stream launch BEFORE any side
   // work that depends on the fork: the side's wait is queued when the signal goes out.
@@ -678,6 +706,7 @@ struct Fwd {
     if (!side_pending) return 0;
     side_pending = false;
     DS_TRY(flush_stream_sig());  // (no-op when the GEMM carried the flag)
+    DS_TRY(debug_delay(ks.sd, false));
     if (!m.first) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
       DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, (int64_t)m.N * m.FT, m.FT * m.N, 0.f, ks.sd));
       DS_TRY(ks.signal(ks.sd, &e_ready));
@@ -909,10 +938,13 @@ struct Fwd {
       side_io = c;
       e_side = !m.first;
     }
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_tat());
     ht.lap("tat");
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_preconv());
     ht.lap("preconv");
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_sat());
     ht.lap("sat");
     if (split) {
@@ -920,9 +952,11 @@ struct Fwd {
       if (side_xth) DS_TRY(ks.join());
       DS_TRY(cheb_aggregate(c, w.gemm_ws, st));
     } else {
-      DS_TRY(stage_cheb());
+      DS_TRY(debug_delay(st, true));
+    DS_TRY(stage_cheb());
     }
     ht.lap("cheb");
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_tail(split));
     ht.lap("tail");
     return 0;
@@ -959,7 +993,10 @@ struct Bwd {
   int fork() { return ks.fork(); }
   int fork_k() { return ks.fork_k(); }
   // a fork_k's signal went out (or was flushed): side work may be issued
-  int fork_k_done() { return flush_stream_sig(); }
+  int fork_k_done() {
+    DS_TRY(flush_stream_sig());
+    return sd != st ? debug_delay(sd, false) : 0;
+  }
   int join() { return ks.join(); }
   // a point on the side stream that the main stream can wait for later (wait_side)
   SyncTok dx_ready;
@@ -1270,6 +1307,7 @@ struct Bwd {
     // --- side: SAt projection, EmbedS gamma / beta / pos-embedding, pre_conv bias and weight
     // grads; the fork's flag rides on the pre_conv data-gradient GEMM, issued first
     DS_TRY(fork_k());
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_preconv());
     DS_TRY(fork_k_done());
     if (gd.sat_wq || gd.sat_wk) {  // side: [dW_Q'; dW_K'] = dqk^T Zd, then split
@@ -1498,12 +1536,16 @@ struct Bwd {
     ks.init(st);
     sd = ks.sd;
     ht.lap("init");
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_tail());
     ht.lap("tail");
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_cheb());
     ht.lap("cheb");
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_sat());  // + stage_preconv
     ht.lap("sat");
+    DS_TRY(debug_delay(st, true));
     DS_TRY(stage_tat());
     ht.lap("tat");
     if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));  // (+ the fc weight gradient)

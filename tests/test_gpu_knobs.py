@@ -16,6 +16,10 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_FC_SIDE=1    the TAt fc weight gradient on the side stream instead of grouped with the
                        Q|K|V weight gradient on the main stream
   DSTAGNN_TATLN_SIDE=1 the TAt LayerNorm gamma / beta column sums on the side stream
+  DSTAGNN_DEBUG_MAIN_DELAY_US / DSTAGNN_DEBUG_SIDE_DELAY_US   race probes: a 1.5 ms busy-wait
+                       kernel on the main stream before every stage / on the side stream after
+                       every fork, so a cross-stream read without its dependency reads stale
+                       data (block.hip debug_delay); results must not change
 
 PEMS08 geometry (the bench's default path otherwise; t24 for the T = 24 switches), inner block
 with a broadcast res_att in eval and train mode plus the first block, same bounds as
@@ -47,7 +51,10 @@ print("KNOB_OK")
                                        ("DSTAGNN_GTU_GCONV=1", "pems08", 4), ("DSTAGNN_GTU_GCONV=1", "t24", 2),
                                        ("DSTAGNN_TAIL_CT24=0", "t24", 2), ("DSTAGNN_KSIG=0", "pems08", 4),
                                        ("DSTAGNN_KSIG=0", "pems07+flash", 2), ("DSTAGNN_FC_SIDE=1", "pems08", 4),
-                                       ("DSTAGNN_TATLN_SIDE=1", "pems08", 4)])
+                                       ("DSTAGNN_TATLN_SIDE=1", "pems08", 4),
+                                       ("DSTAGNN_DEBUG_MAIN_DELAY_US=1500", "pems08", 4),
+                                       ("DSTAGNN_DEBUG_SIDE_DELAY_US=1500", "pems08", 4),
+                                       ("DSTAGNN_DEBUG_MAIN_DELAY_US=1500", "pems07+flash", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
     import torch
     if not torch.cuda.is_available():
@@ -60,3 +67,24 @@ def test_knob_path_vs_oracle(env, cfg, B):
     code = SCRIPT.format(root=ROOT, tests=os.path.join(ROOT, "tests"), cfg=cfg, B=B, flash=flash)
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=e, capture_output=True, text=True, timeout=170)
     assert r.returncode == 0 and "KNOB_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_race_probe_catches_a_missing_fork():
+    """The main-stream delay probe against a library built with one cross-stream dependency
+    removed on purpose (the TAt LayerNorm column sums issued on the side stream without a
+    fork; built by the round's tooling into abtest/racebug, skipped when absent): the parity
+    check must FAIL there, i.e. the probe exposes a missing fork instead of hiding it."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    lib = os.path.join(ROOT, "abtest", "racebug", "libdstagnn.so")
+    if not os.path.exists(lib):
+        pytest.skip("no racy library variant in this tree")
+    e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", DSTAGNN_DEBUG_MAIN_DELAY_US="3000",
+             LD_LIBRARY_PATH=os.path.dirname(lib))
+    code = ("import sys\nsys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})\n"
+            "import test_gpu_parity as T\n"
+            "T._run_config_vs_oracle('pems08', False, 4, train=True)\nprint('KNOB_OK')\n"
+            ).format(root=ROOT, tests=os.path.join(ROOT, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=e, capture_output=True, text=True, timeout=170)
+    assert "KNOB_OK" not in r.stdout and "AssertionError" in r.stderr, (r.stdout[-1500:], r.stderr[-1500:])
