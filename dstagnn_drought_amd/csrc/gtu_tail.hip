@@ -244,8 +244,12 @@ __global__ __launch_bounds__(256) void gtu_gates_kernel(GtuTailArgs a, int nchun
 
 // Split path, gates backward: one (node, gate, 64-row chunk of the node's zero-padded (t', o)
 // rows, the shared-pad layout of the fused kernel) per 256-thread workgroup.  The dG slice is read along s (coalesced), transposed
-// through LDS to [t][c]; conv rows and the output rows are walked with o fastest.
-__global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int nchunk) {
+// through LDS to [t][c]; conv rows and the output rows are walked with o fastest.  vec (C % 4
+// == 0, 16-B aligned rows): a thread takes 4 channels c of one row and produces both halves
+// (dP | dQ) from one 16-B load of P and of Q — tanh / sigmoid once per (t, c), 16-B loads and
+// stores — instead of one output element per thread (each (P, Q) pair loaded and its
+// activations computed twice, 4-B accesses).
+__global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int nchunk, int vec) {
   extern __shared__ float lds[];
   const int C = a.C, T = a.T, S = 3 * T - 12, C2 = 2 * C, CP = C + 1;
   int id = blockIdx.x;
@@ -265,6 +269,33 @@ __global__ __launch_bounds__(256) void gtu_gates_bwd_kernel(GtuTailArgs a, int n
   __syncthreads();
   const float* cv = (gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2])) + bn * C2 * Tg;
   float* orow = (gi == 0 ? a.dconv_pad[0] : (gi == 1 ? a.dconv_pad[1] : a.dconv_pad[2])) + bn * (int64_t)C2 * T;
+  if (vec) {
+    const int C4 = C >> 2;
+    for (int e = tid; e < kGsW * C4; e += 256) {
+      const int tl = e / C4, c = (e - tl * C4) * 4, tp = tp0 + tl;
+      if (tp >= Lp) continue;
+      const int t = tp - (ks - 1);
+      float4 vp = make_float4(0.f, 0.f, 0.f, 0.f), vq = vp;
+      if (t >= 0 && t < Tg) {
+        const float4 p4 = *reinterpret_cast<const float4*>(cv + (int64_t)t * C2 + c);
+        const float4 q4 = *reinterpret_cast<const float4*>(cv + (int64_t)t * C2 + C + c);
+        const float* dl = lds + tl * CP + c;
+        const float pv[4] = {p4.x, p4.y, p4.z, p4.w}, qv[4] = {q4.x, q4.y, q4.z, q4.w};
+        float op[4], oq[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float th = fast_tanh(pv[j]), sg = fast_sigmoid(qv[j]), dg = dl[j];
+          op[j] = dg * (1.f - th * th) * sg;
+          oq[j] = dg * th * sg * (1.f - sg);
+        }
+        vp = make_float4(op[0], op[1], op[2], op[3]);
+        vq = make_float4(oq[0], oq[1], oq[2], oq[3]);
+      }
+      *reinterpret_cast<float4*>(orow + (int64_t)tp * C2 + c) = vp;
+      *reinterpret_cast<float4*>(orow + (int64_t)tp * C2 + C + c) = vq;
+    }
+    return;
+  }
   for (int e = tid; e < kGsW * C2; e += 256) {
     const int tl = e / C2, o = e - tl * C2, tp = tp0 + tl;
     if (tp >= Lp) continue;
@@ -968,8 +999,11 @@ int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
     const int nchunk = (a.T + 6 + kGsW - 1) / kGsW;  // rows of the longest padded output (ks = 7)
     const int64_t nwg = a.BN * 3 * nchunk;
     if (nwg >= (1ll << 31)) { set_last_error("gtu_gates_bwd: grid too large"); return DSTAGNN_E_SHAPE; }
+    bool vec = a.C % 4 == 0 && !(getenv("DSTAGNN_GATES_BWD_SCALAR") && atoi(getenv("DSTAGNN_GATES_BWD_SCALAR")));
+    for (int q = 0; q < 3; ++q)
+      vec = vec && (reinterpret_cast<uintptr_t>(a.conv[q]) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dconv_pad[q]) & 15) == 0;
     hipLaunchKernelGGL(gtu_gates_bwd_kernel, dim3((unsigned)nwg), dim3(256), sizeof(float) * kGsW * (a.C + 1), st, a,
-                       nchunk);
+                       nchunk, vec ? 1 : 0);
     DS_CHECK_LAUNCH();
     return 0;
   }
