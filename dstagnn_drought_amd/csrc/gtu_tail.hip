@@ -216,44 +216,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) void
 // chunk) per 256-thread workgroup.  Conv rows are read with c fastest (coalesced), the tile
 // is transposed through LDS ([c][s], odd stride) and written as 64-float G row segments.
 // Small LDS (C*65 floats), so many workgroups per CU: this is an HBM stream, not a chain.
-// vec (C % 4 == 0, S % 4 == 0, 16-B aligned rows): 16-B loads of 4 channels of P and Q per
-// thread and 16-B G stores along s (same per-element arithmetic).
 constexpr int kGsW = 64;
-__global__ __launch_bounds__(256) void gtu_gates_kernel(GtuTailArgs a, int nchunk, int vec) {
+__global__ __launch_bounds__(256) void gtu_gates_kernel(GtuTailArgs a, int nchunk) {
   extern __shared__ float lds[];
   const int C = a.C, T = a.T, S = 3 * T - 12, C2 = 2 * C;
   const int64_t bn = blockIdx.x / nchunk;
   const int s0 = (int)(blockIdx.x % nchunk) * kGsW;
   const int tid = threadIdx.x;
-  if (vec) {
-    const int C4 = C >> 2;
-    for (int e = tid; e < kGsW * C4; e += 256) {
-      const int sl = e / C4, c = (e - sl * C4) * 4, sidx = s0 + sl;
-      if (sidx < S) {
-        int gi, t;
-        gate_index(sidx, T, &gi, &t);
-        const int Tg = T - 2 - 2 * gi;
-        const float* cg = gi == 0 ? a.conv[0] : (gi == 1 ? a.conv[1] : a.conv[2]);
-        const float* cv = cg + (bn * Tg + t) * C2;
-        const float4 p4 = *reinterpret_cast<const float4*>(cv + c);
-        const float4 q4 = *reinterpret_cast<const float4*>(cv + C + c);
-        const float pv[4] = {p4.x, p4.y, p4.z, p4.w}, qv[4] = {q4.x, q4.y, q4.z, q4.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) lds[(c + j) * (kGsW + 1) + sl] = fast_tanh(pv[j]) * fast_sigmoid(qv[j]);
-      }
-    }
-    __syncthreads();
-    float* G = a.G + bn * (int64_t)C * S;
-    constexpr int W4 = kGsW / 4;
-    for (int e = tid; e < C * W4; e += 256) {
-      const int c = e / W4, sl = (e - c * W4) * 4;
-      if (s0 + sl < S) {
-        const float* l = lds + c * (kGsW + 1) + sl;
-        *reinterpret_cast<float4*>(G + (int64_t)c * S + s0 + sl) = make_float4(l[0], l[1], l[2], l[3]);
-      }
-    }
-    return;
-  }
   for (int e = tid; e < kGsW * C; e += 256) {
     const int sl = e / C, c = e - sl * C, sidx = s0 + sl;
     if (sidx < S) {
@@ -977,11 +946,8 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
       const int nchunk = (S + kGsW - 1) / kGsW;
       const int64_t nwg = a.BN * nchunk;
       if (nwg >= (1ll << 31)) { set_last_error("gtu_gates: grid too large"); return DSTAGNN_E_SHAPE; }
-      bool vec = a.C % 4 == 0 && S % 4 == 0 && (reinterpret_cast<uintptr_t>(a.G) & 15) == 0 &&
-                 !(getenv("DSTAGNN_GATES_SCALAR") && atoi(getenv("DSTAGNN_GATES_SCALAR")));
-      for (int q = 0; q < 3; ++q) vec = vec && (reinterpret_cast<uintptr_t>(a.conv[q]) & 15) == 0;
       hipLaunchKernelGGL(gtu_gates_kernel, dim3((unsigned)nwg), dim3(256), sizeof(float) * a.C * (kGsW + 1), st, a,
-                         nchunk, vec ? 1 : 0);
+                         nchunk);
       DS_CHECK_LAUNCH();
     }
     DS_TRY(rows_gemm(a.G, S, a.fcmy_w, idx1(1), idx1(S), a.tco, a.T, a.BN * a.C, a.T, S, a.fcmy_b, st));

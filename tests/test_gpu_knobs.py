@@ -16,8 +16,7 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_FC_SIDE=1    the TAt fc weight gradient on the side stream instead of grouped with the
                        Q|K|V weight gradient on the main stream
   DSTAGNN_TATLN_SIDE=1 the TAt LayerNorm gamma / beta column sums on the side stream
-  DSTAGNN_GATES_BWD_SCALAR=1 / DSTAGNN_GATES_SCALAR=1  the split-path GTU gates backward /
-                       forward one element per thread (T = 144)
+  DSTAGNN_GATES_BWD_SCALAR=1  the split-path GTU gates backward one element per thread (T = 144)
   DSTAGNN_DEBUG_MAIN_DELAY_US / DSTAGNN_DEBUG_SIDE_DELAY_US   race probes: a 1.5 ms busy-wait
                        kernel on the main stream before every stage / on the side stream after
                        every fork, so a cross-stream read without its dependency reads stale
@@ -57,8 +56,7 @@ print("KNOB_OK")
                                        ("DSTAGNN_DEBUG_MAIN_DELAY_US=1500", "pems08", 4),
                                        ("DSTAGNN_DEBUG_SIDE_DELAY_US=1500", "pems08", 4),
                                        ("DSTAGNN_DEBUG_MAIN_DELAY_US=1500", "pems07+flash", 2),
-                                       ("DSTAGNN_GATES_BWD_SCALAR=1", "t144k3", 2),
-                                       ("DSTAGNN_GATES_SCALAR=1", "t144k3", 2)])
+                                       ("DSTAGNN_GATES_BWD_SCALAR=1", "t144k3", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
     import torch
     if not torch.cuda.is_available():
