@@ -17,7 +17,21 @@ EXT_FLAGS := -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBC
 EXT_LIBS := -L$(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip \
 	-Ldstagnn_drought_amd -ldstagnn -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
 
-all: $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib
+# deliberately racy variant for the race-probe self-check (tests/test_gpu_knobs.py): the same
+# objects with block.o rebuilt under -DDSTAGNN_RACEBUG_NOFORK (never loaded by the package)
+RACEBUG := abtest/racebug/libdstagnn.so
+
+all: $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib $(RACEBUG)
+
+racebug: $(RACEBUG)
+
+build/racebug/block.o: dstagnn_drought_amd/csrc/block.hip dstagnn_drought_amd/csrc/*.hpp include/dstagnn.h
+	@mkdir -p build/racebug
+	$(HIPCC) $(CXXFLAGS) -DDSTAGNN_RACEBUG_NOFORK -c $< -o $@
+
+$(RACEBUG): $(filter-out build/block.o,$(OBJ)) build/racebug/block.o
+	@mkdir -p abtest/racebug
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 # FETCH_SIZE / WRITE_SIZE width calibration (tools/pmc_step.sh)
 tools/fetch_calib: tools/fetch_calib.hip
@@ -39,6 +53,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 clean:
-	rm -rf build $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib
+	rm -rf build $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib abtest/racebug
 
-.PHONY: all clean
+.PHONY: all clean racebug

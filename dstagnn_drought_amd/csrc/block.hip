@@ -518,6 +518,14 @@ int flush_stream_sig() {
   return sig_wait(s);
 }
 
+// DSTAGNN_DEBUG_STREAMS=1: the fork invariant check (Bwd::sq)
+static bool stream_debug() {
+  static const bool on = getenv("DSTAGNN_DEBUG_STREAMS") && atoi(getenv("DSTAGNN_DEBUG_STREAMS")) != 0;
+  return on;
+}
+// a fork signal for `side` is pending: its writer (and so the side's wait) is not queued yet
+static bool side_sig_pending(hipStream_t side) { return t_sig.p && t_sig.side == side; }
+
 namespace {
 // Race probes (tests/test_gpu_knobs.py): DSTAGNN_DEBUG_MAIN_DELAY_US / DSTAGNN_DEBUG_SIDE_DELAY_US
 // put a bounded busy-wait kernel (<= 20 ms, one wave) on the main stream before every stage /
@@ -565,10 +573,16 @@ SideStream* side_stream_for_device() {
     // DSTAGNN_SIDE_CUMASK=0x<32-bit pattern>: the side stream confined to the CUs the pattern
     // selects (replicated over every 32-CU word; A/B knob: the side stream's weight-gradient
     // GEMMs otherwise take CUs from the latency-bound main chain); no priority with a mask
+    // (hipExtStreamCreateWithCUMask takes no flags: that stream is BLOCKING, so with a caller on
+    // the legacy null stream it also serialises with it — measurements under this knob include
+    // that serialisation)
     const char* cm = getenv("DSTAGNN_SIDE_CUMASK");
     if (cm && *cm) {
       const uint32_t pat = (uint32_t)strtoul(cm, nullptr, 0);
-      std::vector<uint32_t> mask(8, pat);  // 256 CUs
+      int ncu = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, pat);  // one 32-bit word per 32 CUs
+      if (ncu % 32) mask.back() &= (1u << (ncu % 32)) - 1u;
       if (hipExtStreamCreateWithCUMask(&s.side, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
     } else if (hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, lo) != hipSuccess) {
       return nullptr;
@@ -618,6 +632,15 @@ struct SyncTok {
 // writer always precedes the wait in host order (a first version queued the wait at the fork
 // and hung with a CU-masked side stream).  tools/flag_sync_probe.hip modes 4 / 5: 0 stale
 // reads in 300 rounds each way.
+// This relies on the HIP runtime setting the AQL barrier bit on every same-stream dispatch (a
+// kernel's workgroup 0 starts only once every earlier kernel of the stream has completed; true
+// for ROCm 7.2's in-order streams).  Nothing checks it at run time: after a runtime upgrade run
+// the race probes (tests/test_gpu_knobs.py, DSTAGNN_DEBUG_*_DELAY_US with the default
+// DSTAGNN_KSIG=1; tools/gpu_check.sh knobs) before trusting the flags; DSTAGNN_KSIG=0 falls
+// back to hipStreamWriteValue32.
+// Invariant (asserted under DSTAGNN_DEBUG_STREAMS=1, stream_check_side): no side-stream work is
+// issued while a fork's signal is still pending, i.e. every side wait is queued after its writer
+// and before the side work that depends on it.
 struct Streams {
   hipStream_t st = nullptr, sd = nullptr;
   SideStream* ss = nullptr;
@@ -953,7 +976,7 @@ struct Fwd {
       DS_TRY(cheb_aggregate(c, w.gemm_ws, st));
     } else {
       DS_TRY(debug_delay(st, true));
-    DS_TRY(stage_cheb());
+      DS_TRY(stage_cheb());
     }
     ht.lap("cheb");
     DS_TRY(debug_delay(st, true));
@@ -998,6 +1021,17 @@ struct Bwd {
     return sd != st ? debug_delay(sd, false) : 0;
   }
   int join() { return ks.join(); }
+  // the side stream for a launch; DSTAGNN_DEBUG_STREAMS=1 checks the fork invariant (Streams):
+  // side work issued while a fork's signal is still pending would not be ordered after the fork
+  // (its wait is not queued yet) — recorded here, returned as an error at the next stage boundary
+  int order_err = 0;
+  hipStream_t sq() {
+    if (stream_debug() && sd != st && side_sig_pending(sd) && !order_err) {
+      set_last_error("stream invariant: side-stream work issued before its fork's signal went out");
+      order_err = DSTAGNN_E_ARG;
+    }
+    return sd;
+  }
   // a point on the side stream that the main stream can wait for later (wait_side)
   SyncTok dx_ready;
   int mark_side(SyncTok* t) {
@@ -1030,7 +1064,7 @@ struct Bwd {
   // outputs skipped
   int colsums(std::initializer_list<std::pair<const float*, float*>> io, int64_t A, int O, int I,
               bool on_main = false) {
-    const hipStream_t q = on_main ? st : sd;
+    const hipStream_t q = on_main ? st : sq();
     const float* ins[4];
     float* outs[4];
     int n = 0;
@@ -1040,7 +1074,7 @@ struct Bwd {
     return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, q == st ? w.part : w.part_side, kPart, q);
   }
   int gemm(const Gemm& g) { return run_gemm(g, w.gemm_ws, kGemmWs, st); }
-  int sgemm(const Gemm& g) { return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd); }
+  int sgemm(const Gemm& g) { return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sq()); }
 
   int stage_tail() {
     GtuTailArgs t;  // LN / residual backward -> dtc -> dG = dtc W -> gates backward, per node
@@ -1124,7 +1158,7 @@ struct Bwd {
           DS_TRY(colsum_on(sd, w.dconv[q], m.BN * m.T + ks - 1, (int)C2, 1, gd.gtu_b[q]));
         }
       }
-      if (nw) DS_TRY(run_gemm_group(dws, nw, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sd));
+      if (nw) DS_TRY(run_gemm_group(dws, nw, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sq()));
     }
     return 0;
   }
@@ -1148,7 +1182,7 @@ struct Bwd {
       DS_TRY(fork_k());  // its flag rides on the SDDMM, issued before the side's work
       DS_TRY(op_cheb_agg_sddmm(a, st));
       DS_TRY(fork_k_done());
-      DS_TRY(op_cheb_agg_spmm_t(a, sd));
+      DS_TRY(op_cheb_agg_spmm_t(a, sq()));
       DS_TRY(mark_side(&dx_ready));
       {
         Gemm g;  // dTheta[(k,f), c] = sum_{b,j,t} agg[b,j,k,f,t] g[b,j,t,c]
@@ -1163,7 +1197,7 @@ struct Bwd {
           g.C = w.dthcat; g.cm = idx2(F, KC, C); g.cn = idx1(1);
         }
         DS_TRY(sgemm(g));
-        if (!adjacent) DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sd));
+        if (!adjacent) DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sq()));
       }
     } else if (m.sparse) {
       // dW is written on the support only; the softmax backward reads it only where
@@ -1178,7 +1212,7 @@ struct Bwd {
       // dxth = W^T g on the side stream (only the Theta / x gradients, also on the side,
       // read it), dW = (x Theta) g^T on the support on the main chain: independent products
       DS_TRY(fork());
-      DS_TRY(op_cheb_spmm_t_bwd(sp, sd));
+      DS_TRY(op_cheb_spmm_t_bwd(sp, sq()));
       DS_TRY(op_cheb_sddmm_bwd(sp, st));
     } else {
       {
@@ -1217,8 +1251,8 @@ struct Bwd {
       return 0;
     }
     DS_TRY(fork());
-    if (m.flash) DS_TRY(op_flash_mask_grad(fl, sd));
-    else DS_TRY(op_cheb_mask_grad(sm, sd));
+    if (m.flash) DS_TRY(op_flash_mask_grad(fl, sq()));
+    else DS_TRY(op_cheb_mask_grad(sm, sq()));
     if (m.agg) return 0;  // Theta and x gradients came with the aggregate-first kernels above
     {
       Gemm g;  // dTheta_cat[f,(k,c)] = sum_{b,i,t} x[b,i,f,t] dxth[b,i,t,k,c]
@@ -1235,7 +1269,7 @@ struct Bwd {
         g.C = w.dthcat; g.cm = idx1(KC); g.cn = idx1(1);
       }
       DS_TRY(sgemm(g));
-      if (!adjacent) DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sd));
+      if (!adjacent) DS_TRY(unpack_theta(w.dthcat, K, F, C, gd.theta, sq()));
     }
     {
       Gemm g;  // dx[b,i,f,t] += sum_{k,c} Theta_k[f,c] dxth[b,i,t,k,c]
@@ -1259,7 +1293,7 @@ struct Bwd {
     if (defer_mask) {  // side: the mask gradient (stage_cheb's fork_k)
       defer_mask = false;
       DS_TRY(fork_k_done());
-      DS_TRY(op_flash_mask_grad(fl, sd));
+      DS_TRY(op_flash_mask_grad(fl, sq()));
     }
     if (!m.flash) {  // dQ'[b,i,k,:] = sum_j dz[b,k,i,j] K'[b,j,k,:] / sqrt(dk)
       Gemm g;
@@ -1324,7 +1358,7 @@ struct Bwd {
         pk.n = 2; pk.cols = m.D; pk.unpack = 1;
         pk.src[0] = w.dWqk; pk.rows[0] = (int)m.KD; pk.rows[1] = (int)m.KD;
         pk.dst[0] = gd.sat_wq; pk.dst[1] = gd.sat_wk;
-        DS_TRY(op_pack_rows(pk, sd));
+        DS_TRY(op_pack_rows(pk, sq()));
       }
     }
     // gamma / beta: column sums of the LN backward's partial slabs (or contribution tensors)
@@ -1335,7 +1369,7 @@ struct Bwd {
     DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}, {xpart, xpart ? gd.pre_conv_b : nullptr}},
                    ln_bwd_partials_ok(m.D) ? ln_bwd_part_blocks(m.BN) : m.BN, m.D, 1));
     if (!xpart) DS_TRY(colsum_on(sd, w.dY, m.BN, m.D, 1, gd.pre_conv_b));
-    if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sd));
+    if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sq()));
     if (gd.pre_conv_w) {
       Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
       g.M = m.D; g.N = (int)m.FT; g.K = (int)m.BN;
@@ -1437,7 +1471,7 @@ struct Bwd {
       DS_TRY(fork());
       if (part) DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.gcon_e + pb * N, gd.embT_b}}, pb, m.N, 1));
       else DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dE, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
-      if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sd));
+      if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sq()));
       DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
       DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
     } else {
@@ -1538,19 +1572,31 @@ struct Bwd {
     ht.lap("init");
     DS_TRY(debug_delay(st, true));
     DS_TRY(stage_tail());
+    DS_TRY(order_err);
     ht.lap("tail");
     DS_TRY(debug_delay(st, true));
     DS_TRY(stage_cheb());
+    DS_TRY(order_err);
     ht.lap("cheb");
     DS_TRY(debug_delay(st, true));
     DS_TRY(stage_sat());  // + stage_preconv
+    DS_TRY(order_err);
     ht.lap("sat");
     DS_TRY(debug_delay(st, true));
     DS_TRY(stage_tat());
+    DS_TRY(order_err);
     ht.lap("tat");
     if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));  // (+ the fc weight gradient)
     else if (!fc_side() && gd.tat_fc) DS_TRY(gemm(fc_grad_gemm()));
+#ifdef DSTAGNN_RACEBUG_NOFORK
+    // deliberately racy build (make racebug -> abtest/racebug; tests/test_gpu_knobs.py::
+    // test_race_probe_catches_a_missing_fork): the TAt LayerNorm column sums on the side stream
+    // WITHOUT a fork after the LayerNorm backward that writes their partials
+    DS_TRY(tat_ln_colsums(false));
+#else
     if (!tatln_side()) DS_TRY(tat_ln_colsums(true));
+#endif
+    DS_TRY(order_err);
     DS_TRY(join());
     ht.lap("join");
     return 0;

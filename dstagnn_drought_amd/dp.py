@@ -20,11 +20,24 @@ import torch
 import torch.distributed as dist
 
 
-def shard_batch(t, rank, world):
-    """Disjoint contiguous slice of the leading (batch) dim for `rank`."""
+def shard_start(B, rank, world):
+    """Global index of the first sample of `rank`'s shard of a B-sample batch (shard_batch)."""
+    per = (B + world - 1) // world
+    return min(B, rank * per)
+
+
+def shard_batch(t, rank, world, model=None):
+    """Disjoint contiguous slice of the leading (batch) dim for `rank` (ceil(B/world) samples per
+    rank, the last shard shorter).  With `model`, its blocks' dropout sample base is set to the
+    shard's true global offset (model.set_sample_base): the default base, rank * local_B, is
+    right only for equal shards (B=5 over 2 ranks: rank 1 starts at 3, not 2)."""
     B = t.shape[0]
     per = (B + world - 1) // world
-    return t[rank * per:min(B, (rank + 1) * per)]
+    start = shard_start(B, rank, world)
+    if model is not None:
+        from .model import set_sample_base
+        set_sample_base(model, start)
+    return t[start:min(B, (rank + 1) * per)]
 
 
 class GradAllReducer:

@@ -200,8 +200,23 @@ class HipAdam(torch.optim.Optimizer):
         self._plans = {}
 
     def load_state_dict(self, state_dict):
+        """Accepts HipAdam's and torch.optim.Adam's state_dicts alike: torch keeps ``step`` as a
+        (float) tensor, HipAdam as a Python int (a tensor step would key ``by_step`` below by
+        identity: one launch per parameter and no cached plan), so it is converted here."""
         self._plans = {}
         super().load_state_dict(state_dict)
+        for st in self.state.values():
+            if "step" in st and torch.is_tensor(st["step"]):
+                st["step"] = int(st["step"].item())
+
+    def state_dict(self):
+        """torch.optim.Adam's format: ``step`` as a float32 CPU tensor (the live state keeps the
+        int; the returned per-parameter dicts are copies)."""
+        sd = super().state_dict()
+        sd["state"] = {k: (dict(v, step=torch.tensor(float(v["step"]), dtype=torch.float32))
+                           if "step" in v and not torch.is_tensor(v["step"]) else v)
+                       for k, v in sd["state"].items()}
+        return sd
 
     def zero_grad(self, set_to_none=True):
         """torch's zero_grad(set_to_none=True) spends ~1 us per parameter in profiler /
@@ -258,7 +273,7 @@ class HipAdam(torch.optim.Optimizer):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st["step"] += 1
+                st["step"] = int(st["step"]) + 1  # (a tensor step from a foreign state_dict)
                 lists = by_step.setdefault(st["step"], ([], [], [], []))
                 lists[0].append(p if p.is_contiguous() else p.data)
                 lists[1].append(g)  # a strided gradient is copied contiguous by the op

@@ -8,6 +8,9 @@ rank builds the same 2-block make_model, then for eval and train mode:
          global sample index, rank * B + b), SmoothL1, backward with GradAllReducer.attach (the
          RCCL path of the driver's scaling bench), mean all-reduce, Adam step;
   * ref: the same model copy on the whole batch, sample base 0, backward, Adam step.
+Both use the driver's optimiser (train.make_adam -> HipAdam, one launch) and take TWO steps, so the
+second runs HipAdam's cached fast path on the all-reduced gradients; the second step's
+parameters are compared like the first's.
 Split-K off (every tiled reduction in one fixed order).  Writes one JSON record per rank."""
 import copy
 import json
@@ -30,6 +33,7 @@ def main():
     import dstagnn_drought_amd as D
     from dstagnn_drought_amd import _lib
     from dstagnn_drought_amd.dp import GradAllReducer, mask_support_of
+    from dstagnn_drought_amd.train import make_adam
     ops = _lib.load()
     ops.set_splitk_target(1)
     Bl, N, T, K, h, Dm, dk, C, P = 2, 40, 12, 3, 3, 64, 32, 32, 12
@@ -56,26 +60,32 @@ def main():
                 D.set_sample_base(net, 0)  # the whole batch on one device
             nets[kind] = net
         red = GradAllReducer(nets["dp"].named_parameters(), mask_support=mask_support_of(nets["dp"])).attach(nets["dp"])
-        outs, losses, grads, params = {}, {}, {}, {}
+        outs, losses, grads, params, grads2, params2, kinds = {}, {}, {}, {}, {}, {}, {}
         for kind, xb, yb in (("dp", x[sl], y[sl]), ("ref", x, y)):
             net = nets[kind]
-            opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-            opt.zero_grad()
-            torch.manual_seed(77)  # the blocks draw the same dropout seeds in both runs
-            out = net(xb)
-            loss = torch.nn.functional.smooth_l1_loss(out, yb)
-            loss.backward()
-            if kind == "dp":
-                red.all_reduce()
-                lt = loss.detach().clone()
-                dist.all_reduce(lt)
-                loss = lt / world
-            opt.step()
-            torch.cuda.synchronize()
-            outs[kind] = out.detach()
-            losses[kind] = float(loss)
-            grads[kind] = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
-            params[kind] = {n: p.detach().clone() for n, p in net.named_parameters()}
+            opt = make_adam(net.parameters(), 1e-4)
+            kinds[kind] = type(opt).__name__
+            for it in range(2):
+                opt.zero_grad()
+                torch.manual_seed(77 + it)  # the blocks draw the same dropout seeds in both runs
+                out = net(xb if it == 0 else xb.flip(-1))
+                loss = torch.nn.functional.smooth_l1_loss(out, yb)
+                loss.backward()
+                if kind == "dp":
+                    red.all_reduce()
+                    lt = loss.detach().clone()
+                    dist.all_reduce(lt)
+                    loss = lt / world
+                opt.step()
+                torch.cuda.synchronize()
+                g = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+                pr = {n: p.detach().clone() for n, p in net.named_parameters()}
+                if it == 0:
+                    outs[kind] = out.detach()
+                    losses[kind] = float(loss)
+                    grads[kind], params[kind] = g, pr
+                else:
+                    grads2[kind], params2[kind] = g, pr
         fwd_exact = bool(torch.equal(outs["dp"], outs["ref"][sl]))
         fwd_err = float((outs["dp"] - outs["ref"][sl]).abs().max())
         gerr = {n: float((grads["dp"][n] - g).abs().max()) / max(1.0, float(g.abs().max()))
@@ -92,10 +102,21 @@ def main():
                 # update is compared where |g| > 1e-3 * max|g| of the tensor
                 d = d[g.abs() > 1e-3 * float(g.abs().max())]
             perr[n] = (float(d.max()) if d.numel() else 0.0) / max(1.0, float(p.abs().max()))
+        perr2 = {}  # after the second (cached-plan) HipAdam step
+        for n, p in params2["ref"].items():
+            if n.endswith("fcmy.0.bias"):
+                continue
+            d = (params2["dp"][n] - p).abs()
+            g1, g2 = grads["ref"].get(n), grads2["ref"].get(n)
+            if g1 is not None and g2 is not None:
+                d = d[(g1.abs() > 1e-3 * float(g1.abs().max())) & (g2.abs() > 1e-3 * float(g2.abs().max()))]
+            perr2[n] = (float(d.max()) if d.numel() else 0.0) / max(1.0, float(p.abs().max()))
         rec[mode] = {"fwd_exact": fwd_exact, "fwd_err": fwd_err, "loss_dp": losses["dp"], "loss_ref": losses["ref"],
                      "same_grad_keys": sorted(grads["dp"]) == sorted(grads["ref"]),
                      "grad_err": max(gerr.values()), "grad_worst": max(gerr, key=gerr.get),
-                     "param_err": max(perr.values()), "param_worst": max(perr, key=perr.get)}
+                     "param_err": max(perr.values()), "param_worst": max(perr, key=perr.get),
+                     "param_err2": max(perr2.values()), "param_worst2": max(perr2, key=perr2.get),
+                     "optimizer": kinds}
     with open(os.path.join(os.environ["DSTAGNN_DP_OUT"], f"equiv_rank{rank}.json"), "w") as f:
         json.dump(rec, f)
     dist.barrier()

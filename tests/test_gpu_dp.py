@@ -18,7 +18,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _launch(worker, tmp_path):
+def _launch(worker, tmp_path, nproc=2):
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -27,7 +27,7 @@ def _launch(worker, tmp_path):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", DSTAGNN_DP_OUT=str(tmp_path))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
            "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", worker)]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -68,3 +68,20 @@ def test_dp_step_equals_one_gpu_step(tmp_path):
             assert abs(x["loss_dp"] - x["loss_ref"]) <= 1e-6 * max(1.0, abs(x["loss_ref"])), (rec["rank"], mode, x)
             assert x["grad_err"] <= 1e-5, (rec["rank"], mode, x)
             assert x["param_err"] <= 1e-5, (rec["rank"], mode, x)
+            assert x["param_err2"] <= 1e-5, (rec["rank"], mode, x)  # HipAdam's cached second step
+            assert x["optimizer"] == {"dp": "HipAdam", "ref": "HipAdam"}, x
+
+
+@pytest.mark.gpu
+def test_rccl_world1_reducer(tmp_path):
+    """RCCL itself (backend "nccl", device_id as bench.py's init_ranks) on the
+    one GPU of a lease, world size 1, through bench.py's DP step: the post-hook all-reduce of the
+    block's flat gradient buffer on RCCL's stream beside the library's side stream completes,
+    the gradients are unchanged bit for bit, and the reducer's per-step cost is recorded
+    (tests/rccl_worker.py; the 8-GPU scaling curve is the driver's)."""
+    _launch("rccl_worker.py", tmp_path, nproc=1)
+    rec = json.loads((tmp_path / "rccl_world1.json").read_text())
+    print("rccl world 1:", rec)
+    assert rec["backend"] == "nccl" and rec["world"] == 1, rec
+    assert rec["hook_inflight"] == 1, rec   # the node's post-hook issued the async all-reduce
+    assert rec["exact"] and rec["collective_ok"], rec

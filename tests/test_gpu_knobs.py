@@ -17,6 +17,8 @@ a subprocess (the library reads its switches once per process):
                        Q|K|V weight gradient on the main stream
   DSTAGNN_TATLN_SIDE=1 the TAt LayerNorm gamma / beta column sums on the side stream
   DSTAGNN_GATES_BWD_SCALAR=1  the split-path GTU gates backward one element per thread (T = 144)
+  DSTAGNN_DEBUG_STREAMS=1  the fork invariant asserted (block.hip Bwd::sq): no side-stream work
+                       issued while a fork's signal is still pending
   DSTAGNN_DEBUG_MAIN_DELAY_US / DSTAGNN_DEBUG_SIDE_DELAY_US   race probes: a 1.5 ms busy-wait
                        kernel on the main stream before every stage / on the side stream after
                        every fork, so a cross-stream read without its dependency reads stale
@@ -56,7 +58,9 @@ print("KNOB_OK")
                                        ("DSTAGNN_DEBUG_MAIN_DELAY_US=1500", "pems08", 4),
                                        ("DSTAGNN_DEBUG_SIDE_DELAY_US=1500", "pems08", 4),
                                        ("DSTAGNN_DEBUG_MAIN_DELAY_US=1500", "pems07+flash", 2),
-                                       ("DSTAGNN_GATES_BWD_SCALAR=1", "t144k3", 2)])
+                                       ("DSTAGNN_GATES_BWD_SCALAR=1", "t144k3", 2),
+                                       ("DSTAGNN_DEBUG_STREAMS=1", "pems08", 4),
+                                       ("DSTAGNN_DEBUG_STREAMS=1", "pems07+flash", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
     import torch
     if not torch.cuda.is_available():
@@ -74,15 +78,16 @@ def test_knob_path_vs_oracle(env, cfg, B):
 def test_race_probe_catches_a_missing_fork():
     """The main-stream delay probe against a library built with one cross-stream dependency
     removed on purpose (the TAt LayerNorm column sums issued on the side stream without a
-    fork; built by the round's tooling into abtest/racebug, skipped when absent): the parity
-    check must FAIL there, i.e. the probe exposes a missing fork instead of hiding it."""
+    fork: block.hip under -DDSTAGNN_RACEBUG_NOFORK, built by `make` into abtest/racebug from the
+    same sources as the shipped library): the parity check must FAIL there, i.e. the probe
+    exposes a missing fork instead of hiding it.  DSTAGNN_POISON=1: the racing read sees NaN
+    scratch, not a previous run's equal values."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     lib = os.path.join(ROOT, "abtest", "racebug", "libdstagnn.so")
-    if not os.path.exists(lib):
-        pytest.skip("no racy library variant in this tree")
-    e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", DSTAGNN_DEBUG_MAIN_DELAY_US="3000",
+    assert os.path.exists(lib), "abtest/racebug/libdstagnn.so missing: run `make` (target racebug)"
+    e = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", DSTAGNN_DEBUG_MAIN_DELAY_US="3000", DSTAGNN_POISON="1",
              LD_LIBRARY_PATH=os.path.dirname(lib))
     code = ("import sys\nsys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})\n"
             "import test_gpu_parity as T\n"

@@ -169,3 +169,40 @@ def test_dp_world2_equals_single_process(tmp_path):
     # validation batches are split over the ranks and reduced: both ranks report the same
     # mean (batch size 4 there vs 8 here, so only the two ranks are compared)
     assert res[0][2] == pytest.approx(res[1][2], rel=1e-12)
+
+
+def test_hip_adam_state_dict_round_trips_torch_format():
+    """HipAdam keeps ``step`` as an int (its by-step grouping keys on the value); a
+    torch.optim.Adam state_dict (tensor steps) loads as ints, and HipAdam's own state_dict has
+    torch's tensor steps without touching the live state."""
+    p = [nn.Parameter(torch.randn(3, 2)), nn.Parameter(torch.randn(4))]
+    ref = torch.optim.Adam(p, lr=1e-3)
+    for q in p:
+        q.grad = torch.ones_like(q)
+    ref.step()
+    ref.step()
+    ha = TR.HipAdam(p, lr=1e-3)  # (CPU parameters: state handling only, no step here)
+    ha.load_state_dict(ref.state_dict())
+    steps = [ha.state[q]["step"] for q in p]
+    assert steps == [2, 2] and all(type(s) is int for s in steps)
+    sd = ha.state_dict()
+    assert all(torch.is_tensor(s["step"]) and float(s["step"]) == 2.0 for s in sd["state"].values())
+    assert all(type(ha.state[q]["step"]) is int for q in p)  # the live state keeps ints
+    ref2 = torch.optim.Adam(p, lr=1e-3)
+    ref2.load_state_dict(sd)  # and torch takes it back
+    assert all(float(ref2.state[q]["step"]) == 2.0 for q in p)
+
+
+def test_shard_batch_sets_true_sample_base():
+    """a short last shard keys its dropout masks from its true global offset."""
+    from dstagnn_drought_amd.dp import shard_batch, shard_start
+
+    from dstagnn_drought_amd import model as M
+    blk = M.DSTAGNN_block.__new__(M.DSTAGNN_block)
+    nn.Module.__init__(blk)
+    blk.sample_base = None
+    t = torch.arange(5)
+    assert [shard_start(5, r, 2) for r in range(2)] == [0, 3]
+    part = shard_batch(t, 1, 2, model=blk)
+    assert part.tolist() == [3, 4] and blk.sample_base == 3
+    assert shard_batch(t, 0, 2, model=blk).tolist() == [0, 1, 2] and blk.sample_base == 0
