@@ -50,6 +50,8 @@ struct Dims {
   bool first, sparse, flash;
   bool fsmall;      // flash on a small graph (flash_small): the LDS-staged kernels
   bool agg;         // sparse path in aggregate-first order (cheb_agg.hip): no x Theta GEMM
+  bool tfused;      // the temporal-attention stage as one kernel per direction (tat_fused.hip)
+  int NP;           // tfused: node count padded to 16 (the re-laid Q|K|V weights' row length)
   int64_t nnz;      // flash: union-support entries
   int64_t apa_nnz;  // small-graph flash: A_pa support entries
 };
@@ -70,6 +72,8 @@ Dims mkdims(const dstagnn_block_dims& d) {
   static const bool agg_env = !getenv("DSTAGNN_CHEB_AGG") || atoi(getenv("DSTAGNN_CHEB_AGG")) != 0;
   m.agg = agg_env && m.sparse && cheb_agg_ok(m.F, m.C, m.K, m.T);
   m.apa_nnz = m.fsmall ? std::max(d.cheb_apa_nnz, 0) : 0;
+  m.tfused = tat_fused_fwd_ok(m.N, m.T, m.h, m.dk, m.dv);
+  m.NP = m.tfused ? tat_fused_np(m.N) : 0;
   return m;
 }
 
@@ -78,6 +82,7 @@ struct SaveBufs {
   // stacked projections [Wq; Wk; Wv] (QW, N) and [W_Q'; W_K'] (2KD, D), pre_conv as
   // (D, F*T), Theta_cat (F, K*C), GTU conv weights (o, j, c) fwd and (j', o, c) flipped bwd
   float *Wqkv, *Wqk, *Wp, *thcat, *Wgf[3], *Wgb[3];
+  float* Wqkv_p;  // tfused: [Wq; Wk; Wv] with rows zero-padded to NP
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float *lse, *psupp, *wsupp;  // flash path: column log-sum-exp (B,K,N), P and T o P on the support (B,K,nnz)
   float *am, *amt, *papa;      // small-graph flash: A_pa o M_k (K,N,N) and its transpose, P on the A_pa support
@@ -88,6 +93,7 @@ struct SaveBufs {
 SaveBufs plan_save(const Dims& m, Arena& a) {
   SaveBufs s;
   s.Wqkv = a.take(m.QW * m.N);
+  s.Wqkv_p = m.tfused ? a.take(m.QW * m.NP) : nullptr;
   s.Wqk = a.take(2 * m.KD * m.D);
   s.Wp = a.take((int64_t)m.D * m.FT);
   s.thcat = a.take((int64_t)m.F * m.KC);
@@ -730,12 +736,34 @@ struct Fwd {
     side_pending = false;
     DS_TRY(flush_stream_sig());  // (no-op when the GEMM carried the flag)
     DS_TRY(debug_delay(ks.sd, false));
-    if (!m.first) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
+    if (e_side) {  // E = x transposed (read by the TAt LayerNorm and saved for the backward)
       DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, (int64_t)m.N * m.FT, m.FT * m.N, 0.f, ks.sd));
       DS_TRY(ks.signal(ks.sd, &e_ready));
     }
     if (side_xth_pending) DS_TRY(cheb_xtheta(side_io, w.gemm_ws_side, ks.sd));
     return 0;
+  }
+
+  // the whole stage as one kernel (tat_fused.hip): E read in place from x (inner block) or from
+  // the EmbedT LayerNorm's output (first block); no E transpose, no intermediate round trips
+  int stage_tat_fused() {
+    const int64_t N = m.N;
+    TatFusedArgs t;
+    if (m.first) {
+      t.src = s.E; t.s0 = N; t.s1 = m.FT * N; t.sN = 1;
+    } else {
+      t.src = x; t.s0 = 1; t.s1 = N * m.FT; t.sN = m.FT;
+    }
+    t.wqkv = s.Wqkv_p; t.wfc = p.tat_fc;
+    t.res = res; t.res_mode = d.res_mode;
+    t.g = p.tat_ln_g; t.bta = p.tat_ln_b;
+    t.qkv = s.qkv; t.re_at = re_at; t.att = s.att; t.ctx = s.ctx;
+    t.u = s.u_tat; t.mu = s.mu_tat; t.rs = s.rs_tat; t.O = s.O;
+    t.FT = m.FT; t.BFT = m.BFT; t.BN = m.BN;
+    t.F = m.F; t.T = m.T; t.N = m.N; t.NP = m.NP; t.h = m.h;
+    t.scale = 1.f / sqrtf((float)m.dk);
+    DS_TRY(op_tat_fused_fwd(t, st));
+    return issue_fwd_side();  // (the fork's flag, if any, rode on the fused kernel)
   }
 
   int stage_tat() {
@@ -751,11 +779,12 @@ struct Fwd {
       a.y = s.E; a.yrow = idx1(N); a.yes = 1;
       a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et;
       DS_TRY(op_ln_fwd(a, st));
-    } else if (!e_side) {
+    } else if (!e_side && !m.tfused) {
       DS_TRY(op_transpose(x, s.E, m.N, (int)m.FT, m.B, N * m.FT, m.FT * N, 0.f, st));
     }
     // Q | K | V projections (MultiHeadAttention :92-94) as ONE GEMM over the stacked weights
     if (params_forked) DS_TRY(ks.join());  // the re-laid parameters (stage_params on the side stream)
+    if (m.tfused) return stage_tat_fused();
     {
       Gemm g;
       g.M = (int)m.BFT; g.N = (int)m.QW; g.K = m.N;
@@ -827,6 +856,11 @@ struct Fwd {
     add(0, p.tat_wq, s.Wqkv, m.HQ * m.N, 0, 0, 0, 0);
     add(0, p.tat_wk, s.Wqkv, m.HQ * m.N, 0, 0, 0, m.HQ * m.N);
     add(0, p.tat_wv, s.Wqkv, m.HV * m.N, 0, 0, 0, 2 * m.HQ * m.N);
+    if (m.tfused) {  // the fused TAt kernel's B operand: rows zero-padded to NP (16-B aligned quads)
+      add(8, p.tat_wq, s.Wqkv_p, m.HQ * m.NP, m.N, m.NP, 0, 0);
+      add(8, p.tat_wk, s.Wqkv_p, m.HQ * m.NP, m.N, m.NP, 0, m.HQ * m.NP);
+      add(8, p.tat_wv, s.Wqkv_p, m.HV * m.NP, m.N, m.NP, 0, 2 * m.HQ * m.NP);
+    }
     add(0, p.sat_wq, s.Wqk, m.KD * m.D, 0, 0, 0, 0);
     add(0, p.sat_wk, s.Wqk, m.KD * m.D, 0, 0, 0, m.KD * m.D);
     add(1, p.pre_conv_w, s.Wp, (int64_t)m.D * m.FT, m.F, m.T);  // Wp[d][f][t] = W[d][t][0][f]
@@ -954,12 +988,13 @@ struct Fwd {
     // aggregate-first Chebyshev (m.agg) has no x Theta GEMM: the side stream then carries only
     // E = x transposed, which the main chain awaits by its own token (e_ready)
     const bool side_xth = split && !m.agg;
-    if (split && (side_xth || !m.first)) {  // x Theta needs only x and Theta: it runs beside the whole attention chain
-      DS_TRY(ks.fork_k());  // issued after the Q|K|V GEMM (issue_fwd_side), which carries the flag
+    const bool e_need = !m.first && !m.tfused;  // the fused TAt kernel reads x in place
+    if (split && (side_xth || e_need)) {  // x Theta needs only x and Theta: it runs beside the whole attention chain
+      DS_TRY(ks.fork_k());  // issued after the Q|K|V GEMM / fused TAt (issue_fwd_side), which carries the flag
       side_pending = true;
       side_xth_pending = side_xth;
       side_io = c;
-      e_side = !m.first;
+      e_side = e_need;
     }
     DS_TRY(debug_delay(st, true));
     DS_TRY(stage_tat());
@@ -1544,7 +1579,11 @@ struct Bwd {
     Gemm g;
     g.M = (int)m.QW; g.N = m.N; g.K = (int)m.BFT;
     g.A = w.dqkv; g.am = idx1(1); g.ak = idx1(m.QW);
-    g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
+    if (m.tfused && !m.first) {  // E = x transposed was never written: E[(b,ft), n] = x[b, n, ft]
+      g.B = x; g.bk = idx2(m.FT, 1, N * m.FT); g.bn = idx1(m.FT);
+    } else {
+      g.B = s.E; g.bk = idx1(N); g.bn = idx1(1);
+    }
     const bool adjacent = gd.tat_wq && gd.tat_wk == gd.tat_wq + m.HQ * N && gd.tat_wv == gd.tat_wk + m.HQ * N;
     g.C = adjacent ? gd.tat_wq : w.dWqkv; g.cm = idx1(N); g.cn = idx1(1);
     if (fc_here) {

@@ -1530,6 +1530,11 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(PackRows a) {
 __global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
   const PrepSeg& g = a.seg[blockIdx.y];
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.n; i += (int64_t)gridDim.x * 256) {
+    if (g.kind == 8) {  // DESTINATION-indexed: src (R, p0) -> dst (R, p1) rows zero-padded to p1 >= p0
+      const int64_t r = i / g.p1, c = i - r * g.p1;
+      g.dst[g.dst_off + i] = c < g.p0 ? g.src[r * g.p0 + c] : 0.f;
+      continue;
+    }
     const float v = g.src[i];
     int64_t o;
     switch (g.kind) {

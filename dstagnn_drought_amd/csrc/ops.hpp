@@ -87,7 +87,7 @@ struct PackRows {
 //   6 product^T      dst[(i % p0) * p0 + i / p0] = src[i] * src2[i]     (its transpose, N = p0)
 struct PrepSeg {
   int kind = 0, p0 = 0, p1 = 0, p2 = 0;
-  int64_t n = 0;        // source elements
+  int64_t n = 0;        // source elements (kind 8: destination elements)
   int64_t dst_off = 0;  // kind 0: element offset into dst
   const float* src = nullptr;
   const float* src2 = nullptr;  // kind 5
@@ -257,6 +257,24 @@ struct GconvArgs {
 bool gtu_conv_fwd_ok(int C, int T, const int* ks, int n);
 int op_gtu_conv_fwd(GconvArgs a, hipStream_t st);
 int op_gtu_tconv(const TconvArgs& a, hipStream_t st);
+// the temporal-attention stage as one kernel (tat_fused.hip): Q|K|V projection, attention, fc,
+// residual and the LayerNorm over N; E(R, n) = src[(R % FT) s0 + (R / FT) s1 + n sN]
+struct TatFusedArgs {
+  const float* src = nullptr; int64_t s0 = 0, s1 = 0, sN = 0;
+  const float* wqkv = nullptr;  // (3 h dk, NP) zero-padded re-layout of [Wq; Wk; Wv]
+  const float* wfc = nullptr;   // (N, h dv) TAt.fc.weight
+  const float* res = nullptr; int res_mode = 0;
+  const float* g = nullptr; const float* bta = nullptr;  // LayerNorm(N) gamma / beta
+  float *qkv = nullptr, *re_at = nullptr, *att = nullptr, *ctx = nullptr;
+  float *u = nullptr, *mu = nullptr, *rs = nullptr, *O = nullptr;  // O[(R % FT) BN + (R / FT) N + n]
+  int64_t FT = 0, BFT = 0, BN = 0;
+  int F = 0, T = 0, N = 0, NP = 0, h = 0;
+  float scale = 1.f, eps = 1e-5f;
+  uint32_t* sig = nullptr; uint32_t sig_v = 0;  // kernel-written stream signal (common.hpp)
+};
+bool tat_fused_fwd_ok(int N, int T, int h, int dk, int dv);
+int tat_fused_np(int N);  // the padded node count of the re-laid Q|K|V weights
+int op_tat_fused_fwd(const TatFusedArgs& a, hipStream_t st);
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st);
 int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
