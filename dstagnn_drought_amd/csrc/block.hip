@@ -52,6 +52,8 @@ struct Dims {
   bool agg;         // sparse path in aggregate-first order (cheb_agg.hip): no x Theta GEMM
   bool tfused;      // the temporal-attention stage as one kernel per direction (tat_fused.hip)
   int NP;           // tfused: node count padded to 16 (the re-laid Q|K|V weights' row length)
+  bool tfused_bwd;  // ... and its backward (tat_fused.hip)
+  int64_t tf_wg;    // tfused_bwd: its workgroups (one gamma / beta partial row each)
   int64_t nnz;      // flash: union-support entries
   int64_t apa_nnz;  // small-graph flash: A_pa support entries
 };
@@ -74,6 +76,8 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.apa_nnz = m.fsmall ? std::max(d.cheb_apa_nnz, 0) : 0;
   m.tfused = tat_fused_fwd_ok(m.N, m.T, m.h, m.dk, m.dv);
   m.NP = m.tfused ? tat_fused_np(m.N) : 0;
+  m.tfused_bwd = m.tfused && tat_fused_bwd_ok(m.N, m.T, m.h, m.dk, m.dv, m.F, d.res_mode);
+  m.tf_wg = m.tfused_bwd ? cdiv64(m.BFT, 48) : 0;
   return m;
 }
 
@@ -83,6 +87,7 @@ struct SaveBufs {
   // (D, F*T), Theta_cat (F, K*C), GTU conv weights (o, j, c) fwd and (j', o, c) flipped bwd
   float *Wqkv, *Wqk, *Wp, *thcat, *Wgf[3], *Wgb[3];
   float* Wqkv_p;  // tfused: [Wq; Wk; Wv] with rows zero-padded to NP
+  float *WfcT, *WqT;  // tfused_bwd: W_fc^T (h dv, NP) and [Wq; Wk; Wv]^T (NP, 3 h dk), zero-padded
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float *lse, *psupp, *wsupp;  // flash path: column log-sum-exp (B,K,N), P and T o P on the support (B,K,nnz)
   float *am, *amt, *papa;      // small-graph flash: A_pa o M_k (K,N,N) and its transpose, P on the A_pa support
@@ -94,6 +99,8 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   SaveBufs s;
   s.Wqkv = a.take(m.QW * m.N);
   s.Wqkv_p = m.tfused ? a.take(m.QW * m.NP) : nullptr;
+  s.WfcT = m.tfused_bwd ? a.take(m.HV * m.NP) : nullptr;
+  s.WqT = m.tfused_bwd ? a.take(m.QW * m.NP) : nullptr;
   s.Wqk = a.take(2 * m.KD * m.D);
   s.Wp = a.take((int64_t)m.D * m.FT);
   s.thcat = a.take((int64_t)m.F * m.KC);
@@ -861,6 +868,16 @@ struct Fwd {
       add(8, p.tat_wk, s.Wqkv_p, m.HQ * m.NP, m.N, m.NP, 0, m.HQ * m.NP);
       add(8, p.tat_wv, s.Wqkv_p, m.HV * m.NP, m.N, m.NP, 0, 2 * m.HQ * m.NP);
     }
+    if (m.tfused_bwd) {  // the fused backward's B operands (zero-padded transposes, kind 9)
+      add(9, p.tat_fc, s.WfcT, m.HV * m.NP, m.NP, (int)m.HV, m.NP, 0);
+      pp.seg[pp.nseg - 1].p3 = m.N;
+      add(9, p.tat_wq, s.WqT, m.NP * m.HQ, (int)m.HQ, m.N, (int)m.QW, 0);
+      pp.seg[pp.nseg - 1].p3 = (int)m.HQ;
+      add(9, p.tat_wk, s.WqT, m.NP * m.HQ, (int)m.HQ, m.N, (int)m.QW, m.HQ);
+      pp.seg[pp.nseg - 1].p3 = (int)m.HQ;
+      add(9, p.tat_wv, s.WqT, m.NP * m.HV, (int)m.HV, m.N, (int)m.QW, 2 * m.HQ);
+      pp.seg[pp.nseg - 1].p3 = (int)m.HV;
+    }
     add(0, p.sat_wq, s.Wqk, m.KD * m.D, 0, 0, 0, 0);
     add(0, p.sat_wk, s.Wqk, m.KD * m.D, 0, 0, 0, m.KD * m.D);
     add(1, p.pre_conv_w, s.Wp, (int64_t)m.D * m.FT, m.F, m.T);  // Wp[d][f][t] = W[d][t][0][f]
@@ -1426,8 +1443,64 @@ struct Bwd {
     return gemm(g);
   }
 
+  // the whole TAt backward as one kernel (tat_fused.hip): LN_N backward, dctx, attention
+  // backward, dE accumulated into dx (inner block) or written for the EmbedT backward (first)
+  int stage_tat_fused() {
+    const int64_t N = m.N;
+    const bool side_any = tatln_side() || (gd.tat_fc && fc_side()) || wqkv_side();
+    if (!m.first) DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
+    if (side_any) DS_TRY(fork_k());  // (its flag rides on the fused kernel)
+    TatFusedBwdArgs t;
+    t.dO = w.dO; t.u = s.u_tat; t.mu = s.mu_tat; t.rs = s.rs_tat; t.g = p.tat_ln_g;
+    t.gpart = w.gcon_a; t.bpart = w.gcon_a + m.tf_wg * N;
+    t.dU = w.dU; t.wfcT = s.WfcT;
+    t.qkv = s.qkv; t.att = s.att; t.dre = dre; t.dqkv = w.dqkv;
+    t.res_mode = d.res_mode;
+    t.dres = dres;  // FULL: dS itself; BCAST: its sum over f (folded in the kernel)
+    t.dpart = w.dscore;
+    t.wqT = s.WqT;
+    if (m.first) {
+      t.dE = w.dE;
+    } else {
+      t.dx = dx; t.dxb = N * m.FT;
+    }
+    t.FT = m.FT; t.BFT = m.BFT; t.BN = m.BN;
+    t.F = m.F; t.T = m.T; t.N = m.N; t.NP = m.NP; t.h = m.h;
+    t.scale = 1.f / sqrtf((float)m.dk);
+    DS_TRY(op_tat_fused_bwd(t, st));
+    if (side_any) {
+      DS_TRY(fork_k_done());
+      if (tatln_side()) DS_TRY(tat_ln_colsums(false));
+      if (gd.tat_fc && fc_side()) DS_TRY(sgemm(fc_grad_gemm()));
+      if (wqkv_side()) DS_TRY(tat_wqkv_grad(true));
+    }
+    return m.first ? embedT_backward() : 0;
+  }
+
+  // first block: the EmbedT LayerNorm backward of dE, its parameter sums, dx += (dE)^T
+  int embedT_backward() {
+    const int64_t N = m.N;
+    LnBwd a;
+    a.R = m.B * m.T; a.L = m.N;
+    a.dy = w.dE; a.dyrow = idx1(N);
+    a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et; a.g = p.embT_g;
+    a.dx = w.du_et; a.dxrow = idx1(N);
+    const int64_t pb = ln_bwd_part_blocks((int64_t)m.B * m.T);
+    const bool part = ln_bwd_partials_ok(m.N) && 2 * pb <= (int64_t)m.B * m.T;
+    if (part) { a.gpart = w.gcon_e; a.bpart = w.gcon_e + pb * N; }
+    else a.gcontrib = w.gcon_e;
+    DS_TRY(op_ln_bwd(a, st));
+    DS_TRY(fork());
+    if (part) DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.gcon_e + pb * N, gd.embT_b}}, pb, m.N, 1));
+    else DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dE, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
+    if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sq()));
+    DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
+    return op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st);
+  }
+
   int stage_tat() {
     const int64_t N = m.N;
+    if (m.tfused_bwd) return stage_tat_fused();
     {  // LN_N backward (:100); dU = d(fc + E)
       LnBwd a;
       a.R = (int)m.BFT; a.L = m.N;
@@ -1493,22 +1566,7 @@ struct Bwd {
     DS_TRY(side_work());
     // dE -> dx
     if (m.first) {
-      LnBwd a;
-      a.R = m.B * m.T; a.L = m.N;
-      a.dy = w.dE; a.dyrow = idx1(N);
-      a.u = s.u_et; a.mu = s.mu_et; a.rs = s.rs_et; a.g = p.embT_g;
-      a.dx = w.du_et; a.dxrow = idx1(N);
-      const int64_t pb = ln_bwd_part_blocks((int64_t)m.B * m.T);
-      const bool part = ln_bwd_partials_ok(m.N) && 2 * pb <= (int64_t)m.B * m.T;
-      if (part) { a.gpart = w.gcon_e; a.bpart = w.gcon_e + pb * N; }
-      else a.gcontrib = w.gcon_e;
-      DS_TRY(op_ln_bwd(a, st));
-      DS_TRY(fork());
-      if (part) DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.gcon_e + pb * N, gd.embT_b}}, pb, m.N, 1));
-      else DS_TRY(colsums({{w.gcon_e, gd.embT_g}, {w.dE, gd.embT_b}}, (int64_t)m.B * m.T, m.N, 1));
-      if (gd.embT_pos) DS_TRY(op_sum_middle(w.du_et, 1, m.B, (int64_t)m.T * m.N, gd.embT_pos, 0.f, sq()));
-      DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
-      DS_TRY(op_transpose(w.du_et, dx, m.T, m.N, m.B, (int64_t)m.T * m.N, (int64_t)m.N * m.T, 1.f, st));
+      DS_TRY(embedT_backward());
     } else {
       DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
       DS_TRY(op_transpose(w.dE, dx, (int)m.FT, m.N, m.B, m.FT * N, N * m.FT, 1.f, st));
@@ -1557,6 +1615,8 @@ struct Bwd {
     return on;
   }
   int tat_ln_colsums(bool on_main) {
+    if (m.tfused_bwd)  // one gamma / beta partial row per fused-kernel workgroup
+      return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + m.tf_wg * m.N, gd.tat_ln_b}}, m.tf_wg, m.N, 1, on_main);
     if (tat_part()) {
       const int64_t pb = ln_bwd_part_blocks(m.BFT);
       return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1, on_main);

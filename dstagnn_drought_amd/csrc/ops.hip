@@ -1535,6 +1535,12 @@ __global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
       g.dst[g.dst_off + i] = c < g.p0 ? g.src[r * g.p0 + c] : 0.f;
       continue;
     }
+    if (g.kind == 9) {  // DESTINATION-indexed zero-padded transpose: src (p3, p1) row-major;
+      // dst row a, column b < p0 (row stride p2): src[b][a] where b < p3 and a < p1, else 0
+      const int64_t ra = i / g.p0, cb = i - ra * g.p0;
+      g.dst[g.dst_off + ra * g.p2 + cb] = (cb < g.p3 && ra < g.p1) ? g.src[cb * g.p1 + ra] : 0.f;
+      continue;
+    }
     const float v = g.src[i];
     int64_t o;
     switch (g.kind) {

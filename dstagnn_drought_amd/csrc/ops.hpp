@@ -86,7 +86,7 @@ struct PackRows {
 //   5 product        dst[i] = src[i] * src2[i]                          (A_pa o M_k)
 //   6 product^T      dst[(i % p0) * p0 + i / p0] = src[i] * src2[i]     (its transpose, N = p0)
 struct PrepSeg {
-  int kind = 0, p0 = 0, p1 = 0, p2 = 0;
+  int kind = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0;
   int64_t n = 0;        // source elements (kind 8: destination elements)
   int64_t dst_off = 0;  // kind 0: element offset into dst
   const float* src = nullptr;
@@ -275,6 +275,27 @@ struct TatFusedArgs {
 bool tat_fused_fwd_ok(int N, int T, int h, int dk, int dv);
 int tat_fused_np(int N);  // the padded node count of the re-laid Q|K|V weights
 int op_tat_fused_fwd(const TatFusedArgs& a, hipStream_t st);
+struct TatFusedBwdArgs {
+  const float* dO = nullptr;  // O's [(f,t)][(b,n)] order
+  const float *u = nullptr, *mu = nullptr, *rs = nullptr, *g = nullptr;
+  float *gpart = nullptr, *bpart = nullptr;  // (ceil(BFT / 48), N) gamma / beta partial rows
+  float* dU = nullptr;                       // (BFT, N)
+  const float* wfcT = nullptr;               // (h dv, NP) zero-padded transpose of TAt.fc.weight
+  const float *qkv = nullptr, *att = nullptr, *dre = nullptr;
+  float* dqkv = nullptr;                     // (BFT, 3 h dk)
+  int res_mode = 0;
+  float* dres = nullptr;                     // FULL: (B,F,h,T,T); BCAST: (B,h,T,T)
+  float* dpart = nullptr; int* cnt = nullptr;  // BCAST: (B, FT/48, h, T, T) partials, per-b tickets
+  const float* wqT = nullptr;                // (NP, 3 h dk) zero-padded transpose of [Wq; Wk; Wv]
+  float* dx = nullptr; int64_t dxb = 0;      // inner block: dx[b dxb + n FT + ft] += dE
+  float* dE = nullptr;                       // first block: (BFT, N)
+  int64_t FT = 0, BFT = 0, BN = 0;
+  int F = 0, T = 0, N = 0, NP = 0, h = 0;
+  float scale = 1.f;
+  uint32_t* sig = nullptr; uint32_t sig_v = 0;
+};
+bool tat_fused_bwd_ok(int N, int T, int h, int dk, int dv, int F, int res_mode);
+int op_tat_fused_bwd(const TatFusedBwdArgs& a, hipStream_t st);
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st);
 int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
