@@ -86,12 +86,54 @@ def run(name, steps=10, warmup=3):
     return out
 
 
+def run_model(name, steps=10, warmup=3):
+    """make_model nb_block=4 (first block F=1) + head, SmoothL1 fwd+bwd — the CPU column's
+    "PEMS04 model" row (BASELINE.md)."""
+    import dstagnn_drought_amd as D_
+    steps = int(os.environ.get("BENCH_CONFIGS_STEPS", steps))
+    warmup = int(os.environ.get("BENCH_CONFIGS_WARMUP", warmup))
+    N, T, K, h, Dm, dk, C, B = CONFIGS[name.split("_")[0]]
+    rs = np.random.RandomState(0)
+    tmd = np.eye(N)
+    pa = np.zeros((N, N))
+    for i in range(N):
+        tmd[i, rs.choice(N, 2, replace=False)] = 1.0
+        pa[i, rs.choice(N, 4, replace=False)] = 1.0
+    torch.manual_seed(1)
+    net = D_.make_model("cpu", 1, 4, 1, K, C, C, 1, torch.FloatTensor(tmd), torch.FloatTensor(pa),
+                        torch.FloatTensor(tmd), 12, T, N, Dm, dk, dk, h)
+    net = D_.set_direct_grads(net.cuda().train())
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.randn(B, N, 1, T, device="cuda", generator=g)
+    y = torch.randn(B, N, 12, device="cuda", generator=g)
+    params = list(net.parameters())
+
+    def step():
+        for p in params:
+            p.grad = None
+        torch.nn.functional.smooth_l1_loss(net(x), y).backward()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out = {"B": B, "ms_per_step": round(dt * 1e3, 3), "samples_per_s": round(B / dt, 1),
+           "what": "make_model nb_block=4 + head, SmoothL1 fwd+bwd (no optimiser step)"}
+    del net, x, y, params
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
-    names = sys.argv[1:] or list(CONFIGS)
+    names = sys.argv[1:] or (list(CONFIGS) + ["PEMS04_model"])
     res = {}
     for n in names:
         print(f"[configs] {n}", file=sys.stderr, flush=True)
-        res[n] = run(n)
+        res[n] = run_model(n) if n.endswith("_model") else run(n)
         print(f"[configs] {n}: {res[n]}", file=sys.stderr, flush=True)
     print(json.dumps(res))
 
