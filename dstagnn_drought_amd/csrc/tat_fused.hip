@@ -37,7 +37,29 @@ constexpr int kTfLQ = kTfQW + 4;        // LDS row stride of the Q|K|V tile
 constexpr int kTfLC = kTfHV + 4;        // ... of the ctx tile
 constexpr int kTfQT = kTfQW / 16;       // 18 column tiles of Q|K|V
 constexpr int kTfQTW = (kTfQT + 3) / 4; // 5 per wave (the last of waves 2, 3 is a discarded duplicate)
-constexpr int kTfNmax = 320;            // N <= 320 (LDS: E tile + Q|K|V tile + ctx tile <= 133 KB)
+constexpr int kTfNmax = 320;            // N <= 320 (LDS: <= 156 KB)
+constexpr int kTfRPW = kTfRows / 4;     // LayerNorm rows per wave
+constexpr int kTfDsMax = 2304;          // (48 / T) h T^2 at T = 16
+
+// phase timestamps (a variant build with -DDSTAGNN_TF_TIMING, e.g. into abtest/tftime): thread 0
+// of workgroups 0 and 100 prints the wall-clock (100 MHz) deltas between the marks
+#ifdef DSTAGNN_TF_TIMING
+#define TF_MARK(k) do { if (threadIdx.x == 0) tmark[k] = wall_clock64(); } while (0)
+#define TF_DECL uint64_t tmark[12] = {}
+#define TF_PRINT(tag, n)                                                                          \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 100)) {                           \
+      double d_[12];                                                                            \
+      for (int k_ = 1; k_ < (n); ++k_) d_[k_] = (double)(tmark[k_] - tmark[k_ - 1]) / 100.0;    \
+      printf("%s wg %d: %.2f %.2f %.2f %.2f %.2f %.2f us\n", tag, (int)blockIdx.x, d_[1], d_[2], \
+             d_[3], d_[4], d_[5], (n) > 6 ? d_[6] : 0.0);                                       \
+    }                                                                                           \
+  } while (0)
+#else
+#define TF_MARK(k) do {} while (0)
+#define TF_DECL
+#define TF_PRINT(tag, n) do {} while (0)
+#endif
 
 __device__ __forceinline__ floatx4 mf16(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -57,6 +79,31 @@ __device__ __forceinline__ float xsum16(float v) {
 __device__ __forceinline__ float f4at(const float4& v, int s) {
   return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
 }
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float tf_ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void tf_st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void tf_wave_sync() {  // LDS hand-off inside one wave
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// a contiguous block of n floats from LDS (row stride ls, row length rl, both multiples of 4)
+// to global memory, float4 per lane (the stores of a kernel go out at its end: stores count in
+// vmcnt on gfx9, so a store issued before a k loop would hold up that loop's operand waits)
+__device__ __forceinline__ void tf_copy_out(float* g, const float* l, int rows, int rl, int ls, int tid) {
+  const int q4 = rl / 4;
+  float4* g4 = reinterpret_cast<float4*>(g);
+  for (int e = tid; e < rows * q4; e += 256) {
+    const int r = e / q4, c4 = e - r * q4;
+    g4[e] = *reinterpret_cast<const float4*>(l + r * ls + 4 * c4);
+  }
+}
 
 // row R of the (B F T) x N input E: src[(R % FT) s0 + (R / FT) s1 + n sN]  (R, FT < 2^31: the
 // host checks; 32-bit division — a 64-bit one is a ~200-instruction software routine)
@@ -64,13 +111,24 @@ __device__ __forceinline__ int64_t tf_row(const TatFusedArgs& a, int64_t R) {
   const uint32_t r = (uint32_t)R, ft = (uint32_t)a.FT, b = r / ft;
   return (int64_t)(r - b * ft) * a.s0 + (int64_t)b * a.s1;
 }
-// the Q|K|V product's k loop step: A fragments of chunk c from the E tile, B fragments bq
+
+// ---- the 48-row products on the matrix cores -------------------------------------------------
+// 3 x NJ tiles (48 x 16 NJ) += A (48 x 16 NC, LDS rows of stride LA) B (16 NC x 16 NJ: lane
+// (i, q) of tile j reads the float4 at wp[j] + 16 c: B row 16 c + 4 q + s, column i).
+// Contraction index of step s of chunk c: 16 c + 4 q + s in both operands.  A and B fragments
+// are double-buffered (ping-pong, no register copies), so chunk c + 1's global and LDS loads are
+// in flight while chunk c is multiplied; sched_barrier keeps the scheduler from sinking them.
 template <int NJ>
-__device__ __forceinline__ void tf_qkv_step(floatx4 (&acc)[3][NJ], const float* Es, int LE, int c, int i, int q,
-                                            const float4 (&bq)[NJ]) {
-  float4 av[3];
+__device__ __forceinline__ void tf_ld_b(float4 (&b)[NJ], const float* const (&wp)[NJ], int off) {
 #pragma unroll
-  for (int mt = 0; mt < 3; ++mt) av[mt] = *reinterpret_cast<const float4*>(Es + (mt * 16 + i) * LE + 16 * c + 4 * q);
+  for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const float4*>(wp[j] + off);
+}
+__device__ __forceinline__ void tf_ld_a(float4 (&av)[3], const float* A, int LA, int c, int i, int q) {
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt) av[mt] = *reinterpret_cast<const float4*>(A + (mt * 16 + i) * LA + 16 * c + 4 * q);
+}
+template <int NJ>
+__device__ __forceinline__ void tf_mma(floatx4 (&acc)[3][NJ], const float4 (&av)[3], const float4 (&bq)[NJ]) {
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -79,42 +137,36 @@ __device__ __forceinline__ void tf_qkv_step(floatx4 (&acc)[3][NJ], const float* 
       for (int j = 0; j < NJ; ++j) acc[mt][j] = mf16(f4at(av[mt], s), f4at(bq[j], s), acc[mt][j]);
 }
 template <int NJ>
-__device__ __forceinline__ void tf_load_b(float4 (&b)[NJ], const float* const (&wp)[NJ], int off) {
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const float4*>(wp[j] + off);
-}
-// 3 x NJ tiles of (48 x 16 NJ) += A (48 x 16 NC, LDS, row stride LA) B (16 NC x 16 NJ, global
-// rows wp[j] + 16 c), the B fragments double-buffered (ping-pong: no register copies, so the
-// loads of chunk c + 1 stay in flight while chunk c is multiplied)
-template <int NJ>
 __device__ __forceinline__ void tf_gemm_rows48(floatx4 (&acc)[3][NJ], const float* A, int LA, int NC, int i, int q,
                                                const float* const (&wp)[NJ]) {
-  // (sched_barrier: the scheduler otherwise sinks each chunk's loads to just before their use)
-  float4 b0[NJ], b1[NJ];
-  tf_load_b(b0, wp, 0);
+  float4 b0[NJ], b1[NJ], a0[3], a1[3];
+  tf_ld_b(b0, wp, 0);
+  tf_ld_a(a0, A, LA, 0, i, q);
   int c = 0;
   for (; c + 1 < NC; c += 2) {
-    tf_load_b(b1, wp, 16 * (c + 1));
+    tf_ld_b(b1, wp, 16 * (c + 1));
+    tf_ld_a(a1, A, LA, c + 1, i, q);
     __builtin_amdgcn_sched_barrier(0);
-    tf_qkv_step(acc, A, LA, c, i, q, b0);
+    tf_mma(acc, a0, b0);
     __builtin_amdgcn_sched_barrier(0);
-    tf_load_b(b0, wp, 16 * min(c + 2, NC - 1));
+    const int cn = min(c + 2, NC - 1);
+    tf_ld_b(b0, wp, 16 * cn);
+    tf_ld_a(a0, A, LA, cn, i, q);
     __builtin_amdgcn_sched_barrier(0);
-    tf_qkv_step(acc, A, LA, c + 1, i, q, b1);
+    tf_mma(acc, a1, b1);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (c < NC) tf_qkv_step(acc, A, LA, c, i, q, b0);
+  if (c < NC) tf_mma(acc, a0, b0);
 }
 
-// E tile (48 x NP, zero-padded) into LDS.  Every load of a thread is issued before its first
-// LDS store (one memory round trip, not one per element).  x (B,N,F,T) with the workgroup's 48
-// rows inside one sample: a node's 48 values are contiguous — float4 per lane; otherwise (E
-// row-major, first block) scalar loads along the nodes.
-__device__ __forceinline__ void tf_load_e_tile(const float* src, const TatFusedArgs& a, int64_t R0, int nrows,
-                                               float* Es, int LE, int NP, int N, int tid) {
-  const uint32_t ft0 = (uint32_t)(R0 % a.FT);
+// E tile (48 x NP, zero-padded) into LDS, every load of a thread issued before its first LDS
+// store.  x (B,N,F,T) with the 48 rows inside one sample: a node's 48 values are contiguous —
+// float4 per lane; otherwise (E row-major, first block) scalar loads along the nodes.
+__device__ __forceinline__ void tf_load_e_tile(const TatFusedArgs& a, int64_t R0, int nrows, float* Es, int LE,
+                                               int NP, int N, int tid, int64_t* roff) {
+  const uint32_t ft0 = (uint32_t)R0 % (uint32_t)a.FT;
   if (a.sN != 1 && a.s0 == 1 && nrows == kTfRows && ft0 + kTfRows <= (uint32_t)a.FT) {
-    const float* base = src + tf_row(a, R0);
+    const float* base = a.src + tf_row(a, R0);
     constexpr int Q4 = kTfRows / 4;  // 12 float4 per node
     const int total = N * Q4;
     for (int e0 = 0; e0 < total; e0 += 256 * 8) {
@@ -143,7 +195,6 @@ __device__ __forceinline__ void tf_load_e_tile(const float* src, const TatFusedA
     }
     return;
   }
-  int64_t* roff = reinterpret_cast<int64_t*>(Es + kTfRows * LE) ;  // (scratch: the Q|K|V tile region)
   if (tid < kTfRows) roff[tid] = tf_row(a, R0 + min(tid, max(nrows - 1, 0)));
   __syncthreads();
   const int total = kTfRows * NP;
@@ -156,7 +207,7 @@ __device__ __forceinline__ void tf_load_e_tile(const float* src, const TatFusedA
       if (a.sN == 1) { r = e / NP; n = e - r * NP; }
       else { n = e / kTfRows; r = e - n * kTfRows; }
       const bool ok = e < total && r < nrows && n < N;
-      v[u] = ok ? src[roff[min(r, kTfRows - 1)] + (int64_t)min(n, N - 1) * a.sN] : 0.f;
+      v[u] = ok ? a.src[roff[min(r, kTfRows - 1)] + (int64_t)min(n, N - 1) * a.sN] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -169,26 +220,54 @@ __device__ __forceinline__ void tf_load_e_tile(const float* src, const TatFusedA
       }
     }
   }
-  __syncthreads();  // (roff is overwritten by the Q|K|V tile later)
+  __syncthreads();  // (roff lives in a region written later)
 }
 
-template <int T, int NTW>
+// =====================================================================================
+// Forward
+// =====================================================================================
+// LDS (floats): Es [48][NP+4] (E, then u = fc + E) | Qs [48][292] Q|K|V | Cs [48][100] ctx |
+// RA [PW h T^2] re_At | AT [PW h T^2] softmax — re_At / A / Q|K|V / ctx go out at the end
+template <int T, int NTW>  // NTW: fc column tiles per wave = LayerNorm values per lane (ceil(NP / 64))
 __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
   static_assert(T % 4 == 0 && T <= 16 && kTfRows % T == 0, "whole problems per workgroup, one 16 x 16 tile");
+  constexpr int PW = kTfRows / T;                  // problems per workgroup
+  constexpr int NTASK = PW * kTfH;                 // (problem, head) attention tasks
+  constexpr int TPW = (NTASK + 3) / 4;             // per wave
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   const int NP = a.NP, LE = NP + 4, N = a.N;
-  float* Es = lds;                       // [48][LE]   E, then u = fc + E
-  float* Qs = Es + kTfRows * LE;         // [48][kTfLQ] Q | K | V
-  float* Cs = Qs + kTfRows * kTfLQ;      // [48][kTfLC] ctx
+  float* Es = lds;
+  float* Qs = Es + kTfRows * LE;
+  float* Cs = Qs + kTfRows * kTfLQ;
+  float* RA = Cs + kTfRows * kTfLC;
+  float* AT = RA + kTfDsMax;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, i = l & 15, q = l >> 4;
   const int64_t R0 = (int64_t)blockIdx.x * kTfRows;
   const int nrows = (int)min<int64_t>(kTfRows, a.BFT - R0);
+  const int64_t P0 = R0 / T;  // first problem (b, f)
   stream_sig_store(a.sig, a.sig_v);
+  TF_DECL;
+  TF_MARK(0);
 
+  // res_att operands of this wave's attention tasks, issued first (they land during the GEMM)
+  float4 rr[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    rr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int task = w + 4 * k, p = task / kTfH, hd = task - p * kTfH;
+    if (task < NTASK && p * T < nrows && i < T && q < T / 4 && a.res_mode != DSTAGNN_RES_NONE) {
+      const int64_t P = P0 + p;
+      const int64_t bP = (uint32_t)P / (uint32_t)a.F;
+      const float* rp = a.res_mode == DSTAGNN_RES_BCAST ? a.res + (bP * kTfH + hd) * T * T
+                                                        : a.res + (P * kTfH + hd) * T * T;
+      rr[k] = *reinterpret_cast<const float4*>(rp + i * T + 4 * q);
+    }
+  }
   // ---- 1. E tile --------------------------------------------------------------------------
-  tf_load_e_tile(a.src, a, R0, nrows, Es, LE, NP, N, tid);
+  tf_load_e_tile(a, R0, nrows, Es, LE, NP, N, tid, reinterpret_cast<int64_t*>(Qs));
   __syncthreads();
+  TF_MARK(1);
 
   // ---- 2. Q | K | V = E Wqkv^T ------------------------------------------------------------
   {
@@ -201,7 +280,6 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
 #pragma unroll
     for (int j = 0; j < kTfQTW; ++j) wp[j] = a.wqkv + (int64_t)(min(w + 4 * j, kTfQT - 1) * 16 + i) * NP + 4 * q;
     tf_gemm_rows48(acc, Es, LE, NP / 16, i, q, wp);
-    // D[4q + r][i] of tile (mt, nt)
 #pragma unroll
     for (int j = 0; j < kTfQTW; ++j) {
       const int nt = w + 4 * j;
@@ -214,15 +292,16 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
     }
   }
   __syncthreads();
+  TF_MARK(2);
 
   // ---- 3. attention per (problem, head) (tat_fwd_mfma_kernel's math, operands from LDS) ----
-  constexpr int PW = kTfRows / T;  // problems per workgroup
-  for (int task = w; task < PW * kTfH; task += 4) {
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int task = w + 4 * k;
+    if (task >= NTASK) break;
     const int p = task / kTfH, hd = task - p * kTfH;
     const int rb = p * T;
-    if (rb >= nrows) continue;  // (wave-uniform)
-    const int64_t P = R0 / T + p;  // global problem (b, f)
-    const int64_t b = P / a.F;
+    if (rb >= nrows) break;  // (wave-uniform)
     const float* Qp = Qs + rb * kTfLQ + hd * kTfD;
     const float* Kp = Qp + kTfHV;
     const float* Vp = Qp + 2 * kTfHV;
@@ -240,12 +319,6 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
       q0 = *reinterpret_cast<const float4*>(Qp + c * kTfLQ + 8 * q);
       q1 = *reinterpret_cast<const float4*>(Qp + c * kTfLQ + 8 * q + 4);
     }
-    const int64_t sbase = (P * kTfH + hd) * T * T;
-    const float* rp = nullptr;
-    if (a.res_mode == DSTAGNN_RES_BCAST) rp = a.res + (b * kTfH + hd) * T * T;
-    else if (a.res_mode == DSTAGNN_RES_FULL) rp = a.res + sbase;
-    float4 rr = {0.f, 0.f, 0.f, 0.f};
-    if (rp && vi && vj) rr = *reinterpret_cast<const float4*>(rp + c * T + 4 * q);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     acc = mf16(k0.x, q0.x, acc);
     acc = mf16(k0.y, q0.y, acc);
@@ -255,14 +328,15 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
     acc = mf16(k1.y, q1.y, acc);
     acc = mf16(k1.z, q1.z, acc);
     acc = mf16(k1.w, q1.w, acc);
-    const float rv[4] = {rr.x, rr.y, rr.z, rr.w};
+    const float rv[4] = {rr[k].x, rr[k].y, rr[k].z, rr[k].w};
     float sc[4], pr[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       sc[r] = acc[r] * a.scale;
       sc[r] += rv[r];
     }
-    if (vi && vj) *reinterpret_cast<float4*>(a.re_at + sbase + c * T + 4 * q) = make_float4(sc[0], sc[1], sc[2], sc[3]);
+    const int tb = task * T * T;  // this task's tile in RA / AT ([p][hd] order = the global order)
+    if (vi && vj) *reinterpret_cast<float4*>(RA + tb + c * T + 4 * q) = make_float4(sc[0], sc[1], sc[2], sc[3]);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float m = xmax16(vi ? sc[r] : -INFINITY);
@@ -270,7 +344,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
       const float inv = 1.f / xsum16(e);
       pr[r] = vj ? e * inv : 0.f;
     }
-    if (vi && vj) *reinterpret_cast<float4*>(a.att + sbase + c * T + 4 * q) = make_float4(pr[0], pr[1], pr[2], pr[3]);
+    if (vi && vj) *reinterpret_cast<float4*>(AT + tb + c * T + 4 * q) = make_float4(pr[0], pr[1], pr[2], pr[3]);
     floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -287,20 +361,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
     }
   }
   __syncthreads();
-
-  // saved Q | K | V and ctx: the workgroup's rows are contiguous in both (coalesced float4)
-  {
-    float4* gq = reinterpret_cast<float4*>(a.qkv + R0 * kTfQW);
-    for (int e = tid; e < nrows * (kTfQW / 4); e += 256) {
-      const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
-      gq[e] = *reinterpret_cast<const float4*>(Qs + r * kTfLQ + 4 * c4);
-    }
-    float4* gc = reinterpret_cast<float4*>(a.ctx + R0 * kTfHV);
-    for (int e = tid; e < nrows * (kTfHV / 4); e += 256) {
-      const int r = e / (kTfHV / 4), c4 = e - r * (kTfHV / 4);
-      gc[e] = *reinterpret_cast<const float4*>(Cs + r * kTfLC + 4 * c4);
-    }
-  }
+  TF_MARK(3);
 
   // ---- 4. u = ctx W_fc^T + E, in the E tile -------------------------------------------------
   {
@@ -329,48 +390,91 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
     }
   }
   __syncthreads();
+  TF_MARK(4);
 
-  // ---- 5. LayerNorm over N per row (ln_fwd_kernel's two-pass statistics) ---------------------
-  constexpr int VPT = (kTfNmax + 63) / 64;
-  for (int r = w; r < nrows; r += 4) {
-    const int64_t R = R0 + r;
-    const float* row = Es + r * LE;
-    float v[VPT];
-    float sum = 0.f;
+  // ---- 5. LayerNorm over N, the wave's 12 rows at once (ln_fwd_kernel's two-pass statistics;
+  // the row sums of all 12 rows in one multi-value reduction instead of 12 dependent chains) ----
+  {
+    float v[kTfRPW][NTW];
+    float s16[16];
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      const int n = l + 64 * k;
-      v[k] = n < N ? row[n] : 0.f;
-      sum += v[k];
-    }
-    const float mean = wave_sum(sum) / N;
-    float var = 0.f;
+    for (int k = 0; k < kTfRPW; ++k) {
+      const float* row = Es + (w + 4 * k) * LE;
+      float sum = 0.f;
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      const int n = l + 64 * k;
-      if (n < N) {
-        const float d = v[k] - mean;
-        var += d * d;
+      for (int j = 0; j < NTW; ++j) {
+        const int n = l + 64 * j;
+        v[k][j] = n < N ? row[n] : 0.f;
+        sum += v[k][j];
       }
+      s16[k] = sum;
     }
-    var = wave_sum(var) / N;
-    const float rs = rsqrtf(var + a.eps);
-    if (l == 0) {
-      a.mu[R] = mean;
-      a.rs[R] = rs;
-    }
-    const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
-    float* orow = a.O + (int64_t)ft * a.BN + (int64_t)bb * N;
-    float* urow = a.u + R * N;
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      const int n = l + 64 * k;
-      if (n < N) {
-        urow[n] = v[k];
-        orow[n] = (v[k] - mean) * rs * a.g[n] + a.bta[n];
+    for (int k = kTfRPW; k < 16; ++k) s16[k] = 0.f;
+    const float tot = wave_sum_many<16>(s16);  // lane 4k holds row k's sum
+    float mean[kTfRPW];
+#pragma unroll
+    for (int k = 0; k < kTfRPW; ++k) mean[k] = rdlane(tot, 4 * k) / N;
+#pragma unroll
+    for (int k = 0; k < kTfRPW; ++k) {
+      float var = 0.f;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int n = l + 64 * j;
+        if (n < N) {
+          const float d = v[k][j] - mean[k];
+          var += d * d;
+        }
+      }
+      s16[k] = var;
+    }
+#pragma unroll
+    for (int k = kTfRPW; k < 16; ++k) s16[k] = 0.f;
+    const float tv = wave_sum_many<16>(s16);
+    float gv[NTW], bv[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = min(l + 64 * j, N - 1);
+      gv[j] = a.g[n];
+      bv[j] = a.bta[n];
+    }
+#pragma unroll
+    for (int k = 0; k < kTfRPW; ++k) {
+      const int r = w + 4 * k;
+      if (r >= nrows) break;
+      const int64_t R = R0 + r;
+      const float rs = rsqrtf(rdlane(tv, 4 * k) / N + a.eps);
+      if (l == 0) {
+        a.mu[R] = mean[k];
+        a.rs[R] = rs;
+      }
+      const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
+      float* orow = a.O + (int64_t)ft * a.BN + (int64_t)bb * N;
+      float* urow = a.u + R * N;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int n = l + 64 * j;
+        if (n < N) {
+          urow[n] = v[k][j];
+          orow[n] = (v[k][j] - mean[k]) * rs * gv[j] + bv[j];
+        }
       }
     }
   }
+  TF_MARK(5);
+  // ---- 6. the saved tiles: Q|K|V, ctx, re_At, A (contiguous blocks for the workgroup) --------
+  tf_copy_out(a.qkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
+  tf_copy_out(a.ctx + R0 * kTfHV, Cs, nrows, kTfHV, kTfLC, tid);
+  const int np = nrows / T;
+  tf_copy_out(a.re_at + P0 * kTfH * T * T, RA, 1, np * kTfH * T * T, 0, tid);
+  tf_copy_out(a.att + P0 * kTfH * T * T, AT, 1, np * kTfH * T * T, 0, tid);
+  TF_MARK(6);
+  TF_PRINT("tat_fused_fwd", 7);
+}
+
+size_t tat_fused_lds(int NP) {
+  return sizeof(float) * ((size_t)kTfRows * (NP + 4) + (size_t)kTfRows * kTfLQ + (size_t)kTfRows * kTfLC +
+                          2 * (size_t)kTfDsMax);
 }
 
 // =====================================================================================
@@ -381,177 +485,206 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
 // Saved for the weight gradients (issued after it): dU (fc) and dqkv (Q|K|V); the LayerNorm's
 // gamma / beta as one partial row per workgroup; the broadcast res_att gradient sum_f dS folded
 // in-kernel (fixed chunk order, tat_bwd_mfma's ticket hand-off).
+// LDS (floats): DUs [48][NP+4] | Qs [48][292] Q|K|V then dQ|dK|dV | Cs [48][100] dctx (first the
+// gamma / beta wave partials) | TRs [4][16][17] | DSs [PW h T^2] dS (+ one int)
 // =====================================================================================
-__device__ __forceinline__ float tf_ld_agent(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void tf_st_agent(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void tf_wave_sync() {  // LDS hand-off inside one wave
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-constexpr int kTfDsMax = 2304;  // (48 / T) * h * T * T floats at T = 16, h = 3
-
 template <int T, int NTW>
 __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a) {
   static_assert(T % 4 == 0 && T <= 16 && kTfRows % T == 0, "whole problems per workgroup, one 16 x 16 tile");
+  constexpr int PW = kTfRows / T;
+  constexpr int NTASK = PW * kTfH;
+  constexpr int TPW = (NTASK + 3) / 4;
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   const int NP = a.NP, LE = NP + 4, N = a.N;
-  float* DUs = lds;                        // [48][LE]    dU
-  float* Qs = DUs + kTfRows * LE;          // [48][kTfLQ] Q | K | V, then dQ | dK | dV in place
-  float* Cs = Qs + kTfRows * kTfLQ;        // [48][kTfLC] dctx (phase A: gamma / beta partials)
-  float* TRs = Cs + kTfRows * kTfLC;       // [4][16][17] per-wave dS transpose
-  float* DSs = TRs + 4 * 16 * 17;          // [48/T][h][T*T] dS tiles (broadcast res_att)
+  float* DUs = lds;
+  float* Qs = DUs + kTfRows * LE;
+  float* Cs = Qs + kTfRows * kTfLQ;
+  float* TRs = Cs + kTfRows * kTfLC;
+  float* DSs = TRs + 4 * 16 * 17;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, i = l & 15, q = l >> 4;
   const int64_t R0 = (int64_t)blockIdx.x * kTfRows;
   const int nrows = (int)min<int64_t>(kTfRows, a.BFT - R0);
+  const int64_t P0 = R0 / T;
   stream_sig_store(a.sig, a.sig_v);
+  TF_DECL;
+  TF_MARK(0);
 
-  // ---- A0. saved Q | K | V rows (contiguous) -> LDS -----------------------------------------
+  // ---- A0. every load of the first phases in one round: Q|K|V rows (-> LDS), the softmax and
+  // d re_At of this wave's attention tasks, the wave's 12 LayerNorm rows of dO and u ----------
+  constexpr int QV4 = kTfRows * kTfQW / 4 / 256;  // 13.5 -> 14 float4 per thread
+  float4 qv[QV4 + 1];
   {
     const float4* gq = reinterpret_cast<const float4*>(a.qkv + R0 * kTfQW);
-    for (int e = tid; e < nrows * (kTfQW / 4); e += 256) {
-      const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
-      *reinterpret_cast<float4*>(Qs + r * kTfLQ + 4 * c4) = gq[e];
+    const int tot = nrows * (kTfQW / 4);
+#pragma unroll
+    for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * 256 + tid, tot - 1)];
+  }
+  float at[TPW][4], dr[TPW][4];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int task = w + 4 * k, p = task / kTfH, hd = task - p * kTfH;
+    const bool live = task < NTASK && p * T < nrows;
+    const int64_t sbase = ((P0 + p) * kTfH + hd) * T * T;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ii = 4 * q + s;
+      const bool ok = live && ii < T && i < T;
+      at[k][s] = ok ? a.att[sbase + ii * T + i] : 0.f;
+      dr[k][s] = ok && a.dre ? a.dre[sbase + ii * T + i] : 0.f;
     }
   }
-  // ---- A1. LayerNorm(N) backward (ln_bwd_kernel's arithmetic), wave per row ----------------
-  constexpr int VPT = (kTfNmax + 63) / 64;
-  float gp[VPT], bp[VPT];
+  float dyv[kTfRPW][NTW], uu[kTfRPW][NTW];
 #pragma unroll
-  for (int k = 0; k < VPT; ++k) { gp[k] = 0.f; bp[k] = 0.f; }
-  for (int r = w; r < kTfRows; r += 4) {
-    float* dur = DUs + r * LE;
-    if (r >= nrows) {  // rows past the end: zeros (they only feed discarded output rows)
-      for (int n = l; n < NP; n += 64) dur[n] = 0.f;
-      continue;
-    }
+  for (int k = 0; k < kTfRPW; ++k) {
+    const int r = min(w + 4 * k, nrows - 1);
     const int64_t R = R0 + r;
     const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
     const float* dyr = a.dO + (int64_t)ft * a.BN + (int64_t)bb * N;
     const float* ur = a.u + R * N;
-    const float mean = a.mu[R], rsv = a.rs[R];
-    float dyv[VPT], xh[VPT], gl[VPT];
-    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      const int n = l + 64 * k;
-      const int e = min(n, N - 1);
-      const float dy = dyr[e], uu = ur[e], gg = a.g[e];
-      const bool ok = n < N;
-      dyv[k] = ok ? dy : 0.f;
-      xh[k] = ok ? (uu - mean) * rsv : 0.f;
-      gl[k] = ok ? gg : 0.f;
-      const float dxh = dyv[k] * gl[k];
-      s1 += dxh;
-      s2 += dxh * xh[k];
-      gp[k] += dyv[k] * xh[k];
-      bp[k] += dyv[k];
+    for (int j = 0; j < NTW; ++j) {
+      const int e = min(l + 64 * j, N - 1);
+      dyv[k][j] = dyr[e];
+      uu[k][j] = ur[e];
     }
-    s1 = wave_sum(s1) / N;
-    s2 = wave_sum(s2) / N;
-    float* gdu = a.dU + R * N;
+  }
+  {
+    const int tot = nrows * (kTfQW / 4);
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      const int n = l + 64 * k;
-      if (n < N) {
-        const float du = rsv * (dyv[k] * gl[k] - s1 - xh[k] * s2);
-        dur[n] = du;
-        gdu[n] = du;
-      } else if (n < NP) {
-        dur[n] = 0.f;
+    for (int u = 0; u <= QV4; ++u) {
+      const int e = u * 256 + tid;
+      if (e < tot) {
+        const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
+        *reinterpret_cast<float4*>(Qs + r * kTfLQ + 4 * c4) = qv[u];
       }
     }
   }
-  {  // gamma / beta: one partial row per workgroup (four wave rows summed in wave order)
+  // ---- A1. LayerNorm(N) backward of the wave's 12 rows at once (ln_bwd_kernel's arithmetic) --
+  float gp[NTW], bp[NTW], gsum[2], bsum[2];
+  {
+    float gl[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      gp[j] = 0.f;
+      bp[j] = 0.f;
+      gl[j] = l + 64 * j < N ? a.g[min(l + 64 * j, N - 1)] : 0.f;
+    }
+    float s32[32], xh[kTfRPW][NTW];
+    float mean[kTfRPW], rsv[kTfRPW];
+#pragma unroll
+    for (int k = 0; k < kTfRPW; ++k) {
+      const int r = w + 4 * k;
+      const int64_t R = R0 + min(r, nrows - 1);
+      mean[k] = a.mu[R];
+      rsv[k] = a.rs[R];
+      const bool live = r < nrows;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const bool ok = live && l + 64 * j < N;
+        if (!ok) dyv[k][j] = 0.f;
+        xh[k][j] = ok ? (uu[k][j] - mean[k]) * rsv[k] : 0.f;
+        const float dxh = dyv[k][j] * gl[j];
+        s1 += dxh;
+        s2 += dxh * xh[k][j];
+        gp[j] += dyv[k][j] * xh[k][j];
+        bp[j] += dyv[k][j];
+      }
+      s32[k] = s1;
+      s32[16 + k] = s2;
+    }
+#pragma unroll
+    for (int k = kTfRPW; k < 16; ++k) { s32[k] = 0.f; s32[16 + k] = 0.f; }
+    const float tot = wave_sum_many<32>(s32);  // lanes 2v, 2v + 1 hold value v
+#pragma unroll
+    for (int k = 0; k < kTfRPW; ++k) {
+      const int r = w + 4 * k;
+      float* dur = DUs + r * LE;
+      const float s1 = rdlane(tot, 2 * k) / N, s2 = rdlane(tot, 2 * (16 + k)) / N;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int n = l + 64 * j;
+        if (n < NP) dur[n] = (r < nrows && n < N) ? rsv[k] * (dyv[k][j] * gl[j] - s1 - xh[k][j] * s2) : 0.f;
+      }
+    }
+  }
+  {  // gamma / beta: the four waves' partials summed in wave order (kept for the end)
     float* red = Cs;  // [2][4][NP] (Cs is free until phase B's epilogue)
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      const int n = l + 64 * k;
+    for (int j = 0; j < NTW; ++j) {
+      const int n = l + 64 * j;
       if (n < NP) {
-        red[(0 * 4 + w) * NP + n] = gp[k];
-        red[(1 * 4 + w) * NP + n] = bp[k];
+        red[(0 * 4 + w) * NP + n] = gp[j];
+        red[(1 * 4 + w) * NP + n] = bp[j];
       }
     }
     __syncthreads();
-    for (int n = tid; n < N; n += 256) {
-      if (a.gpart) a.gpart[(int64_t)blockIdx.x * N + n] = ((red[0 * NP + n] + red[1 * NP + n]) + red[2 * NP + n]) + red[3 * NP + n];
-      if (a.bpart) a.bpart[(int64_t)blockIdx.x * N + n] = ((red[4 * NP + n] + red[5 * NP + n]) + red[6 * NP + n]) + red[7 * NP + n];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // n = tid + 256 j (N <= 320 < 512)
+      const int n = min(tid + 256 * j, NP - 1);
+      gsum[j] = ((red[0 * NP + n] + red[1 * NP + n]) + red[2 * NP + n]) + red[3 * NP + n];
+      bsum[j] = ((red[4 * NP + n] + red[5 * NP + n]) + red[6 * NP + n]) + red[7 * NP + n];
     }
     __syncthreads();
   }
+  TF_MARK(1);
 
   // ---- B. dctx = dU W_fc  (48 x h dv, contraction over the NP nodes) -----------------------
   {
-    constexpr int CT = kTfHV / 16;          // 6 column tiles
-    constexpr int NTL = 3 * CT;             // 18 (row, column) tiles
-    constexpr int TPW = (NTL + 3) / 4;      // 5 per wave (the last of waves 2, 3: a duplicate)
-    floatx4 acc[TPW];
-    const float* wp[TPW];
-    int arow[TPW];
+    constexpr int CT = kTfHV / 16;          // 6 column tiles x 3 row tiles
+    floatx4 acc[3][2];                      // wave w: columns {w, w + 4} (waves 2, 3: one + a duplicate)
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-      const int t = min(w + 4 * j, NTL - 1), mt = t / CT, nt = t - mt * CT;
-      arow[j] = (mt * 16 + i) * LE + 4 * q;
-      wp[j] = a.wfcT + (int64_t)(nt * 16 + i) * NP + 4 * q;
-    }
-    const int NC = NP / 16;
-    auto step = [&](int c, const float4 (&bv)[TPW]) {
-      float4 av[TPW];
+    for (int mt = 0; mt < 3; ++mt) acc[mt][0] = acc[mt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* wp[2];
 #pragma unroll
-      for (int j = 0; j < TPW; ++j) av[j] = *reinterpret_cast<const float4*>(DUs + arow[j] + 16 * c);
+    for (int j = 0; j < 2; ++j) wp[j] = a.wfcT + (int64_t)(min(w + 4 * j, CT - 1) * 16 + i) * NP + 4 * q;
+    tf_gemm_rows48(acc, DUs, LE, NP / 16, i, q, wp);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+    for (int j = 0; j < 2; ++j) {
+      const int nt = w + 4 * j;
+      if (nt < CT) {
 #pragma unroll
-        for (int j = 0; j < TPW; ++j) acc[j] = mf16(f4at(av[j], s), f4at(bv[j], s), acc[j]);
-    };
-    float4 b0[TPW], b1[TPW];
-    tf_load_b(b0, wp, 0);
-    int c = 0;
-    for (; c + 1 < NC; c += 2) {
-      tf_load_b(b1, wp, 16 * (c + 1));
-      __builtin_amdgcn_sched_barrier(0);
-      step(c, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      tf_load_b(b0, wp, 16 * min(c + 2, NC - 1));
-      __builtin_amdgcn_sched_barrier(0);
-      step(c + 1, b1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (c < NC) step(c, b0);
+        for (int mt = 0; mt < 3; ++mt)
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      const int t = w + 4 * j;
-      if (t < NTL) {
-        const int mt = t / CT, nt = t - mt * CT;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Cs[(mt * 16 + 4 * q + r) * kTfLC + nt * 16 + i] = acc[j][r];
+          for (int r = 0; r < 4; ++r) Cs[(mt * 16 + 4 * q + r) * kTfLC + nt * 16 + i] = acc[mt][j][r];
       }
     }
   }
   __syncthreads();
+  TF_MARK(2);
+
+  // the dx tile of D1's epilogue (inner block), issued now: it lands during C and D1
+  float4 dxo[3][NTW];
+  if (a.dx) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = min((w + 4 * j) * 16 + i, N - 1);
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt) {
+        const int64_t R = R0 + min(mt * 16 + 4 * q, nrows - 4);
+        const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
+        dxo[mt][j] = *reinterpret_cast<const float4*>(a.dx + (int64_t)bb * a.dxb + (int64_t)n * a.FT + ft);
+      }
+    }
+  }
 
   // ---- C. attention backward per (problem, head) (tat_bwd_mfma_kernel's math) ---------------
-  constexpr int PW = kTfRows / T;
-  for (int task = w; task < PW * kTfH; task += 4) {
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int task = w + 4 * k;
+    if (task >= NTASK) break;
     const int p = task / kTfH, hd = task - p * kTfH;
     const int rb = p * T;
-    if (rb >= nrows) continue;  // (wave-uniform)
-    const int64_t P = R0 / T + p;
+    if (rb >= nrows) break;  // (wave-uniform)
     float* Qp = Qs + rb * kTfLQ + hd * kTfD;
     float* Kp = Qp + kTfHV;
     float* Vp = Qp + 2 * kTfHV;
     const float* Cp = Cs + rb * kTfLC + hd * kTfD;
-    const int64_t sbase = (P * kTfH + hd) * T * T;
     const int c = i;
     const bool vj = c < T;
     float4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0, v0 = d0, v1 = d0;
-    float cb[2][4], qb[2][4], kb[2][4], at[4], dr[4];
+    float cb[2][4], qb[2][4], kb[2][4];
     if (vj) {
       d0 = *reinterpret_cast<const float4*>(Cp + c * kTfLC + 8 * q);
       d1 = *reinterpret_cast<const float4*>(Cp + c * kTfLC + 8 * q + 4);
@@ -568,8 +701,6 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
         qb[t][s] = ok ? Qp[ii * kTfLQ + c + 16 * t] : 0.f;
         kb[t][s] = ok ? Kp[ii * kTfLQ + c + 16 * t] : 0.f;
       }
-      at[s] = ok && vj ? a.att[sbase + ii * T + c] : 0.f;
-      dr[s] = ok && vj && a.dre ? a.dre[sbase + ii * T + c] : 0.f;
     }
     floatx4 dA = {0.f, 0.f, 0.f, 0.f};
     dA = mf16(d0.x, v0.x, dA);
@@ -582,26 +713,23 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     dA = mf16(d1.w, v1.w, dA);
     float cs = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cs = fmaf(at[r], dA[r], cs);
+    for (int r = 0; r < 4; ++r) cs = fmaf(at[k][r], dA[r], cs);
     cs += __shfl_xor(cs, 16, 64);
     cs += __shfl_xor(cs, 32, 64);
     float ds[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ds[r] = at[r] * (dA[r] - cs) + dr[r];
+    for (int r = 0; r < 4; ++r) ds[r] = at[k][r] * (dA[r] - cs) + dr[k][r];
     if (vj) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (4 * q + r >= T) continue;
-        if (a.res_mode == DSTAGNN_RES_FULL && a.dres) a.dres[sbase + (4 * q + r) * T + c] = ds[r];
-        else if (a.res_mode == DSTAGNN_RES_BCAST) DSs[(p * kTfH + hd) * T * T + (4 * q + r) * T + c] = ds[r];
-      }
+      for (int r = 0; r < 4; ++r)
+        if (4 * q + r < T) DSs[task * T * T + (4 * q + r) * T + c] = ds[r];
     }
     floatx4 z = {0.f, 0.f, 0.f, 0.f};
     floatx4 gv0 = z, gv1 = z, gk0 = z, gk1 = z, gq0 = z, gq1 = z;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      gv0 = mf16(at[s], cb[0][s], gv0);
-      gv1 = mf16(at[s], cb[1][s], gv1);
+      gv0 = mf16(at[k][s], cb[0][s], gv0);
+      gv1 = mf16(at[k][s], cb[1][s], gv1);
       gk0 = mf16(ds[s], qb[0][s], gk0);
       gk1 = mf16(ds[s], qb[1][s], gk1);
     }
@@ -630,24 +758,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
   __syncthreads();
-
-  // ---- D0. dqkv out (the Q|K|V weight gradient's operand); res_att partial per (b, chunk) ----
-  {
-    float4* gq = reinterpret_cast<float4*>(a.dqkv + R0 * kTfQW);
-    for (int e = tid; e < nrows * (kTfQW / 4); e += 256) {
-      const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
-      gq[e] = *reinterpret_cast<const float4*>(Qs + r * kTfLQ + 4 * c4);
-    }
-  }
-  const int nch = (int)(a.FT / kTfRows);
-  const int64_t bwg = (uint32_t)R0 / (uint32_t)a.FT, chw = ((uint32_t)R0 - (uint32_t)bwg * (uint32_t)a.FT) / kTfRows;
-  if (a.res_mode == DSTAGNN_RES_BCAST) {
-    for (int e = tid; e < kTfH * T * T; e += 256) {
-      float v = 0.f;
-      for (int p = 0; p < PW; ++p) v += DSs[p * kTfH * T * T + e];  // problems in order
-      tf_st_agent(a.dpart + (bwg * nch + chw) * kTfH * T * T + e, v);
-    }
-  }
+  TF_MARK(3);
 
   // ---- D1. dE = dU + dqkv [Wq; Wk; Wv] ---------------------------------------------------
   {
@@ -661,6 +772,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 #pragma unroll
     for (int j = 0; j < NTW; ++j) wp[j] = a.wqT + (int64_t)(min(w + 4 * j, NT - 1) * 16 + i) * kTfQW + 4 * q;
     tf_gemm_rows48(acc, Qs, kTfLQ, kTfQW / 16, i, q, wp);
+    TF_MARK(4);
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int n = (w + 4 * j) * 16 + i;
@@ -676,9 +788,8 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
         if (a.dx) {  // inner block: rows R..R+3 are four consecutive ft of one b (FT % 4 == 0)
           const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
           float4* dp = reinterpret_cast<float4*>(a.dx + (int64_t)bb * a.dxb + (int64_t)n * a.FT + ft);
-          float4 o = *dp;
-          o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-          *dp = o;
+          const float4 o = dxo[mt][j];
+          *dp = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) a.dE[(R + r) * N + n] = v[r];
@@ -687,7 +798,35 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
 
-  // ---- D2. broadcast res_att gradient: the last workgroup of each b sums the chunks in order --
+  // ---- E. the saved tiles and partials (stores last: see tf_copy_out) ----------------------
+  tf_copy_out(a.dqkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
+  for (int e = tid; e < nrows * N; e += 256) {  // dU rows (N not a multiple of 4: scalar)
+    const int r = e / N, n = e - r * N;
+    a.dU[R0 * N + e] = DUs[r * LE + n];
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = tid + 256 * j;
+    if (n < N) {
+      if (a.gpart) a.gpart[(int64_t)blockIdx.x * N + n] = gsum[j];
+      if (a.bpart) a.bpart[(int64_t)blockIdx.x * N + n] = bsum[j];
+    }
+  }
+  const int np = nrows / T;
+  if (a.res_mode == DSTAGNN_RES_FULL && a.dres) tf_copy_out(a.dres + P0 * kTfH * T * T, DSs, 1, np * kTfH * T * T, 0, tid);
+  const int nch = (int)(a.FT / kTfRows);
+  const int64_t bwg = (uint32_t)R0 / (uint32_t)a.FT, chw = ((uint32_t)R0 - (uint32_t)bwg * (uint32_t)a.FT) / kTfRows;
+  if (a.res_mode == DSTAGNN_RES_BCAST) {
+    for (int e = tid; e < kTfH * T * T; e += 256) {
+      float v = 0.f;
+      for (int p = 0; p < PW; ++p) v += DSs[p * kTfH * T * T + e];  // problems in order
+      tf_st_agent(a.dpart + (bwg * nch + chw) * kTfH * T * T + e, v);
+    }
+  }
+  TF_MARK(5);
+  TF_PRINT("tat_fused_bwd", 6);
+
+  // ---- F. broadcast res_att gradient: the last workgroup of each b sums the chunks in order ---
   if (a.res_mode == DSTAGNN_RES_BCAST) {
     int& last = *reinterpret_cast<int*>(DSs + kTfDsMax);  // (no static __shared__: it would shift the dynamic base)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -713,10 +852,6 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 size_t tat_fused_bwd_lds(int NP) {
   return sizeof(float) * ((size_t)kTfRows * (NP + 4) + (size_t)kTfRows * kTfLQ + (size_t)kTfRows * kTfLC + 4 * 16 * 17 +
                           kTfDsMax + 4);
-}
-
-size_t tat_fused_lds(int NP) {
-  return sizeof(float) * ((size_t)kTfRows * (NP + 4) + (size_t)kTfRows * kTfLQ + (size_t)kTfRows * kTfLC);
 }
 
 }  // namespace
