@@ -1452,7 +1452,15 @@ struct Bwd {
     if (side_any) DS_TRY(fork_k());  // (its flag rides on the fused kernel)
     TatFusedBwdArgs t;
     t.dO = w.dO; t.u = s.u_tat; t.mu = s.mu_tat; t.rs = s.rs_tat; t.g = p.tat_ln_g;
-    t.gpart = w.gcon_a; t.bpart = w.gcon_a + m.tf_wg * N;
+    // gamma / beta: the kernel's two-level ticket tree sums its partial rows (level-2 rows after
+    // them in the same slabs); TATLN_SIDE keeps the column-sum launch on the side stream (A/B)
+    t.gpart = w.gcon_a; t.bpart = w.gcon_a + tat_bslab() * N;
+#ifdef DSTAGNN_RACEBUG_NOFORK
+    t.ln_fold = 0;  // (the racy build's side-stream column sums must be the only writer)
+#else
+    t.ln_fold = !tatln_side();
+#endif
+    t.gout = gd.tat_ln_g; t.bout = gd.tat_ln_b;
     t.dU = w.dU; t.wfcT = s.WfcT;
     t.qkv = s.qkv; t.att = s.att; t.dre = dre; t.dqkv = w.dqkv;
     t.res_mode = d.res_mode;
@@ -1614,9 +1622,11 @@ struct Bwd {
     static const bool on = getenv("DSTAGNN_TATLN_SIDE") && atoi(getenv("DSTAGNN_TATLN_SIDE")) != 0;
     return on;
   }
+  // fused TAt backward: the beta slab's first row (gamma: level-1 rows, then the ticket tree's level-2 rows)
+  int64_t tat_bslab() const { return m.tf_wg + cdiv64(m.tf_wg, 16); }
   int tat_ln_colsums(bool on_main) {
     if (m.tfused_bwd)  // one gamma / beta partial row per fused-kernel workgroup
-      return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + m.tf_wg * m.N, gd.tat_ln_b}}, m.tf_wg, m.N, 1, on_main);
+      return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + tat_bslab() * m.N, gd.tat_ln_b}}, m.tf_wg, m.N, 1, on_main);
     if (tat_part()) {
       const int64_t pb = ln_bwd_part_blocks(m.BFT);
       return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + pb * m.N, gd.tat_ln_b}}, pb, m.N, 1, on_main);
@@ -1693,7 +1703,7 @@ struct Bwd {
     // WITHOUT a fork after the LayerNorm backward that writes their partials
     DS_TRY(tat_ln_colsums(false));
 #else
-    if (!tatln_side()) DS_TRY(tat_ln_colsums(true));
+    if (!tatln_side() && !m.tfused_bwd) DS_TRY(tat_ln_colsums(true));  // (fused: summed in-kernel)
 #endif
     DS_TRY(order_err);
     DS_TRY(join());

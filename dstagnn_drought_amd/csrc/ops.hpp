@@ -278,7 +278,8 @@ int op_tat_fused_fwd(const TatFusedArgs& a, hipStream_t st);
 struct TatFusedBwdArgs {
   const float* dO = nullptr;  // O's [(f,t)][(b,n)] order
   const float *u = nullptr, *mu = nullptr, *rs = nullptr, *g = nullptr;
-  float *gpart = nullptr, *bpart = nullptr;  // (ceil(BFT / 48), N) gamma / beta partial rows
+  float *gpart = nullptr, *bpart = nullptr;  // (ceil(BFT / 48), N) gamma / beta partial rows (+ level-2 rows)
+  int ln_fold = 0; float *gout = nullptr, *bout = nullptr;  // ln_fold: the column sums in-kernel -> gout / bout
   float* dU = nullptr;                       // (BFT, N)
   const float* wfcT = nullptr;               // (h dv, NP) zero-padded transpose of TAt.fc.weight
   const float *qkv = nullptr, *att = nullptr, *dre = nullptr;
@@ -291,6 +292,7 @@ struct TatFusedBwdArgs {
   float* dE = nullptr;                       // first block: (BFT, N)
   int64_t FT = 0, BFT = 0, BN = 0;
   int F = 0, T = 0, N = 0, NP = 0, h = 0;
+  int B = 0;  // (set by the launcher)
   float scale = 1.f;
   uint32_t* sig = nullptr; uint32_t sig_v = 0;
 };

@@ -40,6 +40,7 @@ constexpr int kTfQTW = (kTfQT + 3) / 4; // 5 per wave (the last of waves 2, 3 is
 constexpr int kTfNmax = 320;            // N <= 320 (LDS: <= 156 KB)
 constexpr int kTfRPW = kTfRows / 4;     // LayerNorm rows per wave
 constexpr int kTfDsMax = 2304;          // (48 / T) h T^2 at T = 16
+constexpr int kTfG1 = 16;               // workgroups per level-1 group of the gamma / beta ticket tree
 
 // phase timestamps (a variant build with -DDSTAGNN_TF_TIMING, e.g. into abtest/tftime): thread 0
 // of workgroups 0 and 100 prints the wall-clock (100 MHz) deltas between the marks
@@ -804,12 +805,18 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     const int r = e / N, n = e - r * N;
     a.dU[R0 * N + e] = DUs[r * LE + n];
   }
+  const bool lnf = a.ln_fold != 0;  // gamma / beta summed in-kernel by a two-level ticket tree
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = tid + 256 * j;
     if (n < N) {
-      if (a.gpart) a.gpart[(int64_t)blockIdx.x * N + n] = gsum[j];
-      if (a.bpart) a.bpart[(int64_t)blockIdx.x * N + n] = bsum[j];
+      if (lnf) {
+        tf_st_agent(a.gpart + (int64_t)blockIdx.x * N + n, gsum[j]);
+        tf_st_agent(a.bpart + (int64_t)blockIdx.x * N + n, bsum[j]);
+      } else {
+        if (a.gpart) a.gpart[(int64_t)blockIdx.x * N + n] = gsum[j];
+        if (a.bpart) a.bpart[(int64_t)blockIdx.x * N + n] = bsum[j];
+      }
     }
   }
   const int np = nrows / T;
@@ -826,26 +833,81 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   TF_MARK(5);
   TF_PRINT("tat_fused_bwd", 6);
 
-  // ---- F. broadcast res_att gradient: the last workgroup of each b sums the chunks in order ---
-  if (a.res_mode == DSTAGNN_RES_BCAST) {
-    int& last = *reinterpret_cast<int*>(DSs + kTfDsMax);  // (no static __shared__: it would shift the dynamic base)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      last = atomicAdd(a.cnt + bwg, 1) == nch - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.cnt + bwg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-      }
+  // ---- F. ticket folds (the partials above went out with agent-scope stores; the last arrival
+  // takes an agent acquire and sums in a fixed order: deterministic) ---------------------------
+  //   res_att (broadcast): the last workgroup of each sample b sums its nch chunks;
+  //   LayerNorm gamma / beta: the last of each group of kTfG1 workgroups sums the group's rows
+  //   into a level-2 row, the last group sums the level-2 rows into the parameter gradients
+  //   (this replaced a colsum2d launch at the end of the main stream)
+  if (a.res_mode != DSTAGNN_RES_BCAST && !lnf) return;
+  int* flag = reinterpret_cast<int*>(DSs + kTfDsMax);  // (no static __shared__: it would shift the dynamic base)
+  const int nwg = (int)gridDim.x, ng = (nwg + kTfG1 - 1) / kTfG1, g1 = (int)blockIdx.x / kTfG1;
+  const int gsz = min(kTfG1, nwg - g1 * kTfG1);
+  int* cnt_ln = a.cnt + a.B;  // [ng] level-1 tickets, then one level-2 ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int lb = a.res_mode == DSTAGNN_RES_BCAST && atomicAdd(a.cnt + bwg, 1) == nch - 1;
+    const int lg = lnf && atomicAdd(cnt_ln + g1, 1) == gsz - 1;
+    if (lb || lg) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
-    if (!last) return;
+    if (lb) __hip_atomic_store(a.cnt + bwg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    if (lg) __hip_atomic_store(cnt_ln + g1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = lb;
+    flag[1] = lg;
+  }
+  __syncthreads();
+  const bool lb = flag[0] != 0, lg = flag[1] != 0;
+  if (lb) {
     for (int e = tid; e < kTfH * T * T; e += 256) {
       float v = 0.f;
       for (int ch = 0; ch < nch; ++ch) v += tf_ld_agent(a.dpart + (bwg * nch + ch) * kTfH * T * T + e);
       a.dres[bwg * kTfH * T * T + e] = v;
     }
+  }
+  if (!lg) return;
+  float* l2g = a.gpart + (int64_t)nwg * N;  // level-2 rows [ng][N] after the level-1 rows (slab of BFT x N)
+  float* l2b = a.bpart + (int64_t)nwg * N;
+  for (int e = tid; e < 2 * N; e += 256) {  // (column, gamma | beta): the group's rows in order
+    const int n = e % N, wh = e / N;
+    const float* src = (wh ? a.bpart : a.gpart) + (int64_t)g1 * kTfG1 * N + n;
+    float u[kTfG1];
+#pragma unroll
+    for (int k = 0; k < kTfG1; ++k) u[k] = k < gsz ? tf_ld_agent(src + (int64_t)k * N) : 0.f;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < kTfG1; ++k) v += u[k];
+    tf_st_agent((wh ? l2b : l2g) + (int64_t)g1 * N + n, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int last2 = atomicAdd(cnt_ln + ng, 1) == ng - 1;
+    if (last2) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt_ln + ng, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    flag[2] = last2;
+  }
+  __syncthreads();
+  if (!flag[2]) return;
+  for (int e = tid; e < 2 * N; e += 256) {
+    const int n = e % N, wh = e / N;
+    float* out = wh ? a.bout : a.gout;
+    if (!out) continue;
+    const float* src = (wh ? l2b : l2g) + n;
+    float v = 0.f;
+    for (int k0 = 0; k0 < ng; k0 += kTfG1) {
+      float u[kTfG1];
+#pragma unroll
+      for (int k = 0; k < kTfG1; ++k) u[k] = k0 + k < ng ? tf_ld_agent(src + (int64_t)(k0 + k) * N) : 0.f;
+#pragma unroll
+      for (int k = 0; k < kTfG1; ++k) v += u[k];
+    }
+    out[n] = v;
   }
 }
 
@@ -932,12 +994,16 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
     return DSTAGNN_E_SHAPE;
   }
   TatFusedBwdArgs a = a0;
-  if (a.res_mode == DSTAGNN_RES_BCAST) {
-    if (!a.dres) {
-      a.res_mode = DSTAGNN_RES_NONE;  // nothing to fold
-    } else {
-      a.cnt = stream_counters(st, (int)(a.BFT / a.FT));
-      if (!a.cnt || !a.dpart) { set_last_error("tat_fused_bwd: no ticket counters"); return DSTAGNN_E_ARG; }
+  if (a.res_mode == DSTAGNN_RES_BCAST && !a.dres) a.res_mode = DSTAGNN_RES_NONE;  // nothing to fold
+  const int64_t nwg = cdiv64(a.BFT, kTfRows);
+  a.B = (int)(a.BFT / a.FT);
+  a.ln_fold = a.ln_fold && a.gpart && a.bpart && (a.gout || a.bout);
+  if (a.res_mode == DSTAGNN_RES_BCAST || a.ln_fold) {
+    // [B] res_att tickets, then the gamma / beta tree's [ng] level-1 tickets and one level-2 ticket
+    a.cnt = stream_counters(st, (int)(a.B + cdiv64(nwg, kTfG1) + 1));
+    if (!a.cnt || (a.res_mode == DSTAGNN_RES_BCAST && !a.dpart)) {
+      set_last_error("tat_fused_bwd: no ticket counters");
+      return DSTAGNN_E_ARG;
     }
   }
   const StreamSig sg = peek_stream_sig(st);
