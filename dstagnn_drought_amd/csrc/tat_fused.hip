@@ -80,8 +80,18 @@ __device__ __forceinline__ float xsum16(float v) {
 __device__ __forceinline__ float f4at(const float4& v, int s) {
   return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
 }
-__device__ __forceinline__ float rdlane(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+// NV independent full-wave sums, every lane ending with every total: the xor butterfly run
+// level by level over all NV values, so each level's NV shuffles are independent (one shuffle
+// latency per level, not per value).  Fixed order, and lanes agree bitwise (each level adds two
+// values in either order: commutative).  (common.hpp's wave_sum_many selects between halves of
+// its register array by lane; the compiler turned that into lane-indexed array accesses with
+// compare chains whose masks spilled ~600 SGPRs here: the forward LayerNorm phase took 16 us.)
+template <int NV>
+__device__ __forceinline__ void tf_wave_sums(float (&v)[NV]) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], o, 64);
 }
 __device__ __forceinline__ float tf_ld_agent(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -299,10 +309,11 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
     const int task = w + 4 * k;
-    if (task >= NTASK) break;
+    // (continue, not break: a break leaves the loop not fully unrolled and the per-task register
+    // arrays rr / at / dr dynamically indexed — readlane / cndmask chains, measured 2x slower)
+    if (task >= NTASK || (task / kTfH) * T >= nrows) continue;  // (wave-uniform)
     const int p = task / kTfH, hd = task - p * kTfH;
     const int rb = p * T;
-    if (rb >= nrows) break;  // (wave-uniform)
     const float* Qp = Qs + rb * kTfLQ + hd * kTfD;
     const float* Kp = Qp + kTfHV;
     const float* Vp = Qp + 2 * kTfHV;
@@ -397,7 +408,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
   // the row sums of all 12 rows in one multi-value reduction instead of 12 dependent chains) ----
   {
     float v[kTfRPW][NTW];
-    float s16[16];
+    float s16[kTfRPW];
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
       const float* row = Es + (w + 4 * k) * LE;
@@ -410,12 +421,10 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
       }
       s16[k] = sum;
     }
-#pragma unroll
-    for (int k = kTfRPW; k < 16; ++k) s16[k] = 0.f;
-    const float tot = wave_sum_many<16>(s16);  // lane 4k holds row k's sum
+    tf_wave_sums(s16);
     float mean[kTfRPW];
 #pragma unroll
-    for (int k = 0; k < kTfRPW; ++k) mean[k] = rdlane(tot, 4 * k) / N;
+    for (int k = 0; k < kTfRPW; ++k) mean[k] = s16[k] / N;
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
       float var = 0.f;
@@ -429,9 +438,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
       }
       s16[k] = var;
     }
-#pragma unroll
-    for (int k = kTfRPW; k < 16; ++k) s16[k] = 0.f;
-    const float tv = wave_sum_many<16>(s16);
+    tf_wave_sums(s16);
     float gv[NTW], bv[NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
@@ -442,9 +449,9 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
       const int r = w + 4 * k;
-      if (r >= nrows) break;
+      if (r >= nrows) continue;
       const int64_t R = R0 + r;
-      const float rs = rsqrtf(rdlane(tv, 4 * k) / N + a.eps);
+      const float rs = rsqrtf(s16[k] / N + a.eps);
       if (l == 0) {
         a.mu[R] = mean[k];
         a.rs[R] = rs;
@@ -571,7 +578,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       bp[j] = 0.f;
       gl[j] = l + 64 * j < N ? a.g[min(l + 64 * j, N - 1)] : 0.f;
     }
-    float s32[32], xh[kTfRPW][NTW];
+    float s32[2 * kTfRPW], xh[kTfRPW][NTW];
     float mean[kTfRPW], rsv[kTfRPW];
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
@@ -593,16 +600,14 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
         bp[j] += dyv[k][j];
       }
       s32[k] = s1;
-      s32[16 + k] = s2;
+      s32[kTfRPW + k] = s2;
     }
-#pragma unroll
-    for (int k = kTfRPW; k < 16; ++k) { s32[k] = 0.f; s32[16 + k] = 0.f; }
-    const float tot = wave_sum_many<32>(s32);  // lanes 2v, 2v + 1 hold value v
+    tf_wave_sums(s32);
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
       const int r = w + 4 * k;
       float* dur = DUs + r * LE;
-      const float s1 = rdlane(tot, 2 * k) / N, s2 = rdlane(tot, 2 * (16 + k)) / N;
+      const float s1 = s32[k] / N, s2 = s32[kTfRPW + k] / N;
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
         const int n = l + 64 * j;
@@ -674,10 +679,11 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
     const int task = w + 4 * k;
-    if (task >= NTASK) break;
+    // (continue, not break: a break leaves the loop not fully unrolled and the per-task register
+    // arrays rr / at / dr dynamically indexed — readlane / cndmask chains, measured 2x slower)
+    if (task >= NTASK || (task / kTfH) * T >= nrows) continue;  // (wave-uniform)
     const int p = task / kTfH, hd = task - p * kTfH;
     const int rb = p * T;
-    if (rb >= nrows) break;  // (wave-uniform)
     float* Qp = Qs + rb * kTfLQ + hd * kTfD;
     float* Kp = Qp + kTfHV;
     float* Vp = Qp + 2 * kTfHV;
