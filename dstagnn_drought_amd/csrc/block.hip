@@ -1126,7 +1126,17 @@ struct Bwd {
     return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, q == st ? w.part : w.part_side, kPart, q);
   }
   int gemm(const Gemm& g) { return run_gemm(g, w.gemm_ws, kGemmWs, st); }
-  int sgemm(const Gemm& g) { return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sq()); }
+  // side-stream weight gradients: their own split-K target (DSTAGNN_SIDE_SPLITK, A/B knob; 0 = the
+  // global one) — fewer K slices mean a cheaper fold and fewer CUs taken from the main chain
+  static int side_splitk() {
+    static const int t = getenv("DSTAGNN_SIDE_SPLITK") ? atoi(getenv("DSTAGNN_SIDE_SPLITK")) : 0;
+    return t;
+  }
+  int sgemm(const Gemm& g0) {
+    Gemm g = g0;
+    if (sd != st && !g.splitk_target) g.splitk_target = side_splitk();
+    return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sq());
+  }
 
   int stage_tail() {
     GtuTailArgs t;  // LN / residual backward -> dtc -> dG = dtc W -> gates backward, per node
@@ -1210,6 +1220,8 @@ struct Bwd {
           DS_TRY(colsum_on(sd, w.dconv[q], m.BN * m.T + ks - 1, (int)C2, 1, gd.gtu_b[q]));
         }
       }
+      if (sd != st)
+        for (int q = 0; q < nw; ++q) dws[q].splitk_target = side_splitk();
       if (nw) DS_TRY(run_gemm_group(dws, nw, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sq()));
     }
     return 0;

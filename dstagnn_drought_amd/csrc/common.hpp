@@ -287,6 +287,7 @@ struct Gemm {
   // optional column sums of A over k: ones_out[m * ones_stride] = alpha * sum_k A[m][k] (a bias
   // gradient folded into its weight-gradient GEMM); plain epilogue only (no beta/bias/relu/emask)
   float* ones_out = nullptr; int64_t ones_stride = 1;
+  int splitk_target = 0;  // split-K workgroup target for this call (0: the global target)
   Gemm() { am = ak = az = bk = bn = bz = cm = cn = cz = om = on = oz = idx1(0); }
 };
 // ws: split-K partial slab scratch (may be null -> no split)

@@ -595,7 +595,9 @@ int plan_gemm(const Gemm& g, float* ws, size_t ws_floats, Plan* out) {
   static const int min_grid = getenv("DSTAGNN_SPLITK_MINGRID") ? atoi(getenv("DSTAGNN_SPLITK_MINGRID")) : 128;
   static const int min_k = getenv("DSTAGNN_SPLITK_MINK") ? atoi(getenv("DSTAGNN_SPLITK_MINK")) : 512;
   if (g.K > 0 && blocks < min_grid && g.K >= min_k && ws) {
-    int want = (int)std::min<int64_t>(512, cdiv64(g_splitk_target, blocks));
+    // (a per-call target yields to the global "split-K off" = 1 of the deterministic tests)
+    const int target = (g.splitk_target > 0 && g_splitk_target != 1) ? g.splitk_target : g_splitk_target;
+    int want = (int)std::min<int64_t>(512, cdiv64(target, blocks));
     int maxk = g.K / 128;  // keep >= 128 k per split
     splitk = std::max(1, std::min(want, maxk));
     if (env_split > 0) splitk = std::min(env_split, std::max(1, g.K / 64));
