@@ -52,8 +52,9 @@ constexpr int kTfG1 = 16;               // workgroups per level-1 group of the g
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 100)) {                           \
       double d_[12];                                                                            \
       for (int k_ = 1; k_ < (n); ++k_) d_[k_] = (double)(tmark[k_] - tmark[k_ - 1]) / 100.0;    \
-      printf("%s wg %d: %.2f %.2f %.2f %.2f %.2f %.2f us\n", tag, (int)blockIdx.x, d_[1], d_[2], \
-             d_[3], d_[4], d_[5], (n) > 6 ? d_[6] : 0.0);                                       \
+      for (int k_ = (n); k_ < 12; ++k_) d_[k_] = 0.0;                                          \
+      printf("%s wg %d: %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f us\n", tag, (int)blockIdx.x, \
+             d_[1], d_[2], d_[3], d_[4], d_[5], d_[6], d_[7], d_[8], d_[9]);                    \
     }                                                                                           \
   } while (0)
 #else
@@ -518,30 +519,9 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   TF_DECL;
   TF_MARK(0);
 
-  // ---- A0. every load of the first phases in one round: Q|K|V rows (-> LDS), the softmax and
-  // d re_At of this wave's attention tasks, the wave's 12 LayerNorm rows of dO and u ----------
-  constexpr int QV4 = kTfRows * kTfQW / 4 / 256;  // 13.5 -> 14 float4 per thread
-  float4 qv[QV4 + 1];
-  {
-    const float4* gq = reinterpret_cast<const float4*>(a.qkv + R0 * kTfQW);
-    const int tot = nrows * (kTfQW / 4);
-#pragma unroll
-    for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * 256 + tid, tot - 1)];
-  }
-  float at[TPW][4], dr[TPW][4];
-#pragma unroll
-  for (int k = 0; k < TPW; ++k) {
-    const int task = w + 4 * k, p = task / kTfH, hd = task - p * kTfH;
-    const bool live = task < NTASK && p * T < nrows;
-    const int64_t sbase = ((P0 + p) * kTfH + hd) * T * T;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int ii = 4 * q + s;
-      const bool ok = live && ii < T && i < T;
-      at[k][s] = ok ? a.att[sbase + ii * T + i] : 0.f;
-      dr[k][s] = ok && a.dre ? a.dre[sbase + ii * T + i] : 0.f;
-    }
-  }
+  // ---- A0. every load of the first phases in one round, in order of use: the wave's 12
+  // LayerNorm rows of dO and u (the LayerNorm waits only for these: vmcnt counts in order), the
+  // softmax and d re_At of the wave's attention tasks, the Q|K|V rows (to LDS after the LayerNorm)
   float dyv[kTfRPW][NTW], uu[kTfRPW][NTW];
 #pragma unroll
   for (int k = 0; k < kTfRPW; ++k) {
@@ -557,17 +537,30 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       uu[k][j] = ur[e];
     }
   }
-  {
-    const int tot = nrows * (kTfQW / 4);
+  float at[TPW][4], dr[TPW][4];
 #pragma unroll
-    for (int u = 0; u <= QV4; ++u) {
-      const int e = u * 256 + tid;
-      if (e < tot) {
-        const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
-        *reinterpret_cast<float4*>(Qs + r * kTfLQ + 4 * c4) = qv[u];
-      }
+  for (int k = 0; k < TPW; ++k) {
+    const int task = w + 4 * k, p = task / kTfH, hd = task - p * kTfH;
+    const bool live = task < NTASK && p * T < nrows;
+    const int64_t sbase = ((P0 + p) * kTfH + hd) * T * T;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ii = 4 * q + s;
+      const bool ok = live && ii < T && i < T;
+      at[k][s] = ok ? a.att[sbase + ii * T + i] : 0.f;
+      dr[k][s] = ok && a.dre ? a.dre[sbase + ii * T + i] : 0.f;
     }
   }
+  constexpr int QV4 = kTfRows * kTfQW / 4 / 256;  // 13.5 -> 14 float4 per thread
+  float4 qv[QV4 + 1];
+  {
+    const float4* gq = reinterpret_cast<const float4*>(a.qkv + R0 * kTfQW);
+    const int tot = nrows * (kTfQW / 4);
+#pragma unroll
+    for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * 256 + tid, tot - 1)];
+  }
+  TF_MARK(1);
+  TF_MARK(2);
   // ---- A1. LayerNorm(N) backward of the wave's 12 rows at once (ln_bwd_kernel's arithmetic) --
   float gp[NTW], bp[NTW], gsum[2], bsum[2];
   {
@@ -615,6 +608,18 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       }
     }
   }
+  {
+    const int tot = nrows * (kTfQW / 4);
+#pragma unroll
+    for (int u = 0; u <= QV4; ++u) {
+      const int e = u * 256 + tid;
+      if (e < tot) {
+        const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
+        *reinterpret_cast<float4*>(Qs + r * kTfLQ + 4 * c4) = qv[u];
+      }
+    }
+  }
+  TF_MARK(3);
   {  // gamma / beta: the four waves' partials summed in wave order (kept for the end)
     float* red = Cs;  // [2][4][NP] (Cs is free until phase B's epilogue)
 #pragma unroll
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
     __syncthreads();
   }
-  TF_MARK(1);
+  TF_MARK(4);
 
   // ---- B. dctx = dU W_fc  (48 x h dv, contraction over the NP nodes) -----------------------
   {
@@ -658,7 +663,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
   __syncthreads();
-  TF_MARK(2);
+  TF_MARK(5);
 
   // the dx tile of D1's epilogue (inner block), issued now: it lands during C and D1
   float4 dxo[3][NTW];
@@ -765,7 +770,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
   __syncthreads();
-  TF_MARK(3);
+  TF_MARK(6);
 
   // ---- D1. dE = dU + dqkv [Wq; Wk; Wv] ---------------------------------------------------
   {
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 #pragma unroll
     for (int j = 0; j < NTW; ++j) wp[j] = a.wqT + (int64_t)(min(w + 4 * j, NT - 1) * 16 + i) * kTfQW + 4 * q;
     tf_gemm_rows48(acc, Qs, kTfLQ, kTfQW / 16, i, q, wp);
-    TF_MARK(4);
+    TF_MARK(7);
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int n = (w + 4 * j) * 16 + i;
@@ -805,6 +810,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
 
+  TF_MARK(8);
   // ---- E. the saved tiles and partials (stores last: see tf_copy_out) ----------------------
   tf_copy_out(a.dqkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
   for (int e = tid; e < nrows * N; e += 256) {  // dU rows (N not a multiple of 4: scalar)
@@ -836,8 +842,8 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       tf_st_agent(a.dpart + (bwg * nch + chw) * kTfH * T * T + e, v);
     }
   }
-  TF_MARK(5);
-  TF_PRINT("tat_fused_bwd", 6);
+  TF_MARK(9);
+  TF_PRINT("tat_fused_bwd", 10);
 
   // ---- F. ticket folds (the partials above went out with agent-scope stores; the last arrival
   // takes an agent acquire and sums in a fixed order: deterministic) ---------------------------
