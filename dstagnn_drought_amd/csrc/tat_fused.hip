@@ -519,22 +519,67 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   TF_DECL;
   TF_MARK(0);
 
-  // ---- A0. every load of the first phases in one round, in order of use: the wave's 12
-  // LayerNorm rows of dO and u (the LayerNorm waits only for these: vmcnt counts in order), the
-  // softmax and d re_At of the wave's attention tasks, the Q|K|V rows (to LDS after the LayerNorm)
-  float dyv[kTfRPW][NTW], uu[kTfRPW][NTW];
+  // ---- A0. every load of the first phases in one round, in order of use — the LayerNorm's
+  // u block (contiguous: float4) and dO rows (float2) into LDS, the softmax and d re_At of the
+  // wave's attention tasks, the Q|K|V rows (to LDS after the LayerNorm) — wide loads: with
+  // dword loads the 63-deep vmcnt queue held ~16 KB per wave in flight, latency-bound (23 us)
+  float* Us = Qs;  // [48][LE] u (the Q|K|V + ctx regions, free until after the LayerNorm)
+  {
+    const int tot = nrows * N;
+    const float* gu = a.u + R0 * N;
+    constexpr int UV = 12;  // float4 per thread: 48 x 320 / 4 / 256 = 15 max -> two rounds at most
+    if ((tot & 3) == 0) {
+      for (int e0 = 0; e0 < tot / 4; e0 += 256 * UV) {
+        float4 v[UV];
 #pragma unroll
-  for (int k = 0; k < kTfRPW; ++k) {
-    const int r = min(w + 4 * k, nrows - 1);
-    const int64_t R = R0 + r;
-    const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
-    const float* dyr = a.dO + (int64_t)ft * a.BN + (int64_t)bb * N;
-    const float* ur = a.u + R * N;
+        for (int u = 0; u < UV; ++u) v[u] = reinterpret_cast<const float4*>(gu)[min(e0 + u * 256 + tid, tot / 4 - 1)];
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int e = min(l + 64 * j, N - 1);
-      dyv[k][j] = dyr[e];
-      uu[k][j] = ur[e];
+        for (int u = 0; u < UV; ++u) {
+          const int e4 = e0 + u * 256 + tid;
+          if (e4 >= tot / 4) continue;
+          const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int z = 0; z < 4; ++z) {
+            const int e = 4 * e4 + z, r = e / N, n = e - r * N;
+            Us[r * LE + n] = vv[z];
+          }
+        }
+      }
+    } else {
+      for (int e = tid; e < tot; e += 256) {
+        const int r = e / N, n = e - r * N;
+        Us[r * LE + n] = gu[e];
+      }
+    }
+    const int h2 = N / 2;  // dO rows: float2 (row offsets are even when N is)
+    if ((N & 1) == 0) {
+      constexpr int DV = 16;
+      const int tot2 = nrows * h2;
+      for (int e0 = 0; e0 < tot2; e0 += 256 * DV) {
+        float2 v[DV];
+#pragma unroll
+        for (int u = 0; u < DV; ++u) {
+          const int e = min(e0 + u * 256 + tid, tot2 - 1), r = e / h2, c2 = e - r * h2;
+          const int64_t R = R0 + r;
+          const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
+          v[u] = *reinterpret_cast<const float2*>(a.dO + (int64_t)ft * a.BN + (int64_t)bb * N + 2 * c2);
+        }
+#pragma unroll
+        for (int u = 0; u < DV; ++u) {
+          const int e = e0 + u * 256 + tid;
+          if (e >= tot2) continue;
+          const int r = e / h2, c2 = e - r * h2;
+          DUs[r * LE + 2 * c2] = v[u].x;
+          DUs[r * LE + 2 * c2 + 1] = v[u].y;
+        }
+      }
+    } else {
+      for (int e = tid; e < nrows * N; e += 256) {
+        const int r = e / N, n = e - r * N;
+        const int64_t R = R0 + r;
+        const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
+        DUs[r * LE + n] = a.dO[(int64_t)ft * a.BN + (int64_t)bb * N + n];
+      }
     }
   }
   float at[TPW][4], dr[TPW][4];
@@ -559,6 +604,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 #pragma unroll
     for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * 256 + tid, tot - 1)];
   }
+  __syncthreads();  // the u / dO tiles
   TF_MARK(1);
   TF_MARK(2);
   // ---- A1. LayerNorm(N) backward of the wave's 12 rows at once (ln_bwd_kernel's arithmetic) --
@@ -571,7 +617,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       bp[j] = 0.f;
       gl[j] = l + 64 * j < N ? a.g[min(l + 64 * j, N - 1)] : 0.f;
     }
-    float s32[2 * kTfRPW], xh[kTfRPW][NTW];
+    float s32[2 * kTfRPW], xh[kTfRPW][NTW], dyv[kTfRPW][NTW];
     float mean[kTfRPW], rsv[kTfRPW];
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
@@ -580,12 +626,19 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       mean[k] = a.mu[R];
       rsv[k] = a.rs[R];
       const bool live = r < nrows;
+      float uu[NTW];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int n = min(l + 64 * j, N - 1);
+        dyv[k][j] = DUs[min(r, kTfRows - 1) * LE + n];
+        uu[j] = Us[min(r, kTfRows - 1) * LE + n];
+      }
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
         const bool ok = live && l + 64 * j < N;
         if (!ok) dyv[k][j] = 0.f;
-        xh[k][j] = ok ? (uu[k][j] - mean[k]) * rsv[k] : 0.f;
+        xh[k][j] = ok ? (uu[j] - mean[k]) * rsv[k] : 0.f;
         const float dxh = dyv[k][j] * gl[j];
         s1 += dxh;
         s2 += dxh * xh[k][j];
@@ -608,6 +661,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       }
     }
   }
+  __syncthreads();  // (every wave's reads of the u tile, which the Q|K|V tile overwrites)
   {
     const int tot = nrows * (kTfQW / 4);
 #pragma unroll
@@ -813,9 +867,22 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   TF_MARK(8);
   // ---- E. the saved tiles and partials (stores last: see tf_copy_out) ----------------------
   tf_copy_out(a.dqkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
-  for (int e = tid; e < nrows * N; e += 256) {  // dU rows (N not a multiple of 4: scalar)
-    const int r = e / N, n = e - r * N;
-    a.dU[R0 * N + e] = DUs[r * LE + n];
+  if (((nrows * N) & 3) == 0) {  // dU: the workgroup's rows are one contiguous block (float4)
+    float4* g4 = reinterpret_cast<float4*>(a.dU + R0 * N);
+    for (int e4 = tid; e4 < nrows * N / 4; e4 += 256) {
+      float vv[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int e = 4 * e4 + z, r = e / N, n = e - r * N;
+        vv[z] = DUs[r * LE + n];
+      }
+      g4[e4] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    }
+  } else {
+    for (int e = tid; e < nrows * N; e += 256) {
+      const int r = e / N, n = e - r * N;
+      a.dU[R0 * N + e] = DUs[r * LE + n];
+    }
   }
   const bool lnf = a.ln_fold != 0;  // gamma / beta summed in-kernel by a two-level ticket tree
 #pragma unroll
