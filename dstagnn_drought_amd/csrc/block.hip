@@ -1152,6 +1152,15 @@ struct Bwd {
     // contributions instead of the (B,N,C,T) tensors: the column sums below read BN*C floats
     t.gpart = w.gcon_t; t.bpart = w.gcon_t + m.BN * m.C;
     if (m.first) { t.rpart = w.bcon_t; t.dpart = w.bcon_t + m.BN * m.C; }
+    // the LN gamma / beta (and residual_conv) sums folded in-kernel where the compile-time tail
+    // runs (no colsum2d launch on the side stream); level-2 rows after the partials in gcon_t
+    const bool tail_fold = gtu_tail_bwd_folds(t);
+    if (tail_fold) {
+      t.fold = 1;
+      t.fold_out[0] = gd.ln_g; t.fold_out[1] = gd.ln_b;
+      if (m.first) { t.fold_out[2] = gd.res_w; t.fold_out[3] = gd.res_b; }
+      t.fold_ws = w.gcon_t + 2 * m.BN * m.C;
+    }
     DS_TRY(op_gtu_tail_bwd(t, st));
     DS_TRY(fork_k());
     {
@@ -1186,8 +1195,9 @@ struct Bwd {
     // --- side: LN / residual / fcmy / GTU parameter gradients (one fork; its flag rides on
     // the GTU input-gradient launch, issued first)
     DS_TRY(fork_k_done());
-    DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + m.BN * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
-                    {w.bcon_t + m.BN * m.C, m.first ? gd.res_b : nullptr}}, m.BN, m.C, 1));
+    if (!tail_fold)
+      DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + m.BN * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
+                      {w.bcon_t + m.BN * m.C, m.first ? gd.res_b : nullptr}}, m.BN, m.C, 1));
     // the bias gradients ride on their weight-gradient GEMMs as a column-sum column
     // (Gemm::ones_out: sum over the reduction of the gradient operand); a bias whose weight
     // gradient is not requested gets its own column sum

@@ -25,6 +25,82 @@
 
 namespace {
 
+// agent-scope stores / loads of the in-kernel partial hand-off (colsum2d's protocol)
+__device__ __forceinline__ void gt_st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float gt_ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int kGtG1 = 64;  // workgroups (nodes) per level-1 group of the partial-sum ticket tree
+
+// the last workgroup of each kGtG1 group sums the group's rows of the NS partial arrays (fixed
+// order) into level-2 rows; the last group sums those into fold_out.  Called by every
+// workgroup after its partial rows went out with agent-scope stores.
+template <int C, int NT, int NS>
+__device__ __forceinline__ void tail_fold(const GtuTailArgs& a, float* red, int* flag) {
+  const int tid = threadIdx.x;
+  const float* part[4] = {a.gpart, a.bpart, a.rpart, a.dpart};
+  const int nwg = (int)gridDim.x, ng = (nwg + kGtG1 - 1) / kGtG1, g1 = (int)blockIdx.x / kGtG1;
+  const int gsz = min(kGtG1, nwg - g1 * kGtG1);
+  constexpr int ITEMS = NS * C, SPL = NT / ITEMS > 0 ? NT / ITEMS : 1;  // (item, row-split) per thread
+  static_assert(NT % ITEMS == 0 || ITEMS % NT == 0, "thread layout");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int last = atomicAdd(a.fold_cnt + g1, 1) == gsz - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.fold_cnt + g1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  for (int e = tid; e < ITEMS * SPL; e += NT) {  // level 1: rows [g1 * kGtG1, + gsz) of each array
+    const int it = e % ITEMS, sp = e / ITEMS, q = it / C, c = it - q * C;
+    const float* src = part[q] + (int64_t)g1 * kGtG1 * C + c;
+    float v = 0.f;
+    for (int r = sp; r < gsz; r += SPL) v += gt_ld_agent(src + (int64_t)r * C);
+    red[e] = v;
+  }
+  __syncthreads();
+  for (int it = tid; it < ITEMS; it += NT) {
+    float v = 0.f;
+    for (int sp = 0; sp < SPL; ++sp) v += red[sp * ITEMS + it];
+    gt_st_agent(a.fold_ws + ((int64_t)(it / C) * ng + g1) * C + it % C, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int last = atomicAdd(a.fold_cnt + ng, 1) == ng - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.fold_cnt + ng, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  for (int e = tid; e < ITEMS * SPL; e += NT) {  // level 2: the ng group rows
+    const int it = e % ITEMS, sp = e / ITEMS, q = it / C, c = it - q * C;
+    const float* src = a.fold_ws + (int64_t)q * ng * C + c;
+    float v = 0.f;
+    for (int r = sp; r < ng; r += SPL) v += gt_ld_agent(src + (int64_t)r * C);
+    red[e] = v;
+  }
+  __syncthreads();
+  for (int it = tid; it < ITEMS; it += NT) {
+    float v = 0.f;
+    for (int sp = 0; sp < SPL; ++sp) v += red[sp * ITEMS + it];
+    float* o = a.fold_out[it / C];
+    if (o) o[it % C] = v;
+  }
+}
+
+
 __device__ __forceinline__ void gate_index(int s, int T, int* gi, int* t) {
   const int T0 = T - 2, T1 = T - 4;
   *gi = s < T0 ? 0 : (s < T0 + T1 ? 1 : 2);
@@ -767,8 +843,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
           g = fmaf(dy, xhl[c * T + t], g);
           b += dy;
         }
-        a.gpart[bn * C + c] = g;
-        a.bpart[bn * C + c] = b;
+        if (a.fold) {
+          gt_st_agent(a.gpart + bn * C + c, g);
+          gt_st_agent(a.bpart + bn * C + c, b);
+        } else {
+          a.gpart[bn * C + c] = g;
+          a.bpart[bn * C + c] = b;
+        }
       }
     }
     for (int l = tid; l < P * T; l += NT) {  // sum_c dxhat and dxhat*xhat per t, P lane groups
@@ -826,8 +907,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
             rw = fmaf(xhl[c * T + t], a.x[bn * T + t], rw);
             rb += xhl[c * T + t];
           }
-          a.rpart[bn * C + c] = rw;
-          a.dpart[bn * C + c] = rb;
+          if (a.fold) {
+            gt_st_agent(a.rpart + bn * C + c, rw);
+            gt_st_agent(a.dpart + bn * C + c, rb);
+          } else {
+            a.rpart[bn * C + c] = rw;
+            a.dpart[bn * C + c] = rb;
+          }
         }
       }
     }
@@ -844,6 +930,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
     tail_gate_bwd<C, T, NT, NQ5>(a.dconv_pad[1], 5, T - 2, bn, last, dGs, SP, p5, q5);
     tail_gate_bwd<C, T, NT, NQ7>(a.dconv_pad[2], 7, 2 * T - 6, bn, last, dGs, SP, p7, q7);
     __syncthreads();  // LDS reuse by the next node
+  }
+  if (a.fold) {  // (one node per workgroup: the launcher sets fold only then)
+    __shared__ int flag;
+    tail_fold<C, NT, FIRST ? 4 : 2>(a, sh, &flag);
   }
 }
 
@@ -985,8 +1075,26 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
   return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, true>, lds, a, st);
 }
 
-int op_gtu_tail_bwd(const GtuTailArgs& a, hipStream_t st) {
+static bool tail_generic() {
   static const bool generic = getenv("DSTAGNN_TAIL_GENERIC") && atoi(getenv("DSTAGNN_TAIL_GENERIC")) != 0;
+  return generic;
+}
+// the compile-time C / T backward with one node per workgroup, which folds its partial sums
+// in-kernel (DSTAGNN_TAIL_FOLD=0: colsum2d launches instead)
+bool gtu_tail_bwd_folds(const GtuTailArgs& a) {
+  static const bool on = !getenv("DSTAGNN_TAIL_FOLD") || atoi(getenv("DSTAGNN_TAIL_FOLD")) != 0;
+  if (!on || tail_split_bwd(a) || tail_generic() || !a.gpart || a.BN > 65536) return false;
+  return tail_ct24(a) || (a.C == 32 && a.T == 12 && tail_ct());
+}
+
+int op_gtu_tail_bwd(const GtuTailArgs& a0, hipStream_t st) {
+  const bool generic = tail_generic();
+  GtuTailArgs a = a0;
+  a.fold = a0.fold && gtu_tail_bwd_folds(a0) && a0.fold_ws;
+  if (a.fold) {
+    a.fold_cnt = stream_counters(st, (int)cdiv64(a.BN, 64) + 1);
+    if (!a.fold_cnt) a.fold = 0;
+  }
   if (tail_split_bwd(a)) {  // long series: LN / residual | dG GEMM | gates
     if (!a.dG) { set_last_error("gtu_tail: split backward needs the dG scratch"); return DSTAGNN_E_ARG; }
     const int S = 3 * a.T - 12;

@@ -126,7 +126,13 @@ struct GtuTailArgs {
   float* gpart = nullptr; float* bpart = nullptr; float* rpart = nullptr; float* dpart = nullptr;
   float* dconv_pad[3] = {};       // rows [bn*T + t'][2C]: ks-1 zero rows + T-ks+1 gate rows per node, ks-1 zero rows after the last
   float* dG = nullptr;            // [bn][C][3T-12] scratch of the split (long-series) backward
+  // in-kernel column sums of the four partial arrays above (compile-time C / T backward, one node
+  // per workgroup; gtu_tail_bwd_folds): fold_out[q] = sum over bn of {gpart, bpart, rpart, dpart}
+  // (null: skipped) by a two-level ticket tree, level-2 rows in fold_ws (4 x ceil(BN / 64) x C)
+  int fold = 0; float* fold_out[4] = {}; float* fold_ws = nullptr;
+  int* fold_cnt = nullptr;        // (set by the launcher)
 };
+bool gtu_tail_bwd_folds(const GtuTailArgs& a);  // the launcher will fold (a.fold honoured)
 
 
 
