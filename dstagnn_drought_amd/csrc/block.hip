@@ -1444,16 +1444,24 @@ struct Bwd {
                    ln_bwd_partials_ok(m.D) ? ln_bwd_part_blocks(m.BN) : m.BN, m.D, 1));
     if (!xpart) DS_TRY(colsum_on(sd, w.dY, m.BN, m.D, 1, gd.pre_conv_b));
     if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sq()));
-    if (gd.pre_conv_w) {
-      Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
-      g.M = m.D; g.N = (int)m.FT; g.K = (int)m.BN;
-      g.A = w.dY; g.am = idx1(1); g.ak = idx1(m.D);
-      g.B = s.O; g.bk = idx1(1); g.bn = idx1(m.BN);
-      // written straight into pre_conv.weight's [d][t][0][f] layout: n = f*T + t
-      g.C = gd.pre_conv_w; g.cm = idx1(m.FT); g.cn = idx2(m.T, m.F, 1);
-      DS_TRY(sgemm(g));
-    }
+    if (gd.pre_conv_w && !dwp_main()) DS_TRY(sgemm(dwp_gemm()));
     return 0;
+  }
+
+  Gemm dwp_gemm() {
+    Gemm g;  // dWp[d,(f,t)] = sum_{(b,n)} dY[(b,n),d] O[b,f,t,n]
+    g.M = m.D; g.N = (int)m.FT; g.K = (int)m.BN;
+    g.A = w.dY; g.am = idx1(1); g.ak = idx1(m.D);
+    g.B = s.O; g.bk = idx1(1); g.bn = idx1(m.BN);
+    // written straight into pre_conv.weight's [d][t][0][f] layout: n = f*T + t
+    g.C = gd.pre_conv_w; g.cm = idx1(m.FT); g.cn = idx2(m.T, m.F, 1);
+    return g;
+  }
+  // DSTAGNN_DWP_MAIN=1: the pre_conv weight gradient as the main stream's last product instead of
+  // the side stream's (stream balance A/B: the side stream's tail sets the step's end)
+  static bool dwp_main() {
+    static const bool on = getenv("DSTAGNN_DWP_MAIN") && atoi(getenv("DSTAGNN_DWP_MAIN")) != 0;
+    return on;
   }
 
   int stage_preconv() {
@@ -1719,6 +1727,7 @@ struct Bwd {
     ht.lap("tat");
     if (!wqkv_side()) DS_TRY(tat_wqkv_grad(false));  // (+ the fc weight gradient)
     else if (!fc_side() && gd.tat_fc) DS_TRY(gemm(fc_grad_gemm()));
+    if (gd.pre_conv_w && dwp_main()) DS_TRY(gemm(dwp_gemm()));
 #ifdef DSTAGNN_RACEBUG_NOFORK
     // deliberately racy build (make racebug -> abtest/racebug; tests/test_gpu_knobs.py::
     // test_race_probe_catches_a_missing_fork): the TAt LayerNorm column sums on the side stream

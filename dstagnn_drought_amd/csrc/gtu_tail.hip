@@ -801,6 +801,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
       if (e < T * S) Wl[e] = wv[u];
     }
   }
+  float facc[4] = {0.f, 0.f, 0.f, 0.f};  // fold: this workgroup's partial sums (thread c < C)
   for (int64_t bn = blockIdx.x; bn < a.BN; bn += gridDim.x) {
     const int64_t base = bn * CT;
     const bool last = bn == a.BN - 1;
@@ -843,9 +844,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
           g = fmaf(dy, xhl[c * T + t], g);
           b += dy;
         }
-        if (a.fold) {
-          gt_st_agent(a.gpart + bn * C + c, g);
-          gt_st_agent(a.bpart + bn * C + c, b);
+        if (a.fold) {  // (tid == c < C: this workgroup's sums over its nodes)
+          facc[0] += g;
+          facc[1] += b;
         } else {
           a.gpart[bn * C + c] = g;
           a.bpart[bn * C + c] = b;
@@ -908,8 +909,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
             rb += xhl[c * T + t];
           }
           if (a.fold) {
-            gt_st_agent(a.rpart + bn * C + c, rw);
-            gt_st_agent(a.dpart + bn * C + c, rb);
+            facc[2] += rw;
+            facc[3] += rb;
           } else {
             a.rpart[bn * C + c] = rw;
             a.dpart[bn * C + c] = rb;
@@ -931,7 +932,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
     tail_gate_bwd<C, T, NT, NQ7>(a.dconv_pad[2], 7, 2 * T - 6, bn, last, dGs, SP, p7, q7);
     __syncthreads();  // LDS reuse by the next node
   }
-  if (a.fold) {  // (one node per workgroup: the launcher sets fold only then)
+  if (a.fold) {  // one partial row per workgroup (its grid-stride nodes), then the ticket tree
+    if (tid < C) {
+      gt_st_agent(a.gpart + (int64_t)blockIdx.x * C + tid, facc[0]);
+      gt_st_agent(a.bpart + (int64_t)blockIdx.x * C + tid, facc[1]);
+      if (FIRST) {
+        gt_st_agent(a.rpart + (int64_t)blockIdx.x * C + tid, facc[2]);
+        gt_st_agent(a.dpart + (int64_t)blockIdx.x * C + tid, facc[3]);
+      }
+    }
     __shared__ int flag;
     tail_fold<C, NT, FIRST ? 4 : 2>(a, sh, &flag);
   }
@@ -1075,6 +1084,10 @@ int op_gtu_tail_fwd(const GtuTailArgs& a, hipStream_t st) {
   return launch_node_kernel(gtu_tail_fwd_kernel<0, 0, true>, lds, a, st);
 }
 
+static int64_t fold_wgs() {
+  static const int v = getenv("DSTAGNN_TAIL_FOLD_WGS") ? atoi(getenv("DSTAGNN_TAIL_FOLD_WGS")) : 2048;
+  return v > 0 ? v : 2048;
+}
 static bool tail_generic() {
   static const bool generic = getenv("DSTAGNN_TAIL_GENERIC") && atoi(getenv("DSTAGNN_TAIL_GENERIC")) != 0;
   return generic;
@@ -1082,8 +1095,8 @@ static bool tail_generic() {
 // the compile-time C / T backward with one node per workgroup, which folds its partial sums
 // in-kernel (DSTAGNN_TAIL_FOLD=0: colsum2d launches instead)
 bool gtu_tail_bwd_folds(const GtuTailArgs& a) {
-  static const bool on = !getenv("DSTAGNN_TAIL_FOLD") || atoi(getenv("DSTAGNN_TAIL_FOLD")) != 0;
-  if (!on || tail_split_bwd(a) || tail_generic() || !a.gpart || a.BN > 65536) return false;
+  static const bool on = getenv("DSTAGNN_TAIL_FOLD") && atoi(getenv("DSTAGNN_TAIL_FOLD")) != 0;
+  if (!on || tail_split_bwd(a) || tail_generic() || !a.gpart) return false;
   return tail_ct24(a) || (a.C == 32 && a.T == 12 && tail_ct());
 }
 
@@ -1092,7 +1105,7 @@ int op_gtu_tail_bwd(const GtuTailArgs& a0, hipStream_t st) {
   GtuTailArgs a = a0;
   a.fold = a0.fold && gtu_tail_bwd_folds(a0) && a0.fold_ws;
   if (a.fold) {
-    a.fold_cnt = stream_counters(st, (int)cdiv64(a.BN, 64) + 1);
+    a.fold_cnt = stream_counters(st, (int)cdiv64(std::min<int64_t>(a.BN, fold_wgs()), 64) + 1);
     if (!a.fold_cnt) a.fold = 0;
   }
   if (tail_split_bwd(a)) {  // long series: LN / residual | dG GEMM | gates
@@ -1116,15 +1129,18 @@ int op_gtu_tail_bwd(const GtuTailArgs& a0, hipStream_t st) {
     return 0;
   }
   const size_t lds = bwd_lds(a, true);
+  // folding: fewer workgroups, each walking several nodes, so the per-workgroup hand-off (store
+  // drain, barrier, ticket) is paid once per ~3 nodes (one node per workgroup: 36 -> 72 us)
+  const unsigned fold_grid = (unsigned)std::min<int64_t>(a.BN, fold_wgs());
   if (tail_ct24(a) && !generic) {
-    const dim3 g(node_grid(a.BN));
+    const dim3 g(a.fold ? fold_grid : node_grid(a.BN));
     if (a.first) hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 24, 256, 1, true>), g, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 24, 256, 1, false>), g, dim3(256), 0, st, a);
     DS_CHECK_LAUNCH();
     return 0;
   }
   if (a.C == 32 && a.T == 12 && !generic && tail_ct()) {
-    const dim3 g(node_grid(a.BN));
+    const dim3 g(a.fold ? fold_grid : node_grid(a.BN));
     if (tail_ct() == 2) {
       if (a.first) hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 5, true>), g, dim3(256), 0, st, a);
       else hipLaunchKernelGGL((gtu_tail_bwd_ct_kernel<32, 12, 256, 5, false>), g, dim3(256), 0, st, a);

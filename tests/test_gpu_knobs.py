@@ -19,8 +19,9 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_GATES_BWD_SCALAR=1  the split-path GTU gates backward one element per thread (T = 144)
   DSTAGNN_TAT_FUSED=0  the temporal-attention stage as separate launches (Q|K|V GEMM, attention,
                        fc GEMM, LayerNorm, x transpose) instead of tat_fused.hip's one kernel
-  DSTAGNN_TAIL_FOLD=0  the GTU tail backward's LayerNorm / residual_conv partial sums by colsum2d
-                       launches instead of the kernel's in-kernel ticket tree
+  DSTAGNN_TAIL_FOLD=1  the GTU tail backward folds its LayerNorm / residual_conv partial sums
+                       in-kernel (ticket tree over grid-stride workgroups) instead of colsum2d
+  DSTAGNN_DWP_MAIN=1   the pre_conv weight gradient on the main stream instead of the side stream
   DSTAGNN_DEBUG_STREAMS=1  the fork invariant asserted (block.hip Bwd::sq): no side-stream work
                        issued while a fork's signal is still pending
   DSTAGNN_DEBUG_MAIN_DELAY_US / DSTAGNN_DEBUG_SIDE_DELAY_US   race probes: a 1.5 ms busy-wait
@@ -65,7 +66,8 @@ print("KNOB_OK")
                                        ("DSTAGNN_GATES_BWD_SCALAR=1", "t144k3", 2),
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems08", 4),
                                        ("DSTAGNN_TAT_FUSED=0", "pems08", 4),
-                                       ("DSTAGNN_TAIL_FOLD=0", "pems08", 4),
+                                       ("DSTAGNN_TAIL_FOLD=1", "pems08", 4),
+                                       ("DSTAGNN_DWP_MAIN=1", "pems08", 4),
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems07+flash", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
     import torch
