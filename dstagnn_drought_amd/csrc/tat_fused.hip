@@ -276,6 +276,14 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
       rr[k] = *reinterpret_cast<const float4*>(rp + i * T + 4 * q);
     }
   }
+  // the LayerNorm's gamma / beta for this lane's nodes (used at the end; loaded now)
+  float gv[NTW], bv[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int n = min(l + 64 * j, N - 1);
+    gv[j] = a.g[n];
+    bv[j] = a.bta[n];
+  }
   // ---- 1. E tile --------------------------------------------------------------------------
   tf_load_e_tile(a, R0, nrows, Es, LE, NP, N, tid, reinterpret_cast<int64_t*>(Qs));
   __syncthreads();
@@ -440,13 +448,6 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
       s16[k] = var;
     }
     tf_wave_sums(s16);
-    float gv[NTW], bv[NTW];
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int n = min(l + 64 * j, N - 1);
-      gv[j] = a.g[n];
-      bv[j] = a.bta[n];
-    }
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
       const int r = w + 4 * k;
@@ -582,6 +583,15 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       }
     }
   }
+  // the LayerNorm statistics of the wave's rows (lane k < 12: row w + 4k) and gamma, early
+  float mu_l, rs_l, gl[NTW];
+  {
+    const int64_t R = R0 + min(w + 4 * min(l, kTfRPW - 1), nrows - 1);
+    mu_l = a.mu[R];
+    rs_l = a.rs[R];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) gl[j] = a.g[min(l + 64 * j, N - 1)];
+  }
   float at[TPW][4], dr[TPW][4];
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
@@ -610,21 +620,19 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   // ---- A1. LayerNorm(N) backward of the wave's 12 rows at once (ln_bwd_kernel's arithmetic) --
   float gp[NTW], bp[NTW], gsum[2], bsum[2];
   {
-    float gl[NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       gp[j] = 0.f;
       bp[j] = 0.f;
-      gl[j] = l + 64 * j < N ? a.g[min(l + 64 * j, N - 1)] : 0.f;
+      if (l + 64 * j >= N) gl[j] = 0.f;
     }
     float s32[2 * kTfRPW], xh[kTfRPW][NTW], dyv[kTfRPW][NTW];
     float mean[kTfRPW], rsv[kTfRPW];
 #pragma unroll
     for (int k = 0; k < kTfRPW; ++k) {
       const int r = w + 4 * k;
-      const int64_t R = R0 + min(r, nrows - 1);
-      mean[k] = a.mu[R];
-      rsv[k] = a.rs[R];
+      mean[k] = __shfl(mu_l, k, 64);
+      rsv[k] = __shfl(rs_l, k, 64);
       const bool live = r < nrows;
       float uu[NTW];
 #pragma unroll
