@@ -53,6 +53,7 @@ struct Dims {
   bool tfused;      // the temporal-attention stage as one kernel per direction (tat_fused.hip)
   int NP;           // tfused: node count padded to 16 (the re-laid Q|K|V weights' row length)
   bool tfused_bwd;  // ... and its backward (tat_fused.hip)
+  bool gfused;      // the GTU stage forward as one kernel (gtu_fused.hip)
   int64_t tf_wg;    // tfused_bwd: its workgroups (one gamma / beta partial row each)
   int64_t nnz;      // flash: union-support entries
   int64_t apa_nnz;  // small-graph flash: A_pa support entries
@@ -78,6 +79,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.NP = m.tfused ? tat_fused_np(m.N) : 0;
   m.tfused_bwd = m.tfused && tat_fused_bwd_ok(m.N, m.T, m.h, m.dk, m.dv, m.F, d.res_mode);
   m.tf_wg = m.tfused_bwd ? cdiv64(m.BFT, 48) : 0;
+  m.gfused = gtu_fused_fwd_ok(m.C, m.T);
   return m;
 }
 
@@ -88,6 +90,7 @@ struct SaveBufs {
   float *Wqkv, *Wqk, *Wp, *thcat, *Wgf[3], *Wgb[3];
   float* Wqkv_p;  // tfused: [Wq; Wk; Wv] with rows zero-padded to NP
   float *WfcT, *WqT;  // tfused_bwd: W_fc^T (h dv, NP) and [Wq; Wk; Wv]^T (NP, 3 h dk), zero-padded
+  float* Wgt[3];      // gfused: GTU weights (o, j, c) for the fused GTU forward
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float *lse, *psupp, *wsupp;  // flash path: column log-sum-exp (B,K,N), P and T o P on the support (B,K,nnz)
   float *am, *amt, *papa;      // small-graph flash: A_pa o M_k (K,N,N) and its transpose, P on the A_pa support
@@ -101,6 +104,7 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   s.Wqkv_p = m.tfused ? a.take(m.QW * m.NP) : nullptr;
   s.WfcT = m.tfused_bwd ? a.take(m.HV * m.NP) : nullptr;
   s.WqT = m.tfused_bwd ? a.take(m.QW * m.NP) : nullptr;
+  for (int g = 0; g < 3; ++g) s.Wgt[g] = m.gfused ? a.take(2 * (int64_t)m.C * m.C * m.ks[g]) : nullptr;
   s.Wqk = a.take(2 * m.KD * m.D);
   s.Wp = a.take((int64_t)m.D * m.FT);
   s.thcat = a.take((int64_t)m.F * m.KC);
@@ -884,7 +888,8 @@ struct Fwd {
     for (int k = 0; k < m.K; ++k) add(2, p.theta[k], s.thcat, (int64_t)m.F * m.C, m.C, (int)m.KC, k);
     for (int g = 0; g < 3; ++g) {
       const int64_t n = 2 * (int64_t)m.C * m.C * m.ks[g];
-      add(7, p.gtu_w[g], s.Wgf[g], n, m.C, m.ks[g]);  // (j, c, o)
+      if (m.gfused) add(3, p.gtu_w[g], s.Wgt[g], n, m.C, m.ks[g]);  // (o, j, c): the fused forward
+      else add(7, p.gtu_w[g], s.Wgf[g], n, m.C, m.ks[g]);            // (j, c, o)
       add(4, p.gtu_w[g], s.Wgb[g], n, m.C, m.ks[g]);
     }
     if (m.fsmall)  // the dense A_pa o M_k of the small-graph attention kernels (:122)
@@ -970,6 +975,17 @@ struct Fwd {
   }
 
   int stage_tail(bool /*split*/) {
+    if (m.gfused) {  // convolutions + gates + fcmy + residual + LN in one kernel (gtu_fused.hip)
+      GtuFusedArgs g;
+      g.BN = m.BN; g.C = m.C; g.T = m.T; g.first = m.first;
+      g.X = s.X; g.x = x;
+      for (int q = 0; q < 3; ++q) { g.wt[q] = s.Wgt[q]; g.bias[q] = p.gtu_b[q]; g.conv[q] = s.conv[q]; }
+      g.fcmy_w = p.fcmy_w; g.fcmy_b = p.fcmy_b; g.res_w = p.res_w; g.res_b = p.res_b;
+      g.ln_g = p.ln_g; g.ln_b = p.ln_b;
+      if (d.train && d.drop_p > 0.f) { g.drop_p = d.drop_p; g.seed = d.seed; g.drop_off = drop_off(d, 1); }
+      g.G = s.G; g.tco = s.tco; g.r = s.r; g.mu = s.mu_c; g.rs = s.rs_c; g.out = out;
+      return op_gtu_fused_fwd(g, st);
+    }
     // the three independent convolutions (kernel widths 3, 5, 7) as ONE grouped launch
     if (gconv_on() && gtu_conv_fwd_ok(m.C, m.T, m.ks, 3)) {  // sliding-window kernel (gtu_tconv.hip)
       GconvArgs gc{};

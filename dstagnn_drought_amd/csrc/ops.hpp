@@ -304,6 +304,23 @@ struct TatFusedBwdArgs {
 };
 bool tat_fused_bwd_ok(int N, int T, int h, int dk, int dv, int F, int res_mode);
 int op_tat_fused_bwd(const TatFusedBwdArgs& a, hipStream_t st);
+// the GTU stage forward as one kernel (gtu_fused.hip): the three convolutions, gates, fcmy,
+// dropout, residual, ReLUs, LN over C; C = 32, T = 12
+struct GtuFusedArgs {
+  int64_t BN = 0; int C = 0, T = 0; int first = 0;
+  const float* X = nullptr;        // (BN, T, C) Chebyshev output
+  const float* x = nullptr;        // block input (B,N,F,T)
+  const float* wt[3] = {};         // GTU weights re-laid (2C, k, C) (param_prep kind 3)
+  const float* bias[3] = {};       // (2C)
+  const float* fcmy_w = nullptr; const float* fcmy_b = nullptr;
+  const float* res_w = nullptr; const float* res_b = nullptr;
+  const float* ln_g = nullptr; const float* ln_b = nullptr;
+  float drop_p = 0.f; uint64_t seed = 0; uint64_t drop_off = 0;
+  float* conv[3] = {};             // (BN (T - k + 1), 2C), bias included (saved)
+  float *G = nullptr, *tco = nullptr, *r = nullptr, *mu = nullptr, *rs = nullptr, *out = nullptr;
+};
+bool gtu_fused_fwd_ok(int C, int T);
+int op_gtu_fused_fwd(const GtuFusedArgs& a, hipStream_t st);
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st);
 int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,
