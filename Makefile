@@ -33,6 +33,20 @@ $(RACEBUG): $(filter-out build/block.o,$(OBJ)) build/racebug/block.o
 	@mkdir -p abtest/racebug
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
+# phase-timing variant of the fused kernels (-DDSTAGNN_TF_TIMING: per-phase wall-clock printf from
+# workgroups 0 and 100), loaded by LD_LIBRARY_PATH=abtest/tftime; not part of `all`
+TFTIME := abtest/tftime/libdstagnn.so
+TF_SRC := tat_fused gtu_fused
+tftime: $(TFTIME)
+
+build/tftime/%.o: dstagnn_drought_amd/csrc/%.hip dstagnn_drought_amd/csrc/*.hpp include/dstagnn.h
+	@mkdir -p build/tftime
+	$(HIPCC) $(CXXFLAGS) -DDSTAGNN_TF_TIMING -c $< -o $@
+
+$(TFTIME): $(filter-out $(patsubst %,build/%.o,$(TF_SRC)),$(OBJ)) $(patsubst %,build/tftime/%.o,$(TF_SRC))
+	@mkdir -p abtest/tftime
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
+
 # FETCH_SIZE / WRITE_SIZE width calibration (tools/pmc_step.sh)
 tools/fetch_calib: tools/fetch_calib.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@
@@ -53,6 +67,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 clean:
-	rm -rf build $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib abtest/racebug
+	rm -rf build $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib abtest/racebug abtest/tftime
 
-.PHONY: all clean racebug
+.PHONY: all clean racebug tftime

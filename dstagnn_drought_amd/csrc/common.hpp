@@ -308,3 +308,24 @@ int gemm_prof_start(int capacity);
 int gemm_prof_stop(dstagnn_prof_stats* out);
 int gemm_set_splitk_target(int target);
 int gemm_set_bf16(int on);
+
+// fused-kernel phase timestamps (a variant build with -DDSTAGNN_TF_TIMING, e.g. into
+// abtest/tftime): thread 0 of workgroups 0 and 100 prints the wall-clock (100 MHz) deltas between the marks
+#ifdef DSTAGNN_TF_TIMING
+#define TF_MARK(k) do { if (threadIdx.x == 0) tmark[k] = wall_clock64(); } while (0)
+#define TF_DECL uint64_t tmark[12] = {}
+#define TF_PRINT(tag, n)                                                                          \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 100)) {                           \
+      double d_[12];                                                                            \
+      for (int k_ = 1; k_ < (n); ++k_) d_[k_] = (double)(tmark[k_] - tmark[k_ - 1]) / 100.0;    \
+      for (int k_ = (n); k_ < 12; ++k_) d_[k_] = 0.0;                                          \
+      printf("%s wg %d: %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f us\n", tag, (int)blockIdx.x, \
+             d_[1], d_[2], d_[3], d_[4], d_[5], d_[6], d_[7], d_[8], d_[9]);                    \
+    }                                                                                           \
+  } while (0)
+#else
+#define TF_MARK(k) do {} while (0)
+#define TF_DECL
+#define TF_PRINT(tag, n) do {} while (0)
+#endif

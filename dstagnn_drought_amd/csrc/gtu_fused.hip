@@ -3,17 +3,20 @@
 // GTU.forward x3 + cat + fcmy + dropout + residual + ReLUs + LN over C (model/DSTAGNN_my.py:184-197,
 // 239-252).  Was two launches on the main stream: the grouped implicit-im2col GEMM writing the
 // three convolution outputs conv_k (B*N*(T-k+1), 2C) — 33 MB at PEMS08 — and gtu_tail_fwd_ct
-// reading them back for the gates.  Here a workgroup owns NB = 22 consecutive nodes (B*N/22 ~
-// one workgroup per CU at PEMS08) and keeps everything between X and the block output on chip:
+// reading them back for the gates.  Here a workgroup of 8 waves owns NB = 22 consecutive nodes
+// (B*N/22 ~ one workgroup per CU at PEMS08, two waves per SIMD) and keeps everything between X
+// and the block output on chip:
 //   1. the nodes' X rows (t, c) staged in LDS (rows padded to 36 floats: conflict-free float4
-//      fragments), plus every activation the tail reads, issued in the same round;
+//      fragments) with the residual source, plus the tail's per-lane parameters, in one round;
 //   2. per GTU, conv = X (*) W + b on the f32 matrix cores (v_mfma_f32_16x16x4_f32): output row
 //      (node, t') reads the contiguous window X[node][t'..t'+k-1][:] — the implicit im2col is just
 //      a row offset into the staged tile; a wave owns one channel half (16 of the C tanh columns
-//      and the same 16 sigmoid columns) for every second row tile, so the P and Q of a gate sit in
+//      and the same 16 sigmoid columns) for every fourth row tile, so the P and Q of a gate sit in
 //      the same lane: the gate tanh(P) * sigmoid(Q) is formed in registers and stored into the
 //      node's concat tile G (LDS) — conv_k still goes to HBM (the backward's gate derivative);
-//   3. fcmy + dropout + residual + ReLUs from LDS, the LayerNorm over C per (node, t).
+//   3. per node (one wave each): fcmy as a 32 x 12 x 24 product on the matrix cores, + bias,
+//      dropout, residual and ReLUs in the accumulator registers, and the LayerNorm over C per
+//      (node, t) by two cross-lane sums — no LDS round trip.
 // Weights: the GTU weights re-laid (o, j, c) (param_prep kind 3, rows of k C floats: a lane's B
 // fragment is one float4), streamed from L2 with double-buffered fragments.
 // Outputs and saved tensors are exactly the two-launch path's (conv_k, G, tco, r, mu, rs, out),
@@ -28,10 +31,11 @@ namespace {
 
 constexpr int kGC = 32, kGT = 12, kGS = 3 * kGT - 12, kGCT = kGC * kGT;  // C, T, S = 3T - 12
 constexpr int kGNB = 22;        // nodes per workgroup
+constexpr int kGW = 8;          // waves per workgroup (two per SIMD)
 constexpr int kGXS = kGC + 4;   // LDS row stride of the X tile
 constexpr int kGSP = kGS + 1;   // ... of a node channel's concat row in G
 constexpr int kGMT = (kGNB * (kGT - 2) + 15) / 16;  // row tiles of the widest output (k = 3): 14
-constexpr int kGMTW = (kGMT + 1) / 2;                // per wave (two waves per channel half): 7
+constexpr int kGMTW = (kGMT + 3) / 4;                // per wave (four waves per channel half): 4
 
 __device__ __forceinline__ floatx4 gmf16(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -39,17 +43,32 @@ __device__ __forceinline__ floatx4 gmf16(float a, float b, floatx4 c) {
 __device__ __forceinline__ float g4at(const float4& v, int s) {
   return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
 }
-__device__ __forceinline__ float gf_sigmoid(float x) { return __frcp_rn(1.f + __expf(-x)); }
-__device__ __forceinline__ float gf_tanh(float x) {  // gtu_tail.hip's fast_tanh (same arithmetic)
+// the gates with the hardware reciprocal (v_rcp_f32, 1 ulp): gtu_tail.hip's fast_tanh /
+// fast_sigmoid up to the last bit of the reciprocal
+__device__ __forceinline__ float gf_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float gf_tanh(float x) {
   const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
-  return 1.f - 2.f * __frcp_rn(e + 1.f);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
 }
 
-// one GTU (kernel width KS): conv rows m = node * Tg + t' of this workgroup, channel half h of
-// wave w, row tiles mt = w/2, w/2 + 2, ...; gates into Gs, conv_k (+ bias) to HBM
-template <int KS>
+// sum over the 16 lanes of a DPP row, the same value in every lane (quad swaps, then the half-row
+// and row mirrors)
+__device__ __forceinline__ float gf_row16_sum(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x141, 0xF, 0xF, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x140, 0xF, 0xF, true));
+  return x;
+}
+
+// one GTU (kernel width KS): conv rows m = node * Tg + t' of this workgroup; wave w owns channel
+// half h = w & 1 (16 tanh columns and the same 16 sigmoid columns) for row tiles w/2 + 4u; the
+// gates go to Gs, conv_k (+ bias) to HBM.  p0 / q0 hold the first B fragments on entry (issued
+// by the caller ahead of the previous GTU's stores); on exit they hold the next GTU's (KN = 0:
+// none).
+template <int KS, int KN>
 __device__ __forceinline__ void gf_gtu(const GtuFusedArgs& a, int q, int s_off, int64_t bn0, int nn, const float* Xs,
-                                       float* Gs, int w, int i, int lq) {
+                                       float* Gs, int w, int i, int lq, float4& p0, float4& q0) {
   constexpr int Tg = kGT - KS + 1, KK = KS * kGC, NCH = KK / 16;
   const int M = nn * Tg, MT = (M + 15) / 16;
   const int h = w & 1, mt0 = w >> 1;
@@ -58,27 +77,30 @@ __device__ __forceinline__ void gf_gtu(const GtuFusedArgs& a, int q, int s_off, 
 #pragma unroll
   for (int u = 0; u < kGMTW; ++u) {
     accp[u] = accq[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int m = min((mt0 + 2 * u) * 16 + i, M - 1);  // (clamped rows: computed, never stored)
+    const int m = min((mt0 + 4 * u) * 16 + i, M - 1);  // (clamped rows: computed, never stored)
     const int n = m / Tg, tp = m - n * Tg;
     rowoff[u] = (n * kGT + tp) * kGXS;
   }
   const float* wt = a.wt[q];  // (2C, KS C): row o = output channel, column j C + c
-  const float* wpp = wt + (int64_t)(h * 16 + i) * KK + 4 * lq;          // tanh half, channel h*16 + i
-  const float* wpq = wt + (int64_t)(kGC + h * 16 + i) * KK + 4 * lq;    // sigmoid half
+  const float* wpp = wt + (h * 16 + i) * KK + 4 * lq;          // tanh half, channel h*16 + i
+  const float* wpq = wt + (kGC + h * 16 + i) * KK + 4 * lq;    // sigmoid half
   auto step = [&](int ch, const float4& bp, const float4& bq) {
     const int j = ch >> 1, c0 = (ch & 1) * 16;  // contraction index 16 ch + 4 lq + s = j C + c
+    float4 av[kGMTW];
+#pragma unroll
+    for (int u = 0; u < kGMTW; ++u)
+      if (mt0 + 4 * u < MT) av[u] = *reinterpret_cast<const float4*>(Xs + rowoff[u] + j * kGXS + c0 + 4 * lq);
 #pragma unroll
     for (int u = 0; u < kGMTW; ++u) {
-      if (mt0 + 2 * u >= MT) continue;  // (wave-uniform)
-      const float4 av = *reinterpret_cast<const float4*>(Xs + rowoff[u] + j * kGXS + c0 + 4 * lq);
+      if (mt0 + 4 * u >= MT) continue;  // (wave-uniform)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        accp[u] = gmf16(g4at(av, s), g4at(bp, s), accp[u]);
-        accq[u] = gmf16(g4at(av, s), g4at(bq, s), accq[u]);
+        accp[u] = gmf16(g4at(bp, s), g4at(av[u], s), accp[u]);
+        accq[u] = gmf16(g4at(bq, s), g4at(av[u], s), accq[u]);
       }
     }
   };
-  float4 p0 = *reinterpret_cast<const float4*>(wpp), q0 = *reinterpret_cast<const float4*>(wpq), p1, q1;
+  float4 p1, q1;
   int ch = 0;
   for (; ch + 1 < NCH; ch += 2) {
     p1 = *reinterpret_cast<const float4*>(wpp + 16 * (ch + 1));
@@ -94,155 +116,208 @@ __device__ __forceinline__ void gf_gtu(const GtuFusedArgs& a, int q, int s_off, 
     __builtin_amdgcn_sched_barrier(0);
   }
   if (ch < NCH) step(ch, p0, q0);
-  // epilogue: D[4 lq + r][i] of row tile mt -> row m, channel c = h 16 + i
-  const int c = h * 16 + i;
-  const float bp_ = a.bias[q][c], bq_ = a.bias[q][kGC + c];
+  // the next GTU's first fragments, issued before this epilogue's stores (a later wait on them
+  // then does not wait for the stores: gfx9 counts both in vmcnt, in order)
+  if (KN > 0) {
+    constexpr int KKN = KN * kGC;
+    p0 = *reinterpret_cast<const float4*>(a.wt[q + 1] + (h * 16 + i) * KKN + 4 * lq);
+    q0 = *reinterpret_cast<const float4*>(a.wt[q + 1] + (kGC + h * 16 + i) * KKN + 4 * lq);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // epilogue: the weights are the A operand, so D[4 lq + r][i] of row tile mt is channel
+  // c0 + r = h 16 + 4 lq + r of row m = 16 mt + i: a lane's P and Q are float4 runs of a conv row
+  const int c0 = h * 16 + 4 * lq;
+  const float4 bp4 = *reinterpret_cast<const float4*>(a.bias[q] + c0);
+  const float4 bq4 = *reinterpret_cast<const float4*>(a.bias[q] + kGC + c0);
   float* conv = a.conv[q];
 #pragma unroll
   for (int u = 0; u < kGMTW; ++u) {
-    if (mt0 + 2 * u >= MT) continue;
+    if (mt0 + 4 * u >= MT) continue;
+    const int m = (mt0 + 4 * u) * 16 + i;
+    if (m >= M) continue;
+    const int n = m / Tg, tp = m - n * Tg;
+    const float4 P = make_float4(accp[u][0] + bp4.x, accp[u][1] + bp4.y, accp[u][2] + bp4.z, accp[u][3] + bp4.w);
+    const float4 Q = make_float4(accq[u][0] + bq4.x, accq[u][1] + bq4.y, accq[u][2] + bq4.z, accq[u][3] + bq4.w);
+    float* row = conv + ((bn0 + n) * Tg + tp) * (2 * kGC);
+    *reinterpret_cast<float4*>(row + c0) = P;
+    *reinterpret_cast<float4*>(row + kGC + c0) = Q;
+    float* g = Gs + (n * kGC + c0) * kGSP + s_off + tp;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = (mt0 + 2 * u) * 16 + 4 * lq + r;
-      if (m >= M) continue;
-      const int n = m / Tg, tp = m - n * Tg;
-      const float P = accp[u][r] + bp_, Q = accq[u][r] + bq_;
-      float* row = conv + ((bn0 + n) * Tg + tp) * (2 * kGC);
-      row[c] = P;
-      row[kGC + c] = Q;
-      Gs[(n * kGC + c) * kGSP + s_off + tp] = gf_tanh(P) * gf_sigmoid(Q);
-    }
+    for (int r = 0; r < 4; ++r) g[r * kGSP] = gf_tanh(g4at(P, r)) * gf_sigmoid(g4at(Q, r));
   }
 }
 
 template <bool FIRST>
-__global__ __launch_bounds__(256, 1) void gtu_fwd_fused_kernel(GtuFusedArgs a) {
-  constexpr int NE = (kGNB * kGCT + 255) / 256;  // tail elements per thread (33)
+__global__ __launch_bounds__(kGW * 64, 1) void gtu_fwd_fused_kernel(GtuFusedArgs a) {
+  constexpr int NT = kGW * 64;
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   float* Xs = lds;                                  // [NB T][36]
   float* Gs = Xs + kGNB * kGT * kGXS;               // [NB C][25]
-  float* Rl = Gs + kGNB * kGC * kGSP;               // [NB][C T] r for the LayerNorm
-  float* Wl = Rl + kGNB * kGCT;                     // [T][25] fcmy weight
-  float* mus = Wl + kGT * kGSP;                     // [NB T]
-  float* rss = mus + kGNB * kGT;                    // [NB T]
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, i = l & 15, lq = l >> 4;
+  float* Rl = Gs + kGNB * kGC * kGSP;               // the residual source: [NB][C T] (FIRST: [NB][T])
+  // (the wave index in an SGPR: every per-wave tile condition below is a scalar branch)
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, i = l & 15, lq = l >> 4;
   const int64_t bn0 = (int64_t)blockIdx.x * kGNB;
   const int nn = (int)min<int64_t>(kGNB, a.BN - bn0);
   const int ne = nn * kGCT;
+  TF_DECL;
+  TF_MARK(0);
 
-  // ---- 1. one round of loads: X tile, the fcmy weight, this thread's tail operands ----------
+  // ---- 1. one round of loads: X tile, the residual source, the first GTU's B fragments, the
+  //         fcmy A fragments and the per-channel parameters of the tail ---------------------
+  constexpr int XV = (kGNB * kGCT / 4 + NT - 1) / NT;  // 5
+  float4 p0, q0;
+  {
+    const int h = w & 1;
+    p0 = *reinterpret_cast<const float4*>(a.wt[0] + (h * 16 + i) * 3 * kGC + 4 * lq);
+    q0 = *reinterpret_cast<const float4*>(a.wt[0] + (kGC + h * 16 + i) * 3 * kGC + 4 * lq);
+  }
   {
     const float4* gx = reinterpret_cast<const float4*>(a.X + bn0 * kGCT);
-    constexpr int XV = (kGNB * kGCT / 4 + 255) / 256;  // 9
     float4 xv[XV];
 #pragma unroll
-    for (int u = 0; u < XV; ++u) xv[u] = gx[min(u * 256 + tid, ne / 4 - 1)];
-    float wv[2];
+    for (int u = 0; u < XV; ++u) xv[u] = gx[min(u * NT + tid, ne / 4 - 1)];
+    if (FIRST) {
+      if (tid < nn * kGT) Rl[tid] = a.x[bn0 * kGT + tid];
+    } else {
+      const float4* gr = reinterpret_cast<const float4*>(a.x + bn0 * kGCT);
+      float4 rv4[XV];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) wv[u] = a.fcmy_w[min(tid + 256 * u, kGT * kGS - 1)];
+      for (int u = 0; u < XV; ++u) rv4[u] = gr[min(u * NT + tid, ne / 4 - 1)];
+#pragma unroll
+      for (int u = 0; u < XV; ++u)
+        if (u * NT + tid < ne / 4) reinterpret_cast<float4*>(Rl)[u * NT + tid] = rv4[u];
+    }
 #pragma unroll
     for (int u = 0; u < XV; ++u) {
-      const int e4 = u * 256 + tid;
+      const int e4 = u * NT + tid;
       if (e4 < ne / 4) {
         const int e = 4 * e4, row = e / kGC, c = e - row * kGC;  // X rows (n t, c)
         *reinterpret_cast<float4*>(Xs + row * kGXS + c) = xv[u];
       }
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + 256 * u;
-      if (e < kGT * kGS) Wl[(e / kGS) * kGSP + e % kGS] = wv[u];
-    }
   }
-  float xr[NE];  // the residual source of this thread's tail elements e = (n, c, t)
+  // tail operands of this lane: fcmy weight rows t = i (the A operand; lanes i >= T zero) and
+  // the per-channel parameters of channels c = i and 16 + i
+  float aw[kGS / 4];  // A[m = t][k = s = 4 kk + lq] = fcmy_w[t][s]
 #pragma unroll
-  for (int u = 0; u < NE; ++u) {
-    const int e = min(tid + 256 * u, ne - 1), n = e / kGCT, t = e % kGT;
-    xr[u] = FIRST ? a.x[(bn0 + n) * kGT + t] : a.x[bn0 * kGCT + e];
+  for (int kk = 0; kk < kGS / 4; ++kk) aw[kk] = i < kGT ? a.fcmy_w[min(i, kGT - 1) * kGS + 4 * kk + lq] : 0.f;
+  const int t0 = min(4 * lq, kGT - 4);  // this lane's 4 output columns t0..t0+3 (lq = 3: a copy, not stored)
+  const float4 fb = *reinterpret_cast<const float4*>(a.fcmy_b + t0);
+  float lg[2], lb[2], rw[2], rb[2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    lg[v] = a.ln_g[16 * v + i];
+    lb[v] = a.ln_b[16 * v + i];
+    rw[v] = FIRST ? a.res_w[16 * v + i] : 0.f;
+    rb[v] = FIRST ? a.res_b[16 * v + i] : 0.f;
   }
   __syncthreads();
+  TF_MARK(1);
 
   // ---- 2. the three convolutions and their gates --------------------------------------------
-  gf_gtu<3>(a, 0, 0, bn0, nn, Xs, Gs, w, i, lq);
-  gf_gtu<5>(a, 1, kGT - 2, bn0, nn, Xs, Gs, w, i, lq);
-  gf_gtu<7>(a, 2, 2 * kGT - 6, bn0, nn, Xs, Gs, w, i, lq);
+  gf_gtu<3, 5>(a, 0, 0, bn0, nn, Xs, Gs, w, i, lq, p0, q0);
+  TF_MARK(2);
+  gf_gtu<5, 7>(a, 1, kGT - 2, bn0, nn, Xs, Gs, w, i, lq, p0, q0);
+  TF_MARK(3);
+  gf_gtu<7, 0>(a, 2, 2 * kGT - 6, bn0, nn, Xs, Gs, w, i, lq, p0, q0);
+  TF_MARK(4);
   __syncthreads();
+  TF_MARK(5);
 
-  // ---- 3. fcmy + dropout + residual + ReLUs (gtu_tail_fwd_ct's arithmetic) -----------------
-  float rv[NE];
+  // ---- 3. per node (one wave each): fcmy on the matrix cores (tc[t][c] = sum_s W[t][s] G[c][s],
+  //         two 16-channel tiles), + bias, dropout, residual, ReLUs (gtu_tail_fwd_ct's
+  //         arithmetic), then the LayerNorm over C per (node, t) in registers: lane (i, lq) holds
+  //         columns t0..t0+3 of channels i and 16 + i, the channel sums are DPP row sums ---------
+  const bool tv = lq < kGT / 4;
 #pragma unroll
-  for (int u = 0; u < NE; ++u) {
-    const int e = tid + 256 * u;
-    rv[u] = 0.f;
-    if (e >= ne) continue;
-    const int n = e / kGCT, ct = e - n * kGCT, c = ct / kGT, t = ct - c * kGT;
-    float tc = a.fcmy_b[t];
-    const float* gr = Gs + (n * kGC + c) * kGSP;
-    const float* wr = Wl + t * kGSP;
-#pragma unroll 8
-    for (int s = 0; s < kGS; ++s) tc = fmaf(gr[s], wr[s], tc);
-    const int64_t ge = bn0 * kGCT + e;  // global (b, n, c, t) index
-    if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)ge + a.drop_off, a.drop_p);
-    float tco, xres;
-    if (FIRST) {
-      tco = fmaxf(tc, 0.f);
-      xres = a.res_w[c] * xr[u] + a.res_b[c];
-    } else {
-      tco = fmaxf(Xs[(n * kGT + t) * kGXS + c] + tc, 0.f);
-      xres = xr[u];
+  for (int j = 0; j < (kGNB + kGW - 1) / kGW; ++j) {
+    const int n = w + kGW * j;
+    if (n >= nn) continue;
+    floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+    const float* g0 = Gs + (n * kGC + i) * kGSP + lq;
+#pragma unroll
+    for (int kk = 0; kk < kGS / 4; ++kk) {
+      acc[0] = gmf16(aw[kk], g0[4 * kk], acc[0]);
+      acc[1] = gmf16(aw[kk], g0[16 * kGSP + 4 * kk], acc[1]);
     }
-    const float r = fmaxf(xres + tco, 0.f);
-    a.tco[ge] = tco;
-    a.r[ge] = r;
-    Rl[e] = r;
-    rv[u] = r;
+    float rv[2][4];
+    float sum[4];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int c = 16 * v + i;
+      const int e0 = n * kGCT + c * kGT + t0;
+      const int64_t ge0 = bn0 * kGCT + e0;  // global (b, n, c, t0) index
+      float4 xres4;
+      if (!FIRST) xres4 = *reinterpret_cast<const float4*>(Rl + e0);
+      float tco[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float tc = acc[v][r] + g4at(fb, r);
+        if (a.drop_p > 0.f) tc *= drop_scale(a.seed, 1, (uint64_t)(ge0 + r) + a.drop_off, a.drop_p);
+        float xres;
+        if (FIRST) {
+          tco[r] = fmaxf(tc, 0.f);
+          xres = rw[v] * Rl[n * kGT + t0 + r] + rb[v];
+        } else {
+          tco[r] = fmaxf(Xs[(n * kGT + t0 + r) * kGXS + c] + tc, 0.f);
+          xres = g4at(xres4, r);
+        }
+        rv[v][r] = fmaxf(xres + tco[r], 0.f);
+      }
+      if (tv) {
+        *reinterpret_cast<float4*>(a.tco + ge0) = make_float4(tco[0], tco[1], tco[2], tco[3]);
+        *reinterpret_cast<float4*>(a.r + ge0) = make_float4(rv[v][0], rv[v][1], rv[v][2], rv[v][3]);
+      }
+    }
+    float mean[4], rs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sum[r] = gf_row16_sum(rv[0][r] + rv[1][r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mean[r] = sum[r] * (1.f / kGC);
+      const float d0 = rv[0][r] - mean[r], d1 = rv[1][r] - mean[r];
+      rs[r] = d0 * d0 + d1 * d1;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rs[r] = rsqrtf(gf_row16_sum(rs[r]) * (1.f / kGC) + 1e-5f);
+    if (tv) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (rv[v][r] - mean[r]) * rs[r] * lg[v] + lb[v];
+        *reinterpret_cast<float4*>(a.out + bn0 * kGCT + n * kGCT + (16 * v + i) * kGT + t0) =
+            make_float4(o[0], o[1], o[2], o[3]);
+      }
+      if (i == 0) {
+        *reinterpret_cast<float4*>(a.mu + (bn0 + n) * kGT + t0) = make_float4(mean[0], mean[1], mean[2], mean[3]);
+        *reinterpret_cast<float4*>(a.rs + (bn0 + n) * kGT + t0) = make_float4(rs[0], rs[1], rs[2], rs[3]);
+      }
+    }
   }
-  __syncthreads();
+  TF_MARK(6);
   // G out (the fcmy weight gradient's operand): the nodes' [c][s] rows are one contiguous block
-  for (int e = tid; e < nn * kGC * kGS; e += 256) {
-    const int nc = e / kGS, s = e - nc * kGS;
-    a.G[bn0 * kGC * kGS + e] = Gs[nc * kGSP + s];
-  }
-  // ---- 4. LayerNorm over C per (node, t): two fixed-order passes -----------------------------
-  for (int row = tid; row < nn * kGT; row += 256) {
-    const int n = row / kGT, t = row - n * kGT;
-    const float* rr = Rl + n * kGCT + t;
-    float sum = 0.f;
-#pragma unroll 8
-    for (int c = 0; c < kGC; ++c) sum += rr[c * kGT];
-    const float mean = sum * (1.f / kGC);
-    float var = 0.f;
-#pragma unroll 8
-    for (int c = 0; c < kGC; ++c) {
-      const float d = rr[c * kGT] - mean;
-      var += d * d;
+  {
+    float4* gout = reinterpret_cast<float4*>(a.G + bn0 * kGC * kGS);
+    for (int e4 = tid; e4 < nn * kGC * (kGS / 4); e4 += NT) {
+      const int nc = e4 / (kGS / 4), s = 4 * (e4 - nc * (kGS / 4));
+      const float* g = Gs + nc * kGSP + s;
+      gout[e4] = make_float4(g[0], g[1], g[2], g[3]);
     }
-    const float rs = rsqrtf(var * (1.f / kGC) + 1e-5f);
-    mus[row] = mean;
-    rss[row] = rs;
-    a.mu[(bn0 + n) * kGT + t] = mean;
-    a.rs[(bn0 + n) * kGT + t] = rs;
   }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < NE; ++u) {
-    const int e = tid + 256 * u;
-    if (e >= ne) continue;
-    const int n = e / kGCT, ct = e - n * kGCT, c = ct / kGT, t = ct - c * kGT;
-    a.out[bn0 * kGCT + e] = (rv[u] - mus[n * kGT + t]) * rss[n * kGT + t] * a.ln_g[c] + a.ln_b[c];
-  }
+  TF_MARK(7);
+  TF_PRINT("gtu_fused", 8);
 }
 
 size_t gtu_fused_lds() {
-  return sizeof(float) * ((size_t)kGNB * kGT * kGXS + (size_t)kGNB * kGC * kGSP + (size_t)kGNB * kGCT +
-                          (size_t)kGT * kGSP + 2 * (size_t)kGNB * kGT);
+  return sizeof(float) * ((size_t)kGNB * kGT * kGXS + (size_t)kGNB * kGC * kGSP + (size_t)kGNB * kGCT);
 }
 
 }  // namespace
 
 bool gtu_fused_fwd_ok(int C, int T) {
-  static const bool on = getenv("DSTAGNN_GTU_FUSED") && atoi(getenv("DSTAGNN_GTU_FUSED")) != 0;
+  static const bool on = !getenv("DSTAGNN_GTU_FUSED") || atoi(getenv("DSTAGNN_GTU_FUSED")) != 0;  // default on
   return on && C == kGC && T == kGT;
 }
 
@@ -268,7 +343,7 @@ int op_gtu_fused_fwd(const GtuFusedArgs& a, hipStream_t st) {
   const double flops = 2.0 * a.BN * (2.0 * kGC) * kGC * ((kGT - 2) * 3 + (kGT - 4) * 5 + (kGT - 6) * 7);
   const double bytes = 4.0 * a.BN * (kGCT * 6.0 + 2 * kGC * 24.0 + kGC * kGS);
   void* rec = gemm_prof_begin(flops, bytes, st);
-  hipLaunchKernelGGL(k, dim3((unsigned)cdiv64(a.BN, kGNB)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)cdiv64(a.BN, kGNB)), dim3(kGW * 64), lds, st, a);
   DS_CHECK_LAUNCH();
   gemm_prof_end(rec, st);
   return 0;
