@@ -54,6 +54,7 @@ struct Dims {
   int NP;           // tfused: node count padded to 16 (the re-laid Q|K|V weights' row length)
   bool tfused_bwd;  // ... and its backward (tat_fused.hip)
   bool gfused;      // the GTU stage forward as one kernel (gtu_fused.hip)
+  bool gbfused;     // ... and its backward (gtu_fused.hip): compact gate-gradient rows, no tconv
   int64_t tf_wg;    // tfused_bwd: its workgroups (one gamma / beta partial row each)
   int64_t nnz;      // flash: union-support entries
   int64_t apa_nnz;  // small-graph flash: A_pa support entries
@@ -80,6 +81,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.tfused_bwd = m.tfused && tat_fused_bwd_ok(m.N, m.T, m.h, m.dk, m.dv, m.F, d.res_mode);
   m.tf_wg = m.tfused_bwd ? cdiv64(m.BFT, 48) : 0;
   m.gfused = gtu_fused_fwd_ok(m.C, m.T);
+  m.gbfused = gtu_fused_bwd_ok(m.C, m.T);
   return m;
 }
 
@@ -889,8 +891,8 @@ struct Fwd {
     for (int g = 0; g < 3; ++g) {
       const int64_t n = 2 * (int64_t)m.C * m.C * m.ks[g];
       if (m.gfused) add(3, p.gtu_w[g], s.Wgt[g], n, m.C, m.ks[g]);  // (o, j, c): the fused forward
-      else add(7, p.gtu_w[g], s.Wgf[g], n, m.C, m.ks[g]);            // (j, c, o)
-      add(4, p.gtu_w[g], s.Wgb[g], n, m.C, m.ks[g]);
+      if (!m.gfused || m.gbfused) add(7, p.gtu_w[g], s.Wgf[g], n, m.C, m.ks[g]);  // (j, c, o): also the fused bwd
+      if (!m.gbfused) add(4, p.gtu_w[g], s.Wgb[g], n, m.C, m.ks[g]);
     }
     if (m.fsmall)  // the dense A_pa o M_k of the small-graph attention kernels (:122)
       for (int k = 0; k < m.K; ++k) {
@@ -1154,7 +1156,28 @@ struct Bwd {
     return run_gemm(g, sd == st ? w.gemm_ws : w.gemm_ws_side, kGemmWs, sq());
   }
 
+  // the GTU stage backward as one kernel (gtu_fused.hip): LN / residual / dropout backward, dG,
+  // the gate derivatives (compact (BN Tg, 2C) rows) and the transposed convolutions -> gpre
+  int stage_tail_fused() {
+    GtuFusedBwdArgs g;
+    g.BN = m.BN; g.C = m.C; g.T = m.T; g.first = m.first;
+    g.dout = dout; g.r = s.r; g.tco = s.tco; g.mu = s.mu_c; g.rs = s.rs_c; g.x = x; g.X = s.X;
+    for (int q = 0; q < 3; ++q) { g.conv[q] = s.conv[q]; g.wf[q] = s.Wgf[q]; g.dconv[q] = w.dconv[q]; }
+    g.fcmy_w = p.fcmy_w; g.ln_g = p.ln_g; g.res_w = p.res_w;
+    if (d.train && d.drop_p > 0.f) { g.drop_p = d.drop_p; g.seed = d.seed; g.drop_off = drop_off(d, 1); }
+    g.dtc = w.dtc; g.dx = dx; g.gpre = w.gpre;
+    const int64_t nwg = gtu_fused_bwd_wgs(m.BN);  // one partial-sum row per workgroup
+    g.gpart = w.gcon_t; g.bpart = w.gcon_t + nwg * m.C;
+    if (m.first) { g.rpart = w.bcon_t; g.dpart = w.bcon_t + nwg * m.C; }
+    DS_TRY(op_gtu_fused_bwd(g, st));
+    DS_TRY(fork());
+    DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + nwg * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
+                    {w.bcon_t + nwg * m.C, m.first ? gd.res_b : nullptr}}, nwg, m.C, 1));
+    return stage_tail_wgrads(true);
+  }
+
   int stage_tail() {
+    if (m.gbfused) return stage_tail_fused();
     GtuTailArgs t;  // LN / residual backward -> dtc -> dG = dtc W -> gates backward, per node
     t.BN = m.BN; t.C = m.C; t.T = m.T; t.first = m.first;
     for (int q = 0; q < 3; ++q) { t.conv[q] = s.conv[q]; t.dconv_pad[q] = w.dconv[q]; }
@@ -1214,6 +1237,11 @@ struct Bwd {
     if (!tail_fold)
       DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + m.BN * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
                       {w.bcon_t + m.BN * m.C, m.first ? gd.res_b : nullptr}}, m.BN, m.C, 1));
+    return stage_tail_wgrads(false);
+  }
+  // side: the fcmy and GTU weight / bias gradients; compact: the gate gradients in (BN Tg, 2C)
+  // rows (the fused backward) instead of the zero-padded (BN T + ks - 1, 2C) layout
+  int stage_tail_wgrads(bool compact) {
     // the bias gradients ride on their weight-gradient GEMMs as a column-sum column
     // (Gemm::ones_out: sum over the reduction of the gradient operand); a bias whose weight
     // gradient is not requested gets its own column sum
@@ -1238,12 +1266,14 @@ struct Bwd {
         if (gd.gtu_w[q]) {
           Gemm& g = dws[nw++];  // dW[o,c,j] = sum_{(bn,t')} dconv[bn,t',o] X[bn,t'+j,c]; db[o] = sum dconv[.,o]
           g.M = (int)C2; g.N = m.C * ks; g.K = (int)(m.BN * Tg);
-          g.A = w.dconv[q]; g.a_off = (ks - 1) * C2; g.am = idx1(1); g.ak = idx2(Tg, C2, cs);
+          g.A = w.dconv[q]; g.am = idx1(1);
+          if (compact) g.ak = idx1(C2);
+          else { g.a_off = (ks - 1) * C2; g.ak = idx2(Tg, C2, cs); }
           g.B = s.X; g.bk = idx2(Tg, m.C, m.CT); g.bn = idx1(1);
           g.C = gd.gtu_w[q]; g.cm = idx1((int64_t)m.C * ks); g.cn = idx2(m.C, ks, 1);
           g.ones_out = gd.gtu_b[q];
         } else {
-          DS_TRY(colsum_on(sd, w.dconv[q], m.BN * m.T + ks - 1, (int)C2, 1, gd.gtu_b[q]));
+          DS_TRY(colsum_on(sd, w.dconv[q], compact ? m.BN * Tg : m.BN * m.T + ks - 1, (int)C2, 1, gd.gtu_b[q]));
         }
       }
       if (sd != st)

@@ -310,8 +310,337 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_fwd_fused_kernel(GtuFusedArgs
   TF_PRINT("gtu_fused", 8);
 }
 
+bool gf_al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 size_t gtu_fused_lds() {
   return sizeof(float) * ((size_t)kGNB * kGT * kGXS + (size_t)kGNB * kGC * kGSP + (size_t)kGNB * kGCT);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Backward: the GTU stage's backward as ONE kernel (model/DSTAGNN_my.py:184-197, 239-252 by
+// autograd).  Was gtu_tail_bwd_ct (LN / ReLU / residual / dropout backward, dG = dtc W, the gate
+// derivatives into zero-padded 2C-wide rows, 50 MB at PEMS08) + gtu_tconv (the transposed
+// convolutions over the padded rows, 60 % of its MACs on zeros).  Here a workgroup of 8 waves
+// owns the same NB = 22 nodes as the forward:
+//   A. per node (one wave each), in the forward tail's register layout (lane (i, lq): channels
+//      i and 16 + i, columns t0..t0+3): the LayerNorm backward with DPP row sums, the ReLU /
+//      dropout / residual backward, dtc and dx out; dG = dtc W as 2 x 2 matrix-core tiles whose
+//      k steps contract t = 4 lq + r — the lane's own dtc values ARE the A fragments, and the
+//      result holds 4 consecutive channels of one s: the gate derivatives read P / Q and write
+//      dconv as float4 runs, compact (BN Tg, 2C) — the weight gradients' operand, no zero rows;
+//   B. per GTU, its gate-gradient rows staged in LDS (read back from L2: one workgroup's rows),
+//      then dX[n][t' + j][c] += sum_o dconv[(n, t')][o] W[o][c][j] input-stationary: a wave owns
+//      16-row tiles of (node, t') rows x 16-channel halves and computes all k taps against the
+//      same B fragments, then the workgroup adds tap by tap into the LDS accumulator rows
+//      shifted by j (float4 read-modify-write, a barrier between taps: a fixed summation order
+//      per output row) — exactly the convolution's MACs, none on padding;
+//   C. gpre = (X > 0) ? dX : 0 (the Chebyshev output's ReLU backward), float4 rows.
+// LN gamma / beta (and first-block residual_conv) partial sums: one row per workgroup.
+// ---------------------------------------------------------------------------------------------
+constexpr int kGBS = 2 * kGC + 4;            // LDS row stride of a staged gate-gradient / weight row
+constexpr int kGBX = kGC + 4;                // ... of a dX accumulator row
+// per GTU q: its row tiles' gate-gradient rows, then its weights (j, c) rows of 2C
+constexpr int gb_rows(int q) { return (kGNB * (kGT - 2 - 2 * q) + 15) / 16 * 16; }
+constexpr int gb_stage(int q) { return (gb_rows(q) + (3 + 2 * q) * kGC) * kGBS; }
+constexpr int gb_cmax(int a, int b) { return a > b ? a : b; }
+constexpr int kGBStage = gb_cmax(gb_stage(0), gb_cmax(gb_stage(1), gb_stage(2)));
+
+size_t gtu_fused_bwd_lds() {
+  return sizeof(float) * ((size_t)kGBStage + (size_t)kGNB * kGT * kGBX + 4 * kGW * kGC);
+}
+
+// step B for GTU KQ (kernel width KS)
+template <int KQ>
+__device__ __forceinline__ void gb_tconv(const GtuFusedBwdArgs& a, int64_t bn0, int nn, float* Ds, float* dXs, int w,
+                                         int i, int lq) {
+  constexpr int KS = 3 + 2 * KQ, Tg = kGT - KS + 1, NT = kGW * 64;
+  const int M = nn * Tg, MT = (M + 15) / 16;
+  // stage the rows (rows M..16 MT zero) and the weights (j, c, o) as rows j C + c, one round
+  constexpr int RX = gb_rows(KQ);  // rows of a full workgroup
+  float* Ws = Ds + RX * kGBS;
+  {
+    constexpr int NV = (RX * 16 + NT - 1) / NT, NW = (KS * kGC * 16 + NT - 1) / NT;
+    const float4* src = reinterpret_cast<const float4*>(a.dconv[KQ] + bn0 * Tg * 2 * kGC);
+    const float4* wsrc = reinterpret_cast<const float4*>(a.wf[KQ]);
+    float4 v[NV], wv[NW];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int e4 = u * NT + (int)threadIdx.x;
+      v[u] = e4 < M * 16 ? src[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < NW; ++u) wv[u] = wsrc[min(u * NT + (int)threadIdx.x, KS * kGC * 16 - 1)];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int e4 = u * NT + (int)threadIdx.x, row = e4 >> 4;
+      if (row < RX) *reinterpret_cast<float4*>(Ds + row * kGBS + (e4 & 15) * 4) = v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int e4 = u * NT + (int)threadIdx.x, row = e4 >> 4;
+      if (row < KS * kGC) *reinterpret_cast<float4*>(Ws + row * kGBS + (e4 & 15) * 4) = wv[u];
+    }
+  }
+  __syncthreads();
+  // every unit's k taps first (unit u = (tile u / 2, channel half u % 2), wave w: u = w + 8 uu) ...
+  constexpr int MTX = (kGNB * Tg + 15) / 16, UPW = (2 * MTX + kGW - 1) / kGW;
+  const int units = 2 * MT;
+  floatx4 acc[UPW][KS];
+#pragma unroll
+  for (int uu = 0; uu < UPW; ++uu) {
+    const int u = w + kGW * uu;
+    if (u >= units) continue;  // (wave-uniform)
+    const int mt = u >> 1, ct = u & 1;
+#pragma unroll
+    for (int j = 0; j < KS; ++j) acc[uu][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* brow = Ds + (mt * 16 + i) * kGBS + 4 * lq;             // B[k = o][n = row]
+    const float* wrow = Ws + (16 * ct + i) * kGBS + 4 * lq;             // A[m = c][k = o], tap j at + j C rows
+#pragma unroll
+    for (int ch = 0; ch < 2 * kGC / 16; ++ch) {
+      const float4 b = *reinterpret_cast<const float4*>(brow + 16 * ch);
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
+        const float4 av = *reinterpret_cast<const float4*>(wrow + j * kGC * kGBS + 16 * ch);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[uu][j] = gmf16(g4at(av, s), g4at(b, s), acc[uu][j]);
+      }
+    }
+  }
+  // ... then tap by tap into the accumulator rows: D[4 lq + r][i] is channel 16 ct + 4 lq + r of
+  // input row m = 16 mt + i, and tap j sends it to row t' + j.  For one tap the input -> output
+  // row map is one-to-one (no two writers of a row); the taps go in order with a barrier
+  // between them, so every output row sums its contributions in the fixed order (GTU, tap) —
+  // the same bits wherever the node sits in its workgroup's tiles
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+#pragma unroll
+    for (int uu = 0; uu < UPW; ++uu) {
+      const int u = w + kGW * uu;
+      if (u >= units) continue;
+      const int mt = u >> 1, ct = u & 1, m = mt * 16 + i;
+      if (m >= M) continue;
+      const int n = m / Tg, tp = m - n * Tg;
+      float* d = dXs + (n * kGT + tp + j) * kGBX + 16 * ct + 4 * lq;
+      float4 o = *reinterpret_cast<const float4*>(d);
+      o.x += acc[uu][j][0];
+      o.y += acc[uu][j][1];
+      o.z += acc[uu][j][2];
+      o.w += acc[uu][j][3];
+      *reinterpret_cast<float4*>(d) = o;
+    }
+    __syncthreads();
+  }
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdArgs a) {
+  constexpr int NT = kGW * 64, NS = FIRST ? 4 : 2;
+  extern __shared__ float4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  float* Ds = lds;                          // [16 MT][68] the current GTU's gate-gradient rows, its weights
+  float* dXs = Ds + kGBStage;               // [NB T][36] the dX accumulator
+  float* red = dXs + kGNB * kGT * kGBX;     // [NS][8 waves][C] partial sums
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, i = l & 15, lq = l >> 4;
+  const int64_t bn0 = (int64_t)blockIdx.x * kGNB;
+  const int nn = (int)min<int64_t>(kGNB, a.BN - bn0);
+  const int t0 = min(4 * lq, kGT - 4);  // lq = 3: a copy of lq = 2's columns, never stored
+  const bool tv = lq < kGT / 4;
+  TF_DECL;
+  TF_MARK(0);
+
+  // fcmy weight B fragments: B[k][n = s] at k step r = W[t = 4 lq + r][s = 16 st + i]
+  float aw[2][4];
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = 4 * lq + r, sidx = 16 * st + i;
+      aw[st][r] = (t < kGT && sidx < kGS) ? a.fcmy_w[t * kGS + sidx] : 0.f;
+    }
+  float lg[2], rw[2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    lg[v] = a.ln_g[16 * v + i];
+    rw[v] = FIRST ? a.res_w[16 * v + i] : 0.f;
+  }
+  float acc_s[NS][2];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) acc_s[q][0] = acc_s[q][1] = 0.f;
+
+  // ---- A. per node ------------------------------------------------------------------------
+#pragma unroll
+  for (int jn = 0; jn < (kGNB + kGW - 1) / kGW; ++jn) {
+    const int n = w + kGW * jn;
+    if (n >= nn) continue;
+    const int64_t nb = bn0 + n;
+    float4 dy4[2], r4[2], tc4[2];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int64_t e0 = nb * kGCT + (16 * v + i) * kGT + t0;
+      dy4[v] = *reinterpret_cast<const float4*>(a.dout + e0);
+      r4[v] = *reinterpret_cast<const float4*>(a.r + e0);
+      tc4[v] = *reinterpret_cast<const float4*>(a.tco + e0);
+    }
+    const float4 mu4 = *reinterpret_cast<const float4*>(a.mu + nb * kGT + t0);
+    const float4 rs4 = *reinterpret_cast<const float4*>(a.rs + nb * kGT + t0);
+    float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (FIRST) x4 = *reinterpret_cast<const float4*>(a.x + nb * kGT + t0);
+    // the conv rows behind this lane's dG entries (s = 16 st + i, c = 16 ct + 4 lq + 0..3): float4
+    // runs of P and of Q
+    float4 pv[2][2], qv[2][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int sidx = 16 * st + i;
+      const int kq = sidx < kGT - 2 ? 0 : (sidx < 2 * kGT - 6 ? 1 : 2);
+      const int tp = sidx - (kq == 0 ? 0 : (kq == 1 ? kGT - 2 : 2 * kGT - 6)), Tg = kGT - 2 - 2 * kq;
+      const float* cb = kq == 0 ? a.conv[0] : (kq == 1 ? a.conv[1] : a.conv[2]);
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        pv[st][ct] = qv[st][ct] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (sidx < kGS) {
+          const float* row = cb + (nb * Tg + tp) * (2 * kGC) + 16 * ct + 4 * lq;
+          pv[st][ct] = *reinterpret_cast<const float4*>(row);
+          qv[st][ct] = *reinterpret_cast<const float4*>(row + kGC);
+        }
+      }
+    }
+    // LayerNorm over C backward (the channel sums: DPP row sums over i, two channels a lane)
+    float xh[2][4], dxh[2][4], s1[4], s2[4];
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        xh[v][r] = (g4at(r4[v], r) - g4at(mu4, r)) * g4at(rs4, r);
+        dxh[v][r] = g4at(dy4[v], r) * lg[v];
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[r] = gf_row16_sum(dxh[0][r] + dxh[1][r]) * (1.f / kGC);
+      s2[r] = gf_row16_sum(dxh[0][r] * xh[0][r] + dxh[1][r] * xh[1][r]) * (1.f / kGC);
+    }
+    float dtc[2][4], dr[2][4];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int64_t e0 = nb * kGCT + (16 * v + i) * kGT + t0;
+      float dtco[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float d = g4at(rs4, r) * (dxh[v][r] - s1[r] - xh[v][r] * s2[r]);
+        d = g4at(r4[v], r) > 0.f ? d : 0.f;             // relu(xres + tco)
+        dr[v][r] = d;
+        dtco[r] = g4at(tc4[v], r) > 0.f ? d : 0.f;      // tco = relu(...)
+        float dt = dtco[r];
+        if (a.drop_p > 0.f) dt *= drop_scale(a.seed, 1, (uint64_t)(e0 + r) + a.drop_off, a.drop_p);
+        dtc[v][r] = tv ? dt : 0.f;
+        if (tv) {
+          acc_s[0][v] += g4at(dy4[v], r) * xh[v][r];
+          acc_s[1][v] += g4at(dy4[v], r);
+          if (FIRST) {
+            acc_s[NS > 2 ? 2 : 0][v] += FIRST ? d * g4at(x4, r) : 0.f;
+            acc_s[NS > 3 ? 3 : 0][v] += FIRST ? d : 0.f;
+          }
+        }
+      }
+      if (tv) {
+        *reinterpret_cast<float4*>(a.dtc + e0) = make_float4(dtc[v][0], dtc[v][1], dtc[v][2], dtc[v][3]);
+        if (!FIRST) *reinterpret_cast<float4*>(a.dx + e0) = make_float4(dr[v][0], dr[v][1], dr[v][2], dr[v][3]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dXs[(n * kGT + t0 + r) * kGBX + 16 * v + i] = FIRST ? 0.f : dtco[r];
+      }
+    }
+    if (FIRST) {  // dx[n][t] = sum_c res_w[c] dr[c][t]
+      float dxs[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dxs[r] = gf_row16_sum(rw[0] * dr[0][r] + rw[1] * dr[1][r]);
+      if (tv && i == 0) *reinterpret_cast<float4*>(a.dx + nb * kGT + t0) = make_float4(dxs[0], dxs[1], dxs[2], dxs[3]);
+    }
+    // dG[c][s] = sum_t dtc[c][t] W[t][s] (k step r contracts t = 4 lq + r: the A fragment of
+    // lane (i, lq) is its own dtc[ct][r]); D[4 lq + r'][i] = dG[c = 16 ct + 4 lq + r'][s = 16 st + i]
+    floatx4 g[2][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        g[st][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g[st][ct] = gmf16(dtc[ct][r], aw[st][r], g[st][ct]);
+      }
+    // the gate derivatives: o = c (tanh side) and o = C + c (sigmoid side) of conv row (n, t')
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int sidx = 16 * st + i;
+      if (sidx >= kGS) continue;
+      const int kq = sidx < kGT - 2 ? 0 : (sidx < 2 * kGT - 6 ? 1 : 2);
+      const int tp = sidx - (kq == 0 ? 0 : (kq == 1 ? kGT - 2 : 2 * kGT - 6)), Tg = kGT - 2 - 2 * kq;
+      float* db = kq == 0 ? a.dconv[0] : (kq == 1 ? a.dconv[1] : a.dconv[2]);
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        float dp[4], dq[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float dg = g[st][ct][r];
+          const float th = gf_tanh(g4at(pv[st][ct], r)), sg = gf_sigmoid(g4at(qv[st][ct], r));
+          dp[r] = dg * (1.f - th * th) * sg;
+          dq[r] = dg * th * sg * (1.f - sg);
+        }
+        float* row = db + (nb * Tg + tp) * (2 * kGC) + 16 * ct + 4 * lq;
+        *reinterpret_cast<float4*>(row) = make_float4(dp[0], dp[1], dp[2], dp[3]);
+        *reinterpret_cast<float4*>(row + kGC) = make_float4(dq[0], dq[1], dq[2], dq[3]);
+      }
+    }
+  }
+  // the partial sums: over lq (xor 16, 32), then over the waves
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      float x = acc_s[q][v];
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      if (lq == 0) red[(q * kGW + w) * kGC + 16 * v + i] = x;
+    }
+  TF_MARK(1);
+  __syncthreads();  // (also: every wave's gate-gradient rows are visible to the workgroup)
+  TF_MARK(2);
+  if (tid < NS * kGC) {
+    const int q = tid / kGC, c = tid - q * kGC;
+    float x = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kGW; ++ww) x += red[(q * kGW + ww) * kGC + c];
+    float* out = q == 0 ? a.gpart : (q == 1 ? a.bpart : (q == 2 ? a.rpart : a.dpart));
+    out[(int64_t)blockIdx.x * kGC + c] = x;
+  }
+
+  // ---- B. the transposed convolutions -------------------------------------------------------
+  gb_tconv<0>(a, bn0, nn, Ds, dXs, w, i, lq);
+  TF_MARK(3);
+  gb_tconv<1>(a, bn0, nn, Ds, dXs, w, i, lq);
+  TF_MARK(4);
+  gb_tconv<2>(a, bn0, nn, Ds, dXs, w, i, lq);
+  TF_MARK(5);
+
+  // ---- C. gpre = (X > 0) ? dX : 0 -----------------------------------------------------------
+  {
+    constexpr int XV = (kGNB * kGCT / 4 + NT - 1) / NT;
+    const int ne4 = nn * kGCT / 4;
+    const float4* gx = reinterpret_cast<const float4*>(a.X + bn0 * kGCT);
+    float4* go = reinterpret_cast<float4*>(a.gpre + bn0 * kGCT);
+    float4 xv[XV];
+#pragma unroll
+    for (int u = 0; u < XV; ++u) xv[u] = gx[min(u * NT + tid, ne4 - 1)];
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int e4 = u * NT + tid;
+      if (e4 >= ne4) continue;
+      const int row = e4 / (kGC / 4), c = (e4 - row * (kGC / 4)) * 4;  // (n t, c)
+      const float4 d = *reinterpret_cast<const float4*>(dXs + row * kGBX + c);
+      go[e4] = make_float4(xv[u].x > 0.f ? d.x : 0.f, xv[u].y > 0.f ? d.y : 0.f, xv[u].z > 0.f ? d.z : 0.f,
+                           xv[u].w > 0.f ? d.w : 0.f);
+    }
+  }
+  TF_MARK(6);
+  TF_PRINT("gtu_fused_bwd", 7);
 }
 
 }  // namespace
@@ -325,6 +654,13 @@ int op_gtu_fused_fwd(const GtuFusedArgs& a, hipStream_t st) {
   if (!gtu_fused_fwd_ok(a.C, a.T) || a.BN <= 0 || a.BN * kGCT >= (1ll << 31)) {
     set_last_error("gtu_fused_fwd: unsupported shape");
     return DSTAGNN_E_SHAPE;
+  }
+  bool al = gf_al16(a.X) && gf_al16(a.x) && gf_al16(a.G) && gf_al16(a.tco) && gf_al16(a.r) && gf_al16(a.mu) &&
+            gf_al16(a.rs) && gf_al16(a.out) && gf_al16(a.fcmy_b);
+  for (int q = 0; q < 3; ++q) al = al && gf_al16(a.conv[q]) && gf_al16(a.wt[q]) && gf_al16(a.bias[q]);
+  if (!al) {
+    set_last_error("gtu_fused_fwd: operands must be 16-B aligned");
+    return DSTAGNN_E_ARG;
   }
   using Kern = void (*)(GtuFusedArgs);
   const Kern k = a.first ? gtu_fwd_fused_kernel<true> : gtu_fwd_fused_kernel<false>;
@@ -342,6 +678,48 @@ int op_gtu_fused_fwd(const GtuFusedArgs& a, hipStream_t st) {
   // the three convolutions' algorithmic FLOP (the GEMM family's accounting)
   const double flops = 2.0 * a.BN * (2.0 * kGC) * kGC * ((kGT - 2) * 3 + (kGT - 4) * 5 + (kGT - 6) * 7);
   const double bytes = 4.0 * a.BN * (kGCT * 6.0 + 2 * kGC * 24.0 + kGC * kGS);
+  void* rec = gemm_prof_begin(flops, bytes, st);
+  hipLaunchKernelGGL(k, dim3((unsigned)cdiv64(a.BN, kGNB)), dim3(kGW * 64), lds, st, a);
+  DS_CHECK_LAUNCH();
+  gemm_prof_end(rec, st);
+  return 0;
+}
+
+bool gtu_fused_bwd_ok(int C, int T) {
+  static const bool on = !getenv("DSTAGNN_GTU_FUSED_BWD") || atoi(getenv("DSTAGNN_GTU_FUSED_BWD")) != 0;  // default on
+  return on && C == kGC && T == kGT;
+}
+int64_t gtu_fused_bwd_wgs(int64_t BN) { return cdiv64(BN, kGNB); }
+
+int op_gtu_fused_bwd(const GtuFusedBwdArgs& a, hipStream_t st) {
+  if (!gtu_fused_bwd_ok(a.C, a.T) || a.BN <= 0 || a.BN * kGCT >= (1ll << 31) || !a.gpart || !a.bpart ||
+      (a.first && (!a.rpart || !a.dpart))) {
+    set_last_error("gtu_fused_bwd: unsupported shape or missing partial-sum rows");
+    return DSTAGNN_E_SHAPE;
+  }
+  bool al = gf_al16(a.dout) && gf_al16(a.r) && gf_al16(a.tco) && gf_al16(a.mu) && gf_al16(a.rs) && gf_al16(a.x) &&
+            gf_al16(a.X) && gf_al16(a.dtc) && gf_al16(a.dx) && gf_al16(a.gpre);
+  for (int q = 0; q < 3; ++q) al = al && gf_al16(a.dconv[q]) && gf_al16(a.wf[q]);
+  if (!al) {
+    set_last_error("gtu_fused_bwd: operands must be 16-B aligned");
+    return DSTAGNN_E_ARG;
+  }
+  using Kern = void (*)(GtuFusedBwdArgs);
+  const Kern k = a.first ? gtu_bwd_fused_kernel<true> : gtu_bwd_fused_kernel<false>;
+  const size_t lds = gtu_fused_bwd_lds();
+  {
+    static std::mutex mu;
+    static std::set<Kern> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!done.count(k)) {
+      const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) { set_last_error(std::string("gtu_fused_bwd: ") + hipGetErrorString(e)); return (int)e; }
+      done.insert(k);
+    }
+  }
+  // the transposed convolutions' algorithmic FLOP (the GEMM family's accounting)
+  const double flops = 2.0 * a.BN * (2.0 * kGC) * kGC * ((kGT - 2) * 3 + (kGT - 4) * 5 + (kGT - 6) * 7);
+  const double bytes = 4.0 * a.BN * (kGCT * 7.0 + 2 * kGC * 24.0 * 3);
   void* rec = gemm_prof_begin(flops, bytes, st);
   hipLaunchKernelGGL(k, dim3((unsigned)cdiv64(a.BN, kGNB)), dim3(kGW * 64), lds, st, a);
   DS_CHECK_LAUNCH();

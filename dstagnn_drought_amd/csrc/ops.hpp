@@ -321,6 +321,22 @@ struct GtuFusedArgs {
 };
 bool gtu_fused_fwd_ok(int C, int T);
 int op_gtu_fused_fwd(const GtuFusedArgs& a, hipStream_t st);
+struct GtuFusedBwdArgs {
+  int64_t BN = 0; int C = 0, T = 0; int first = 0;
+  const float *dout = nullptr, *r = nullptr, *tco = nullptr, *mu = nullptr, *rs = nullptr;
+  const float* x = nullptr;        // first block: the block input (BN, T)
+  const float* X = nullptr;        // (BN, T, C) Chebyshev output (the ReLU mask of gpre)
+  const float* conv[3] = {};       // (BN Tg, 2C) saved by the forward
+  const float* wf[3] = {};         // GTU weights re-laid (j, c, o) (param_prep kind 7)
+  const float *fcmy_w = nullptr, *ln_g = nullptr, *res_w = nullptr;
+  float drop_p = 0.f; uint64_t seed = 0; uint64_t drop_off = 0;
+  float *dtc = nullptr, *dx = nullptr, *gpre = nullptr;
+  float* dconv[3] = {};            // (BN Tg, 2C) compact gate gradients (the weight gradients' operand)
+  float *gpart = nullptr, *bpart = nullptr, *rpart = nullptr, *dpart = nullptr;  // [workgroup][C]
+};
+bool gtu_fused_bwd_ok(int C, int T);
+int64_t gtu_fused_bwd_wgs(int64_t BN);
+int op_gtu_fused_bwd(const GtuFusedBwdArgs& a, hipStream_t st);
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st);
 int op_tat_bwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* att, const float* dctx,

@@ -23,6 +23,8 @@ a subprocess (the library reads its switches once per process):
                        in-kernel (ticket tree over grid-stride workgroups) instead of colsum2d
   DSTAGNN_GTU_FUSED=0  the GTU stage forward as the grouped conv GEMM + gtu_tail_fwd_ct instead of
                        gtu_fused.hip's one kernel (convolutions, gates, fcmy, residual, LN)
+  DSTAGNN_GTU_FUSED_BWD=0  the GTU stage backward as gtu_tail_bwd_ct + gtu_tconv (zero-padded gate
+                       gradient rows) instead of gtu_fused.hip's one kernel
   DSTAGNN_DWP_MAIN=1   the pre_conv weight gradient on the main stream instead of the side stream
   DSTAGNN_DEBUG_STREAMS=1  the fork invariant asserted (block.hip Bwd::sq): no side-stream work
                        issued while a fork's signal is still pending
@@ -69,7 +71,7 @@ print("KNOB_OK")
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems08", 4),
                                        ("DSTAGNN_TAT_FUSED=0", "pems08", 4),
                                        ("DSTAGNN_TAIL_FOLD=1", "pems08", 4),
-                                       ("DSTAGNN_GTU_FUSED=0", "pems08", 4),
+                                       ("DSTAGNN_GTU_FUSED=0", "pems08", 4), ("DSTAGNN_GTU_FUSED_BWD=0", "pems08", 4),
                                        ("DSTAGNN_DWP_MAIN=1", "pems08", 4),
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems07+flash", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
