@@ -1144,10 +1144,12 @@ struct Bwd {
     return op_colsum_multi(ins, outs, n, A, O, I, 1, 0.f, q == st ? w.part : w.part_side, kPart, q);
   }
   int gemm(const Gemm& g) { return run_gemm(g, w.gemm_ws, kGemmWs, st); }
-  // side-stream weight gradients: their own split-K target (DSTAGNN_SIDE_SPLITK, A/B knob; 0 = the
-  // global one) — fewer K slices mean a cheaper fold and fewer CUs taken from the main chain
+  // side-stream weight gradients: their own split-K target (DSTAGNN_SIDE_SPLITK; 0 = the global
+  // one) — fewer K slices mean a cheaper fold and fewer CUs taken from the main chain.  192: with
+  // the GTU stage fused the side stream is the step's last to finish, and 192 beat the global
+  // 448 by ~8 us/step (256: ~5) in same-box A/Bs (profiles/r05_knob_sweep.txt)
   static int side_splitk() {
-    static const int t = getenv("DSTAGNN_SIDE_SPLITK") ? atoi(getenv("DSTAGNN_SIDE_SPLITK")) : 0;
+    static const int t = getenv("DSTAGNN_SIDE_SPLITK") ? atoi(getenv("DSTAGNN_SIDE_SPLITK")) : 192;
     return t;
   }
   int sgemm(const Gemm& g0) {
@@ -1165,14 +1167,18 @@ struct Bwd {
     for (int q = 0; q < 3; ++q) { g.conv[q] = s.conv[q]; g.wf[q] = s.Wgf[q]; g.dconv[q] = w.dconv[q]; }
     g.fcmy_w = p.fcmy_w; g.ln_g = p.ln_g; g.res_w = p.res_w;
     if (d.train && d.drop_p > 0.f) { g.drop_p = d.drop_p; g.seed = d.seed; g.drop_off = drop_off(d, 1); }
-    g.dtc = w.dtc; g.dx = dx; g.gpre = w.gpre;
+    g.dx = dx; g.gpre = w.gpre;
     const int64_t nwg = gtu_fused_bwd_wgs(m.BN);  // one partial-sum row per workgroup
     g.gpart = w.gcon_t; g.bpart = w.gcon_t + nwg * m.C;
     if (m.first) { g.rpart = w.bcon_t; g.dpart = w.bcon_t + nwg * m.C; }
+    // the fcmy weight / bias gradients as partial rows too (dtc stays on chip)
+    g.fwpart = w.gcon_t + 2 * nwg * m.C; g.fbpart = g.fwpart + nwg * m.T * m.S;
     DS_TRY(op_gtu_fused_bwd(g, st));
     DS_TRY(fork());
     DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + nwg * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
                     {w.bcon_t + nwg * m.C, m.first ? gd.res_b : nullptr}}, nwg, m.C, 1));
+    DS_TRY(colsums({{g.fwpart, gd.fcmy_w}}, nwg, (int)(m.T * m.S), 1));
+    DS_TRY(colsums({{g.fbpart, gd.fcmy_b}}, nwg, m.T, 1));
     return stage_tail_wgrads(true);
   }
 
@@ -1245,7 +1251,9 @@ struct Bwd {
     // the bias gradients ride on their weight-gradient GEMMs as a column-sum column
     // (Gemm::ones_out: sum over the reduction of the gradient operand); a bias whose weight
     // gradient is not requested gets its own column sum
-    if (gd.fcmy_w) {
+    if (compact) {
+      // (the fused backward's partial rows: summed by the caller)
+    } else if (gd.fcmy_w) {
       Gemm g;  // dW[t,s] = sum_r dtc[r,t] G[r,s]; db[t] = sum_r dtc[r,t]
       g.M = m.T; g.N = (int)m.S; g.K = (int)(m.BN * m.C);
       g.A = w.dtc; g.am = idx1(1); g.ak = idx1(m.T);

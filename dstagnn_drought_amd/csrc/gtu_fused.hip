@@ -346,8 +346,12 @@ constexpr int gb_stage(int q) { return (gb_rows(q) + (3 + 2 * q) * kGC) * kGBS; 
 constexpr int gb_cmax(int a, int b) { return a > b ? a : b; }
 constexpr int kGBStage = gb_cmax(gb_stage(0), gb_cmax(gb_stage(1), gb_stage(2)));
 
+constexpr int kGBTT = kGC * 13;                     // a wave's dtc transpose buffer [c][13]
+constexpr int kGBF = kGT * (kGS + 1);                // fcmy weight + bias gradient entries (t, s <= S)
+static_assert(kGW * kGBTT <= kGBStage, "dtc transpose buffers live in the staging region");
+
 size_t gtu_fused_bwd_lds() {
-  return sizeof(float) * ((size_t)kGBStage + (size_t)kGNB * kGT * kGBX + 4 * kGW * kGC);
+  return sizeof(float) * ((size_t)kGBStage + (size_t)kGNB * kGT * kGBX + 4 * kGW * kGC + (size_t)kGW * kGBF);
 }
 
 // step B for GTU KQ (kernel width KS)
@@ -441,6 +445,8 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
   float* Ds = lds;                          // [16 MT][68] the current GTU's gate-gradient rows, its weights
   float* dXs = Ds + kGBStage;               // [NB T][36] the dX accumulator
   float* red = dXs + kGNB * kGT * kGBX;     // [NS][8 waves][C] partial sums
+  float* redf = red + 4 * kGW * kGC;        // [8 waves][T][S + 1] fcmy gradient partial sums
+  const bool fw = a.fwpart != nullptr;
   const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, i = l & 15, lq = l >> 4;
   const int64_t bn0 = (int64_t)blockIdx.x * kGNB;
   const int nn = (int)min<int64_t>(kGNB, a.BN - bn0);
@@ -467,6 +473,8 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
   float acc_s[NS][2];
 #pragma unroll
   for (int q = 0; q < NS; ++q) acc_s[q][0] = acc_s[q][1] = 0.f;
+  floatx4 accf[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};  // dW_fcmy[t][s]
+  float* tt = Ds + w * kGBTT;  // this wave's dtc transpose buffer (the staging region is free in A)
 
   // ---- A. per node ------------------------------------------------------------------------
 #pragma unroll
@@ -543,7 +551,10 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
         }
       }
       if (tv) {
-        *reinterpret_cast<float4*>(a.dtc + e0) = make_float4(dtc[v][0], dtc[v][1], dtc[v][2], dtc[v][3]);
+        if (!fw) *reinterpret_cast<float4*>(a.dtc + e0) = make_float4(dtc[v][0], dtc[v][1], dtc[v][2], dtc[v][3]);
+        else
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tt[(16 * v + i) * 13 + t0 + r] = dtc[v][r];
         if (!FIRST) *reinterpret_cast<float4*>(a.dx + e0) = make_float4(dr[v][0], dr[v][1], dr[v][2], dr[v][3]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) dXs[(n * kGT + t0 + r) * kGBX + 16 * v + i] = FIRST ? 0.f : dtco[r];
@@ -566,10 +577,16 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
 #pragma unroll
         for (int r = 0; r < 4; ++r) g[st][ct] = gmf16(dtc[ct][r], aw[st][r], g[st][ct]);
       }
-    // the gate derivatives: o = c (tanh side) and o = C + c (sigmoid side) of conv row (n, t')
+    // the gate derivatives: o = c (tanh side) and o = C + c (sigmoid side) of conv row (n, t');
+    // the gates themselves are the fcmy weight gradient's B fragments (below): G is not re-read
+    float gbv[2][2][4];  // [st][ct][r]: G[c = 16 ct + 4 lq + r][s = 16 st + i]; s = S: ones (bias)
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int sidx = 16 * st + i;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gbv[st][ct][r] = sidx == kGS ? 1.f : 0.f;
       if (sidx >= kGS) continue;
       const int kq = sidx < kGT - 2 ? 0 : (sidx < 2 * kGT - 6 ? 1 : 2);
       const int tp = sidx - (kq == 0 ? 0 : (kq == 1 ? kGT - 2 : 2 * kGT - 6)), Tg = kGT - 2 - 2 * kq;
@@ -583,11 +600,27 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
           const float th = gf_tanh(g4at(pv[st][ct], r)), sg = gf_sigmoid(g4at(qv[st][ct], r));
           dp[r] = dg * (1.f - th * th) * sg;
           dq[r] = dg * th * sg * (1.f - sg);
+          gbv[st][ct][r] = th * sg;
         }
         float* row = db + (nb * Tg + tp) * (2 * kGC) + 16 * ct + 4 * lq;
         *reinterpret_cast<float4*>(row) = make_float4(dp[0], dp[1], dp[2], dp[3]);
         *reinterpret_cast<float4*>(row + kGC) = make_float4(dq[0], dq[1], dq[2], dq[3]);
       }
+    }
+    // dW_fcmy[t][s] += sum_c dtc[c][t] G[c][s]: k step kk = 4 ct + r contracts c = 16 ct + 4 lq + r
+    // (the channels whose gates the lane holds); A[m = t][k = c] from the wave's transpose buffer
+    // (its own LDS ops run in order; the fences keep the compiler from moving them)
+    if (fw) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float av = i < kGT ? tt[(16 * ct + 4 * lq + r) * 13 + i] : 0.f;
+#pragma unroll
+          for (int st = 0; st < 2; ++st) accf[st] = gmf16(av, gbv[st][ct][r], accf[st]);
+        }
+      asm volatile("" ::: "memory");
     }
   }
   // the partial sums: over lq (xor 16, 32), then over the waves
@@ -600,6 +633,15 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
       x += __shfl_xor(x, 32, 64);
       if (lq == 0) red[(q * kGW + w) * kGC + 16 * v + i] = x;
     }
+  if (fw) {  // D[4 lq + r][i] = dW_fcmy[t = 4 lq + r][s = 16 st + i]
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 4 * lq + r, sidx = 16 * st + i;
+        if (t < kGT && sidx <= kGS) redf[w * kGBF + t * (kGS + 1) + sidx] = accf[st][r];
+      }
+  }
   TF_MARK(1);
   __syncthreads();  // (also: every wave's gate-gradient rows are visible to the workgroup)
   TF_MARK(2);
@@ -610,6 +652,14 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
     for (int ww = 0; ww < kGW; ++ww) x += red[(q * kGW + ww) * kGC + c];
     float* out = q == 0 ? a.gpart : (q == 1 ? a.bpart : (q == 2 ? a.rpart : a.dpart));
     out[(int64_t)blockIdx.x * kGC + c] = x;
+  }
+  if (fw && tid < kGBF) {
+    const int t = tid / (kGS + 1), sidx = tid - t * (kGS + 1);
+    float x = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kGW; ++ww) x += redf[ww * kGBF + tid];
+    if (sidx < kGS) a.fwpart[(int64_t)blockIdx.x * kGT * kGS + t * kGS + sidx] = x;
+    else a.fbpart[(int64_t)blockIdx.x * kGT + t] = x;
   }
 
   // ---- B. the transposed convolutions -------------------------------------------------------
@@ -699,6 +749,10 @@ int op_gtu_fused_bwd(const GtuFusedBwdArgs& a, hipStream_t st) {
   }
   bool al = gf_al16(a.dout) && gf_al16(a.r) && gf_al16(a.tco) && gf_al16(a.mu) && gf_al16(a.rs) && gf_al16(a.x) &&
             gf_al16(a.X) && gf_al16(a.dtc) && gf_al16(a.dx) && gf_al16(a.gpre);
+  if (a.fwpart ? !a.fbpart : !a.dtc) {
+    set_last_error("gtu_fused_bwd: fcmy weight partial rows need the bias rows; without them, dtc");
+    return DSTAGNN_E_ARG;
+  }
   for (int q = 0; q < 3; ++q) al = al && gf_al16(a.dconv[q]) && gf_al16(a.wf[q]);
   if (!al) {
     set_last_error("gtu_fused_bwd: operands must be 16-B aligned");

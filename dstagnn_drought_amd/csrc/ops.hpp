@@ -333,6 +333,9 @@ struct GtuFusedBwdArgs {
   float *dtc = nullptr, *dx = nullptr, *gpre = nullptr;
   float* dconv[3] = {};            // (BN Tg, 2C) compact gate gradients (the weight gradients' operand)
   float *gpart = nullptr, *bpart = nullptr, *rpart = nullptr, *dpart = nullptr;  // [workgroup][C]
+  // fcmy weight / bias gradient partial rows [workgroup][T S] / [workgroup][T] (dtc never leaves
+  // the chip); null: dtc written instead
+  float *fwpart = nullptr, *fbpart = nullptr;
 };
 bool gtu_fused_bwd_ok(int C, int T);
 int64_t gtu_fused_bwd_wgs(int64_t BN);
