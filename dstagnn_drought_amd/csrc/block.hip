@@ -1168,17 +1168,13 @@ struct Bwd {
     g.fcmy_w = p.fcmy_w; g.ln_g = p.ln_g; g.res_w = p.res_w;
     if (d.train && d.drop_p > 0.f) { g.drop_p = d.drop_p; g.seed = d.seed; g.drop_off = drop_off(d, 1); }
     g.dx = dx; g.gpre = w.gpre;
-    const int64_t nwg = gtu_fused_bwd_wgs(m.BN);  // one partial-sum row per workgroup
-    g.gpart = w.gcon_t; g.bpart = w.gcon_t + nwg * m.C;
-    if (m.first) { g.rpart = w.bcon_t; g.dpart = w.bcon_t + nwg * m.C; }
-    // the fcmy weight / bias gradients as partial rows too (dtc stays on chip)
-    g.fwpart = w.gcon_t + 2 * nwg * m.C; g.fbpart = g.fwpart + nwg * m.T * m.S;
+    // the LN / residual_conv / fcmy parameter gradients summed in-kernel (ticket tree over
+    // per-workgroup rows in gcon_t): no column sums on the side stream
+    g.gout = gd.ln_g; g.bout = gd.ln_b; g.fwout = gd.fcmy_w; g.fbout = gd.fcmy_b;
+    if (m.first) { g.rwout = gd.res_w; g.rbout = gd.res_b; }
+    g.part = w.gcon_t;  // (BN CT floats >= gtu_fused_bwd_part_floats)
     DS_TRY(op_gtu_fused_bwd(g, st));
     DS_TRY(fork());
-    DS_TRY(colsums({{w.gcon_t, gd.ln_g}, {w.gcon_t + nwg * m.C, gd.ln_b}, {w.bcon_t, m.first ? gd.res_w : nullptr},
-                    {w.bcon_t + nwg * m.C, m.first ? gd.res_b : nullptr}}, nwg, m.C, 1));
-    DS_TRY(colsums({{g.fwpart, gd.fcmy_w}}, nwg, (int)(m.T * m.S), 1));
-    DS_TRY(colsums({{g.fbpart, gd.fcmy_b}}, nwg, m.T, 1));
     return stage_tail_wgrads(true);
   }
 

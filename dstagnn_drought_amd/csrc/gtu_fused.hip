@@ -310,6 +310,13 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_fwd_fused_kernel(GtuFusedArgs
   TF_PRINT("gtu_fused", 8);
 }
 
+__device__ __forceinline__ float gf_ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gf_st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 bool gf_al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 size_t gtu_fused_lds() {
@@ -349,6 +356,8 @@ constexpr int kGBStage = gb_cmax(gb_stage(0), gb_cmax(gb_stage(1), gb_stage(2)))
 constexpr int kGBTT = kGC * 13;                     // a wave's dtc transpose buffer [c][13]
 constexpr int kGBF = kGT * (kGS + 1);                // fcmy weight + bias gradient entries (t, s <= S)
 static_assert(kGW * kGBTT <= kGBStage, "dtc transpose buffers live in the staging region");
+constexpr int kGBP = 4 * kGC + kGBF;                 // a workgroup's partial row: gamma, beta, res w, res b, fcmy
+constexpr int kGBG1 = 16;                            // workgroups per level-1 group of the ticket tree
 
 size_t gtu_fused_bwd_lds() {
   return sizeof(float) * ((size_t)kGBStage + (size_t)kGNB * kGT * kGBX + 4 * kGW * kGC + (size_t)kGW * kGBF);
@@ -446,7 +455,7 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
   float* dXs = Ds + kGBStage;               // [NB T][36] the dX accumulator
   float* red = dXs + kGNB * kGT * kGBX;     // [NS][8 waves][C] partial sums
   float* redf = red + 4 * kGW * kGC;        // [8 waves][T][S + 1] fcmy gradient partial sums
-  const bool fw = a.fwpart != nullptr;
+  constexpr bool fw = true;
   const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, i = l & 15, lq = l >> 4;
   const int64_t bn0 = (int64_t)blockIdx.x * kGNB;
   const int nn = (int)min<int64_t>(kGNB, a.BN - bn0);
@@ -551,10 +560,8 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
         }
       }
       if (tv) {
-        if (!fw) *reinterpret_cast<float4*>(a.dtc + e0) = make_float4(dtc[v][0], dtc[v][1], dtc[v][2], dtc[v][3]);
-        else
 #pragma unroll
-          for (int r = 0; r < 4; ++r) tt[(16 * v + i) * 13 + t0 + r] = dtc[v][r];
+        for (int r = 0; r < 4; ++r) tt[(16 * v + i) * 13 + t0 + r] = dtc[v][r];
         if (!FIRST) *reinterpret_cast<float4*>(a.dx + e0) = make_float4(dr[v][0], dr[v][1], dr[v][2], dr[v][3]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) dXs[(n * kGT + t0 + r) * kGBX + 16 * v + i] = FIRST ? 0.f : dtco[r];
@@ -650,16 +657,13 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
     float x = 0.f;
 #pragma unroll
     for (int ww = 0; ww < kGW; ++ww) x += red[(q * kGW + ww) * kGC + c];
-    float* out = q == 0 ? a.gpart : (q == 1 ? a.bpart : (q == 2 ? a.rpart : a.dpart));
-    out[(int64_t)blockIdx.x * kGC + c] = x;
+    gf_st_agent(a.part + (int64_t)blockIdx.x * kGBP + q * kGC + c, x);
   }
-  if (fw && tid < kGBF) {
-    const int t = tid / (kGS + 1), sidx = tid - t * (kGS + 1);
+  if (tid < kGBF) {
     float x = 0.f;
 #pragma unroll
     for (int ww = 0; ww < kGW; ++ww) x += redf[ww * kGBF + tid];
-    if (sidx < kGS) a.fwpart[(int64_t)blockIdx.x * kGT * kGS + t * kGS + sidx] = x;
-    else a.fbpart[(int64_t)blockIdx.x * kGT + t] = x;
+    gf_st_agent(a.part + (int64_t)blockIdx.x * kGBP + 4 * kGC + tid, x);
   }
 
   // ---- B. the transposed convolutions -------------------------------------------------------
@@ -691,6 +695,73 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
   }
   TF_MARK(6);
   TF_PRINT("gtu_fused_bwd", 7);
+
+  // ---- D. the parameter gradients: the last of each group of 16 workgroups sums the group's
+  //         partial rows (agent-scope stores above, agent acquire here) into a level-2 row, the
+  //         last group sums the level-2 rows in order: deterministic, no column-sum launches ---
+  int* flag = reinterpret_cast<int*>(red);  // (red is free after step A)
+  const int nwg = (int)gridDim.x, ng = (nwg + kGBG1 - 1) / kGBG1, g1 = (int)blockIdx.x / kGBG1;
+  const int gsz = min(kGBG1, nwg - g1 * kGBG1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int lg = atomicAdd(a.cnt + g1, 1) == gsz - 1;
+    if (lg) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.cnt + g1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    flag[0] = lg;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  float* l2 = a.part + (int64_t)nwg * kGBP;  // level-2 rows [ng][P]
+  for (int e = tid; e < kGBP; e += NT) {
+    const float* src = a.part + (int64_t)g1 * kGBG1 * kGBP + e;
+    float u[kGBG1];
+#pragma unroll
+    for (int k = 0; k < kGBG1; ++k) u[k] = k < gsz ? gf_ld_agent(src + (int64_t)k * kGBP) : 0.f;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < kGBG1; ++k) v += u[k];
+    gf_st_agent(l2 + (int64_t)g1 * kGBP + e, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int last2 = atomicAdd(a.cnt + ng, 1) == ng - 1;
+    if (last2) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.cnt + ng, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    flag[1] = last2;
+  }
+  __syncthreads();
+  if (!flag[1]) return;
+  for (int e = tid; e < kGBP; e += NT) {
+    float* out;
+    int o;
+    if (e < 4 * kGC) {
+      const int q = e / kGC;
+      out = q == 0 ? a.gout : (q == 1 ? a.bout : (q == 2 ? a.rwout : a.rbout));
+      o = e - q * kGC;
+    } else {
+      const int f = e - 4 * kGC, t = f / (kGS + 1), sidx = f - t * (kGS + 1);
+      out = sidx < kGS ? a.fwout : a.fbout;
+      o = sidx < kGS ? t * kGS + sidx : t;
+    }
+    if (!out) continue;
+    float v = 0.f;
+    for (int k0 = 0; k0 < ng; k0 += kGBG1) {
+      float u[kGBG1];
+#pragma unroll
+      for (int k = 0; k < kGBG1; ++k) u[k] = k0 + k < ng ? gf_ld_agent(l2 + (int64_t)(k0 + k) * kGBP + e) : 0.f;
+#pragma unroll
+      for (int k = 0; k < kGBG1; ++k) v += u[k];
+    }
+    out[o] = v;
+  }
 }
 
 }  // namespace
@@ -739,20 +810,18 @@ bool gtu_fused_bwd_ok(int C, int T) {
   static const bool on = !getenv("DSTAGNN_GTU_FUSED_BWD") || atoi(getenv("DSTAGNN_GTU_FUSED_BWD")) != 0;  // default on
   return on && C == kGC && T == kGT;
 }
-int64_t gtu_fused_bwd_wgs(int64_t BN) { return cdiv64(BN, kGNB); }
+int64_t gtu_fused_bwd_part_floats(int64_t BN) {
+  const int64_t nwg = cdiv64(BN, kGNB);
+  return (nwg + cdiv64(nwg, kGBG1)) * kGBP;
+}
 
 int op_gtu_fused_bwd(const GtuFusedBwdArgs& a, hipStream_t st) {
-  if (!gtu_fused_bwd_ok(a.C, a.T) || a.BN <= 0 || a.BN * kGCT >= (1ll << 31) || !a.gpart || !a.bpart ||
-      (a.first && (!a.rpart || !a.dpart))) {
-    set_last_error("gtu_fused_bwd: unsupported shape or missing partial-sum rows");
+  if (!gtu_fused_bwd_ok(a.C, a.T) || a.BN <= 0 || a.BN * kGCT >= (1ll << 31) || !a.part) {
+    set_last_error("gtu_fused_bwd: unsupported shape or no partial-row workspace");
     return DSTAGNN_E_SHAPE;
   }
   bool al = gf_al16(a.dout) && gf_al16(a.r) && gf_al16(a.tco) && gf_al16(a.mu) && gf_al16(a.rs) && gf_al16(a.x) &&
-            gf_al16(a.X) && gf_al16(a.dtc) && gf_al16(a.dx) && gf_al16(a.gpre);
-  if (a.fwpart ? !a.fbpart : !a.dtc) {
-    set_last_error("gtu_fused_bwd: fcmy weight partial rows need the bias rows; without them, dtc");
-    return DSTAGNN_E_ARG;
-  }
+            gf_al16(a.X) && gf_al16(a.dx) && gf_al16(a.gpre);
   for (int q = 0; q < 3; ++q) al = al && gf_al16(a.dconv[q]) && gf_al16(a.wf[q]);
   if (!al) {
     set_last_error("gtu_fused_bwd: operands must be 16-B aligned");
@@ -774,8 +843,15 @@ int op_gtu_fused_bwd(const GtuFusedBwdArgs& a, hipStream_t st) {
   // the transposed convolutions' algorithmic FLOP (the GEMM family's accounting)
   const double flops = 2.0 * a.BN * (2.0 * kGC) * kGC * ((kGT - 2) * 3 + (kGT - 4) * 5 + (kGT - 6) * 7);
   const double bytes = 4.0 * a.BN * (kGCT * 7.0 + 2 * kGC * 24.0 * 3);
+  GtuFusedBwdArgs b = a;
+  const int64_t nwg = cdiv64(a.BN, kGNB);
+  b.cnt = stream_counters(st, (int)(cdiv64(nwg, kGBG1) + 1));  // [ng] level-1 tickets, one level-2 ticket
+  if (!b.cnt) {
+    set_last_error("gtu_fused_bwd: no ticket counters");
+    return DSTAGNN_E_ARG;
+  }
   void* rec = gemm_prof_begin(flops, bytes, st);
-  hipLaunchKernelGGL(k, dim3((unsigned)cdiv64(a.BN, kGNB)), dim3(kGW * 64), lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(kGW * 64), lds, st, b);
   DS_CHECK_LAUNCH();
   gemm_prof_end(rec, st);
   return 0;

@@ -330,15 +330,17 @@ struct GtuFusedBwdArgs {
   const float* wf[3] = {};         // GTU weights re-laid (j, c, o) (param_prep kind 7)
   const float *fcmy_w = nullptr, *ln_g = nullptr, *res_w = nullptr;
   float drop_p = 0.f; uint64_t seed = 0; uint64_t drop_off = 0;
-  float *dtc = nullptr, *dx = nullptr, *gpre = nullptr;
+  float *dx = nullptr, *gpre = nullptr;
   float* dconv[3] = {};            // (BN Tg, 2C) compact gate gradients (the weight gradients' operand)
-  float *gpart = nullptr, *bpart = nullptr, *rpart = nullptr, *dpart = nullptr;  // [workgroup][C]
-  // fcmy weight / bias gradient partial rows [workgroup][T S] / [workgroup][T] (dtc never leaves
-  // the chip); null: dtc written instead
-  float *fwpart = nullptr, *fbpart = nullptr;
+  // the parameter gradients reduced in-kernel (two-level ticket tree over per-workgroup rows of
+  // gtu_fused_bwd_row() floats in part, level-2 rows after them; null outputs skipped):
+  // LayerNorm gamma / beta, residual_conv weight / bias (first block), fcmy weight / bias
+  float *gout = nullptr, *bout = nullptr, *rwout = nullptr, *rbout = nullptr, *fwout = nullptr, *fbout = nullptr;
+  float* part = nullptr;           // gtu_fused_bwd_part_floats(BN) floats
+  int* cnt = nullptr;              // (set by op_gtu_fused_bwd: the stream's ticket counters)
 };
 bool gtu_fused_bwd_ok(int C, int T);
-int64_t gtu_fused_bwd_wgs(int64_t BN);
+int64_t gtu_fused_bwd_part_floats(int64_t BN);
 int op_gtu_fused_bwd(const GtuFusedBwdArgs& a, hipStream_t st);
 int op_tat_fwd(int B, int F, int T, int h, int dk, int dv, const float* qkv, const float* res, int res_mode,
                float* re_at, float* att, float* ctx, hipStream_t st);
