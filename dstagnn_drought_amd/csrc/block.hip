@@ -1173,6 +1173,8 @@ struct Bwd {
     g.gout = gd.ln_g; g.bout = gd.ln_b; g.fwout = gd.fcmy_w; g.fbout = gd.fcmy_b;
     if (m.first) { g.rwout = gd.res_w; g.rbout = gd.res_b; }
     g.part = w.gcon_t;  // (BN CT floats >= gtu_fused_bwd_part_floats)
+    // (a flag written by the kernel's last workgroup instead of this fork measured 20 us/step
+    // SLOWER: the side's GTU weight-gradient GEMM then starts under the SDDMM and both stretch)
     DS_TRY(op_gtu_fused_bwd(g, st));
     DS_TRY(fork());
     return stage_tail_wgrads(true);
@@ -1529,7 +1531,6 @@ struct Bwd {
     const int64_t N = m.N;
     const bool side_any = tatln_side() || (gd.tat_fc && fc_side()) || wqkv_side();
     if (!m.first) DS_TRY(wait_side(dx_ready));  // dx += the Chebyshev-path gradient (side stream) first
-    if (side_any) DS_TRY(fork_k());  // (its flag rides on the fused kernel)
     TatFusedBwdArgs t;
     t.dO = w.dO; t.u = s.u_tat; t.mu = s.mu_tat; t.rs = s.rs_tat; t.g = p.tat_ln_g;
     // gamma / beta: the kernel's two-level ticket tree sums its partial rows (level-2 rows after
@@ -1557,7 +1558,9 @@ struct Bwd {
     t.scale = 1.f / sqrtf((float)m.dk);
     DS_TRY(op_tat_fused_bwd(t, st));
     if (side_any) {
-      DS_TRY(fork_k_done());
+      // (A/B knobs only) the side work reads this kernel's outputs (dU, dqkv, the LN partial
+      // rows): a fork AFTER it — a flag carried at a kernel's start would let them race
+      DS_TRY(fork());
       if (tatln_side()) DS_TRY(tat_ln_colsums(false));
       if (gd.tat_fc && fc_side()) DS_TRY(sgemm(fc_grad_gemm()));
       if (wqkv_side()) DS_TRY(tat_wqkv_grad(true));
