@@ -485,27 +485,25 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
   floatx4 accf[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};  // dW_fcmy[t][s]
   float* tt = Ds + w * kGBTT;  // this wave's dtc transpose buffer (the staging region is free in A)
 
-  // ---- A. per node ------------------------------------------------------------------------
-#pragma unroll
-  for (int jn = 0; jn < (kGNB + kGW - 1) / kGW; ++jn) {
-    const int n = w + kGW * jn;
-    if (n >= nn) continue;
+  // ---- A. per node (the next node's operands loaded while this one is processed) -----------
+  struct NodeIn {
+    float4 dy[2], r[2], tc[2], mu, rs, x;
+    float4 p[2][2], q[2][2];  // the conv rows behind the lane's dG entries (s = 16 st + i,
+                              // c = 16 ct + 4 lq + 0..3): float4 runs of P and of Q
+  };
+  auto load_node = [&](int n, NodeIn& d) {
     const int64_t nb = bn0 + n;
-    float4 dy4[2], r4[2], tc4[2];
 #pragma unroll
     for (int v = 0; v < 2; ++v) {
       const int64_t e0 = nb * kGCT + (16 * v + i) * kGT + t0;
-      dy4[v] = *reinterpret_cast<const float4*>(a.dout + e0);
-      r4[v] = *reinterpret_cast<const float4*>(a.r + e0);
-      tc4[v] = *reinterpret_cast<const float4*>(a.tco + e0);
+      d.dy[v] = *reinterpret_cast<const float4*>(a.dout + e0);
+      d.r[v] = *reinterpret_cast<const float4*>(a.r + e0);
+      d.tc[v] = *reinterpret_cast<const float4*>(a.tco + e0);
     }
-    const float4 mu4 = *reinterpret_cast<const float4*>(a.mu + nb * kGT + t0);
-    const float4 rs4 = *reinterpret_cast<const float4*>(a.rs + nb * kGT + t0);
-    float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (FIRST) x4 = *reinterpret_cast<const float4*>(a.x + nb * kGT + t0);
-    // the conv rows behind this lane's dG entries (s = 16 st + i, c = 16 ct + 4 lq + 0..3): float4
-    // runs of P and of Q
-    float4 pv[2][2], qv[2][2];
+    d.mu = *reinterpret_cast<const float4*>(a.mu + nb * kGT + t0);
+    d.rs = *reinterpret_cast<const float4*>(a.rs + nb * kGT + t0);
+    d.x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (FIRST) d.x = *reinterpret_cast<const float4*>(a.x + nb * kGT + t0);
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int sidx = 16 * st + i;
@@ -514,14 +512,28 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
       const float* cb = kq == 0 ? a.conv[0] : (kq == 1 ? a.conv[1] : a.conv[2]);
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        pv[st][ct] = qv[st][ct] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d.p[st][ct] = d.q[st][ct] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (sidx < kGS) {
           const float* row = cb + (nb * Tg + tp) * (2 * kGC) + 16 * ct + 4 * lq;
-          pv[st][ct] = *reinterpret_cast<const float4*>(row);
-          qv[st][ct] = *reinterpret_cast<const float4*>(row + kGC);
+          d.p[st][ct] = *reinterpret_cast<const float4*>(row);
+          d.q[st][ct] = *reinterpret_cast<const float4*>(row + kGC);
         }
       }
     }
+  };
+  NodeIn nx;
+  if (w < nn) load_node(w, nx);
+#pragma unroll
+  for (int jn = 0; jn < (kGNB + kGW - 1) / kGW; ++jn) {
+    const int n = w + kGW * jn;
+    if (n >= nn) continue;
+    const int64_t nb = bn0 + n;
+    const NodeIn cur = nx;
+    if (jn + 1 < (kGNB + kGW - 1) / kGW && n + kGW < nn) load_node(n + kGW, nx);
+    const float4 *dy4 = cur.dy, *r4 = cur.r, *tc4 = cur.tc;
+    const float4 mu4 = cur.mu, rs4 = cur.rs, x4 = cur.x;
+    const float4(&pv)[2][2] = cur.p;
+    const float4(&qv)[2][2] = cur.q;
     // LayerNorm over C backward (the channel sums: DPP row sums over i, two channels a lane)
     float xh[2][4], dxh[2][4], s1[4], s2[4];
 #pragma unroll
