@@ -91,14 +91,13 @@ __device__ __forceinline__ void gf_gtu(const GtuFusedArgs& a, int q, int s_off, 
     for (int u = 0; u < kGMTW; ++u)
       if (mt0 + 4 * u < MT) av[u] = *reinterpret_cast<const float4*>(Xs + rowoff[u] + j * kGXS + c0 + 4 * lq);
 #pragma unroll
-    for (int u = 0; u < kGMTW; ++u) {
-      if (mt0 + 4 * u >= MT) continue;  // (wave-uniform)
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int u = 0; u < kGMTW; ++u) {
+        if (mt0 + 4 * u >= MT) continue;  // (wave-uniform)
         accp[u] = gmf16(g4at(bp, s), g4at(av[u], s), accp[u]);
         accq[u] = gmf16(g4at(bq, s), g4at(av[u], s), accq[u]);
       }
-    }
   };
   float4 p1, q1;
   int ch = 0;
@@ -363,39 +362,51 @@ size_t gtu_fused_bwd_lds() {
   return sizeof(float) * ((size_t)kGBStage + (size_t)kGNB * kGT * kGBX + 4 * kGW * kGC + (size_t)kGW * kGBF);
 }
 
-// step B for GTU KQ (kernel width KS)
+// step B for GTU KQ (kernel width KS): the staged operands — its rows (rows M..16 MT zero) and
+// its weights (j, c, o) as rows j C + c — are loaded into registers one GTU ahead (GbStage)
 template <int KQ>
-__device__ __forceinline__ void gb_tconv(const GtuFusedBwdArgs& a, int64_t bn0, int nn, float* Ds, float* dXs, int w,
-                                         int i, int lq) {
-  constexpr int KS = 3 + 2 * KQ, Tg = kGT - KS + 1, NT = kGW * 64;
-  const int M = nn * Tg, MT = (M + 15) / 16;
-  // stage the rows (rows M..16 MT zero) and the weights (j, c, o) as rows j C + c, one round
-  constexpr int RX = gb_rows(KQ);  // rows of a full workgroup
-  float* Ws = Ds + RX * kGBS;
-  {
-    constexpr int NV = (RX * 16 + NT - 1) / NT, NW = (KS * kGC * 16 + NT - 1) / NT;
-    const float4* src = reinterpret_cast<const float4*>(a.dconv[KQ] + bn0 * Tg * 2 * kGC);
-    const float4* wsrc = reinterpret_cast<const float4*>(a.wf[KQ]);
-    float4 v[NV], wv[NW];
+struct GbStage {
+  static constexpr int KS = 3 + 2 * KQ, RX = gb_rows(KQ), NT = kGW * 64;
+  static constexpr int NV = (RX * 16 + NT - 1) / NT, NW = (KS * kGC * 16 + NT - 1) / NT;
+  float4 v[NV], wv[NW];
+};
+template <int KQ>
+__device__ __forceinline__ void gb_load(const GtuFusedBwdArgs& a, int64_t bn0, int nn, GbStage<KQ>& g) {
+  using S = GbStage<KQ>;
+  constexpr int Tg = kGT - S::KS + 1;
+  const int M = nn * Tg;
+  const float4* src = reinterpret_cast<const float4*>(a.dconv[KQ] + bn0 * Tg * 2 * kGC);
+  const float4* wsrc = reinterpret_cast<const float4*>(a.wf[KQ]);
 #pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int e4 = u * NT + (int)threadIdx.x;
-      v[u] = e4 < M * 16 ? src[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < NW; ++u) wv[u] = wsrc[min(u * NT + (int)threadIdx.x, KS * kGC * 16 - 1)];
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int e4 = u * NT + (int)threadIdx.x, row = e4 >> 4;
-      if (row < RX) *reinterpret_cast<float4*>(Ds + row * kGBS + (e4 & 15) * 4) = v[u];
-    }
-#pragma unroll
-    for (int u = 0; u < NW; ++u) {
-      const int e4 = u * NT + (int)threadIdx.x, row = e4 >> 4;
-      if (row < KS * kGC) *reinterpret_cast<float4*>(Ws + row * kGBS + (e4 & 15) * 4) = wv[u];
-    }
+  for (int u = 0; u < S::NV; ++u) {
+    const int e4 = u * S::NT + (int)threadIdx.x;
+    g.v[u] = e4 < M * 16 ? src[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < S::NW; ++u) g.wv[u] = wsrc[min(u * S::NT + (int)threadIdx.x, S::KS * kGC * 16 - 1)];
+}
+template <int KQ>
+__device__ __forceinline__ void gb_store(float* Ds, const GbStage<KQ>& g) {
+  using S = GbStage<KQ>;
+  float* Ws = Ds + S::RX * kGBS;
+#pragma unroll
+  for (int u = 0; u < S::NV; ++u) {
+    const int e4 = u * S::NT + (int)threadIdx.x, row = e4 >> 4;
+    if (row < S::RX) *reinterpret_cast<float4*>(Ds + row * kGBS + (e4 & 15) * 4) = g.v[u];
+  }
+#pragma unroll
+  for (int u = 0; u < S::NW; ++u) {
+    const int e4 = u * S::NT + (int)threadIdx.x, row = e4 >> 4;
+    if (row < S::KS * kGC) *reinterpret_cast<float4*>(Ws + row * kGBS + (e4 & 15) * 4) = g.wv[u];
+  }
+}
+// the staged operands in LDS on entry; next() issues the next GTU's loads between this GTU's
+// matrix-core work and its accumulator taps; Ds is free on exit
+template <int KQ, class NX>
+__device__ __forceinline__ void gb_tconv(int nn, float* Ds, float* dXs, int w, int i, int lq, NX&& next) {
+  constexpr int KS = 3 + 2 * KQ, Tg = kGT - KS + 1;
+  const int M = nn * Tg, MT = (M + 15) / 16;
+  float* Ws = Ds + gb_rows(KQ) * kGBS;
   // every unit's k taps first (unit u = (tile u / 2, channel half u % 2), wave w: u = w + 8 uu) ...
   constexpr int MTX = (kGNB * Tg + 15) / 16, UPW = (2 * MTX + kGW - 1) / kGW;
   const int units = 2 * MT;
@@ -409,17 +420,27 @@ __device__ __forceinline__ void gb_tconv(const GtuFusedBwdArgs& a, int64_t bn0, 
     for (int j = 0; j < KS; ++j) acc[uu][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const float* brow = Ds + (mt * 16 + i) * kGBS + 4 * lq;             // B[k = o][n = row]
     const float* wrow = Ws + (16 * ct + i) * kGBS + 4 * lq;             // A[m = c][k = o], tap j at + j C rows
+    // fragments of chunk ch + 1 loaded while chunk ch multiplies; within a chunk the k taps'
+    // independent accumulators interleave (no back-to-back dependent MFMA)
+    float4 bq[2], aq[2][KS];
+    auto frag = [&](int ch, int buf) {
+      bq[buf] = *reinterpret_cast<const float4*>(brow + 16 * ch);
+#pragma unroll
+      for (int j = 0; j < KS; ++j) aq[buf][j] = *reinterpret_cast<const float4*>(wrow + j * kGC * kGBS + 16 * ch);
+    };
+    frag(0, 0);
 #pragma unroll
     for (int ch = 0; ch < 2 * kGC / 16; ++ch) {
-      const float4 b = *reinterpret_cast<const float4*>(brow + 16 * ch);
+      if (ch + 1 < 2 * kGC / 16) frag(ch + 1, (ch + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < KS; ++j) {
-        const float4 av = *reinterpret_cast<const float4*>(wrow + j * kGC * kGBS + 16 * ch);
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc[uu][j] = gmf16(g4at(av, s), g4at(b, s), acc[uu][j]);
-      }
+        for (int j = 0; j < KS; ++j) acc[uu][j] = gmf16(g4at(aq[ch & 1][j], s), g4at(bq[ch & 1], s), acc[uu][j]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
+  next();
   // ... then tap by tap into the accumulator rows: D[4 lq + r][i] is channel 16 ct + 4 lq + r of
   // input row m = 16 mt + i, and tap j sends it to row t' + j.  For one tap the input -> output
   // row map is one-to-one (no two writers of a row); the taps go in order with a barrier
@@ -678,23 +699,37 @@ __global__ __launch_bounds__(kGW * 64, 1) void gtu_bwd_fused_kernel(GtuFusedBwdA
     gf_st_agent(a.part + (int64_t)blockIdx.x * kGBP + 4 * kGC + tid, x);
   }
 
-  // ---- B. the transposed convolutions -------------------------------------------------------
-  gb_tconv<0>(a, bn0, nn, Ds, dXs, w, i, lq);
+  // ---- B. the transposed convolutions (each GTU's operands loaded during the previous one) ---
+  {
+    GbStage<0> st0;
+    gb_load<0>(a, bn0, nn, st0);
+    gb_store<0>(Ds, st0);
+  }
+  __syncthreads();
+  GbStage<1> st1;
+  gb_tconv<0>(nn, Ds, dXs, w, i, lq, [&]() { gb_load<1>(a, bn0, nn, st1); });
+  gb_store<1>(Ds, st1);
+  __syncthreads();
   TF_MARK(3);
-  gb_tconv<1>(a, bn0, nn, Ds, dXs, w, i, lq);
+  GbStage<2> st2;
+  gb_tconv<1>(nn, Ds, dXs, w, i, lq, [&]() { gb_load<2>(a, bn0, nn, st2); });
+  gb_store<2>(Ds, st2);
+  __syncthreads();
   TF_MARK(4);
-  gb_tconv<2>(a, bn0, nn, Ds, dXs, w, i, lq);
+  // (the X rows of step C ride on the last GTU)
+  constexpr int XV = (kGNB * kGCT / 4 + NT - 1) / NT;
+  const int ne4 = nn * kGCT / 4;
+  float4 xv[XV];
+  gb_tconv<2>(nn, Ds, dXs, w, i, lq, [&]() {
+    const float4* gx = reinterpret_cast<const float4*>(a.X + bn0 * kGCT);
+#pragma unroll
+    for (int u = 0; u < XV; ++u) xv[u] = gx[min(u * NT + tid, ne4 - 1)];
+  });
   TF_MARK(5);
 
   // ---- C. gpre = (X > 0) ? dX : 0 -----------------------------------------------------------
   {
-    constexpr int XV = (kGNB * kGCT / 4 + NT - 1) / NT;
-    const int ne4 = nn * kGCT / 4;
-    const float4* gx = reinterpret_cast<const float4*>(a.X + bn0 * kGCT);
     float4* go = reinterpret_cast<float4*>(a.gpre + bn0 * kGCT);
-    float4 xv[XV];
-#pragma unroll
-    for (int u = 0; u < XV; ++u) xv[u] = gx[min(u * NT + tid, ne4 - 1)];
 #pragma unroll
     for (int u = 0; u < XV; ++u) {
       const int e4 = u * NT + tid;
