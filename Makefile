@@ -36,7 +36,7 @@ $(RACEBUG): $(filter-out build/block.o,$(OBJ)) build/racebug/block.o
 # phase-timing variant of the fused kernels (-DDSTAGNN_TF_TIMING: per-phase wall-clock printf from
 # workgroups 0 and 100), loaded by LD_LIBRARY_PATH=abtest/tftime; not part of `all`
 TFTIME := abtest/tftime/libdstagnn.so
-TF_SRC := tat_fused gtu_fused
+TF_SRC := tat_fused gtu_fused sat_fused
 tftime: $(TFTIME)
 
 build/tftime/%.o: dstagnn_drought_amd/csrc/%.hip dstagnn_drought_amd/csrc/*.hpp include/dstagnn.h

@@ -55,6 +55,7 @@ struct Dims {
   bool tfused_bwd;  // ... and its backward (tat_fused.hip)
   bool gfused;      // the GTU stage forward as one kernel (gtu_fused.hip)
   bool gbfused;     // ... and its backward (gtu_fused.hip): compact gate-gradient rows, no tconv
+  bool sfused;      // the SAt projection backward + EmbedS LN backward as one kernel (sat_fused.hip)
   int64_t tf_wg;    // tfused_bwd: its workgroups (one gamma / beta partial row each)
   int64_t nnz;      // flash: union-support entries
   int64_t apa_nnz;  // small-graph flash: A_pa support entries
@@ -82,6 +83,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.tf_wg = m.tfused_bwd ? cdiv64(m.BFT, 48) : 0;
   m.gfused = gtu_fused_fwd_ok(m.C, m.T);
   m.gbfused = gtu_fused_bwd_ok(m.C, m.T);
+  m.sfused = sat_ln_bwd_fused_ok(m.D, 2 * m.KD);
   return m;
 }
 
@@ -93,6 +95,7 @@ struct SaveBufs {
   float* Wqkv_p;  // tfused: [Wq; Wk; Wv] with rows zero-padded to NP
   float *WfcT, *WqT;  // tfused_bwd: W_fc^T (h dv, NP) and [Wq; Wk; Wv]^T (NP, 3 h dk), zero-padded
   float* Wgt[3];      // gfused: GTU weights (o, j, c) for the fused GTU forward
+  float* WqkT;        // sfused: [W_Q'; W_K']^T (D, 2 KD)
   float *E, *qkv, *att, *ctx, *u_tat, *mu_tat, *rs_tat, *O, *u_s, *mu_s, *rs_s, *Zd, *qk, *P, *W, *xth, *X;
   float *lse, *psupp, *wsupp;  // flash path: column log-sum-exp (B,K,N), P and T o P on the support (B,K,nnz)
   float *am, *amt, *papa;      // small-graph flash: A_pa o M_k (K,N,N) and its transpose, P on the A_pa support
@@ -107,6 +110,7 @@ SaveBufs plan_save(const Dims& m, Arena& a) {
   s.WfcT = m.tfused_bwd ? a.take(m.HV * m.NP) : nullptr;
   s.WqT = m.tfused_bwd ? a.take(m.QW * m.NP) : nullptr;
   for (int g = 0; g < 3; ++g) s.Wgt[g] = m.gfused ? a.take(2 * (int64_t)m.C * m.C * m.ks[g]) : nullptr;
+  s.WqkT = m.sfused ? a.take((int64_t)m.D * 2 * m.KD) : nullptr;
   s.Wqk = a.take(2 * m.KD * m.D);
   s.Wp = a.take((int64_t)m.D * m.FT);
   s.thcat = a.take((int64_t)m.F * m.KC);
@@ -886,6 +890,12 @@ struct Fwd {
     }
     add(0, p.sat_wq, s.Wqk, m.KD * m.D, 0, 0, 0, 0);
     add(0, p.sat_wk, s.Wqk, m.KD * m.D, 0, 0, 0, m.KD * m.D);
+    if (m.sfused) {  // [W_Q'; W_K']^T (D, 2 KD): WqkT[d][k] = W[k][d]
+      add(9, p.sat_wq, s.WqkT, m.D * m.KD, (int)m.KD, m.D, (int)(2 * m.KD), 0);
+      pp.seg[pp.nseg - 1].p3 = (int)m.KD;
+      add(9, p.sat_wk, s.WqkT, m.D * m.KD, (int)m.KD, m.D, (int)(2 * m.KD), m.KD);
+      pp.seg[pp.nseg - 1].p3 = (int)m.KD;
+    }
     add(1, p.pre_conv_w, s.Wp, (int64_t)m.D * m.FT, m.F, m.T);  // Wp[d][f][t] = W[d][t][0][f]
     for (int k = 0; k < m.K; ++k) add(2, p.theta[k], s.thcat, (int64_t)m.F * m.C, m.C, (int)m.KC, k);
     for (int g = 0; g < 3; ++g) {
@@ -1439,6 +1449,18 @@ struct Bwd {
       g.alpha = sc;
       DS_TRY(gemm(g));
     }
+    int64_t ln_rows = ln_bwd_partials_ok(m.D) ? ln_bwd_part_blocks(m.BN) : m.BN;  // partial rows
+    if (m.sfused) {  // dZd GEMM + EmbedS LN backward in one kernel (sat_fused.hip): dZd never written
+      SatLnBwdArgs a;
+      a.R = m.BN; a.D = m.D; a.K2 = ld;
+      a.dqk = w.dqk; a.wT = s.WqkT;
+      a.u = s.u_s; a.mu = s.mu_s; a.rs = s.rs_s; a.g = p.embS_g;
+      if (d.train && d.drop_p > 0.f) { a.drop_p = d.drop_p; a.seed = d.seed; a.drop_off = drop_off(d, 0); }
+      a.dx = w.dY;
+      a.gpart = w.gcon_s; a.bpart = w.bcon_s; a.xpart = preconv_bias_part();
+      DS_TRY(op_sat_ln_bwd_fused(a, st));
+      ln_rows = sat_ln_bwd_fused_wgs(m.BN);
+    } else {
     {
       Gemm g;  // dZd = dqk [W_Q'; W_K']
       g.M = (int)m.BN; g.N = m.D; g.K = (int)ld;
@@ -1463,6 +1485,7 @@ struct Bwd {
         a.gcontrib = w.gcon_s; a.bcontrib = w.bcon_s;
       }
       DS_TRY(op_ln_bwd(a, st));
+    }
     }
     // --- side: SAt projection, EmbedS gamma / beta / pos-embedding, pre_conv bias and weight
     // grads; the fork's flag rides on the pre_conv data-gradient GEMM, issued first
@@ -1493,7 +1516,7 @@ struct Bwd {
     // column tile to the 384-wide output: measured slower), else its own column sum
     float* xpart = preconv_bias_part();
     DS_TRY(colsums({{w.gcon_s, gd.embS_g}, {w.bcon_s, gd.embS_b}, {xpart, xpart ? gd.pre_conv_b : nullptr}},
-                   ln_bwd_partials_ok(m.D) ? ln_bwd_part_blocks(m.BN) : m.BN, m.D, 1));
+                   ln_rows, m.D, 1));
     if (!xpart) DS_TRY(colsum_on(sd, w.dY, m.BN, m.D, 1, gd.pre_conv_b));
     if (gd.embS_pos) DS_TRY(op_sum_middle(w.dY, 1, m.B, (int64_t)m.N * m.D, gd.embS_pos, 0.f, sq()));
     if (gd.pre_conv_w && !dwp_main()) DS_TRY(sgemm(dwp_gemm()));

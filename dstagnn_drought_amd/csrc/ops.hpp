@@ -319,6 +319,18 @@ struct GtuFusedArgs {
   float* conv[3] = {};             // (BN (T - k + 1), 2C), bias included (saved)
   float *G = nullptr, *tco = nullptr, *r = nullptr, *mu = nullptr, *rs = nullptr, *out = nullptr;
 };
+struct SatLnBwdArgs {  // sat_fused.hip: dZd = dqk [W_Q'; W_K'] + EmbedS LayerNorm(D) backward
+  int64_t R = 0, D = 0, K2 = 0;    // rows B N, d_model, 2 K d_k
+  const float* dqk = nullptr;      // (R, K2)
+  const float* wT = nullptr;       // (D, K2) = [W_Q'; W_K']^T (param_prep kind 9)
+  const float *u = nullptr, *mu = nullptr, *rs = nullptr, *g = nullptr;
+  float drop_p = 0.f; uint64_t seed = 0; uint64_t drop_off = 0;  // the EmbedS dropout (which = 0)
+  float* dx = nullptr;             // dY (R, D)
+  float *gpart = nullptr, *bpart = nullptr, *xpart = nullptr;  // [workgroup][D] partial rows (xpart optional)
+};
+bool sat_ln_bwd_fused_ok(int64_t D, int64_t K2);
+int64_t sat_ln_bwd_fused_wgs(int64_t R);
+int op_sat_ln_bwd_fused(const SatLnBwdArgs& a, hipStream_t st);
 bool gtu_fused_fwd_ok(int C, int T);
 int op_gtu_fused_fwd(const GtuFusedArgs& a, hipStream_t st);
 struct GtuFusedBwdArgs {

@@ -25,6 +25,8 @@ a subprocess (the library reads its switches once per process):
                        gtu_fused.hip's one kernel (convolutions, gates, fcmy, residual, LN)
   DSTAGNN_GTU_FUSED_BWD=0  the GTU stage backward as gtu_tail_bwd_ct + gtu_tconv (zero-padded gate
                        gradient rows) instead of gtu_fused.hip's one kernel
+  DSTAGNN_SATLN_FUSED=1  the SAt projection backward (dZd GEMM) and the EmbedS LayerNorm backward as one
+                       kernel (sat_fused.hip) instead of a GEMM + ln_bwd
   DSTAGNN_DWP_MAIN=1   the pre_conv weight gradient on the main stream instead of the side stream
   DSTAGNN_DEBUG_STREAMS=1  the fork invariant asserted (block.hip Bwd::sq): no side-stream work
                        issued while a fork's signal is still pending
@@ -71,7 +73,7 @@ print("KNOB_OK")
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems08", 4),
                                        ("DSTAGNN_TAT_FUSED=0", "pems08", 4),
                                        ("DSTAGNN_TAIL_FOLD=1", "pems08", 4),
-                                       ("DSTAGNN_GTU_FUSED=0", "pems08", 4), ("DSTAGNN_GTU_FUSED_BWD=0", "pems08", 4),
+                                       ("DSTAGNN_GTU_FUSED=0", "pems08", 4), ("DSTAGNN_GTU_FUSED_BWD=0", "pems08", 4), ("DSTAGNN_SATLN_FUSED=1", "pems08", 4),
                                        ("DSTAGNN_DWP_MAIN=1", "pems08", 4),
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems07+flash", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
