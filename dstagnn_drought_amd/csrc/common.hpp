@@ -199,18 +199,40 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ---------------------------------------------------------------------------------
-// Counter-based dropout RNG (splitmix64 finaliser of seed ^ stream ^ index).
+// Counter-based dropout RNG: a splitmix64 key per (seed, mask), two 32-bit finalisers per element.
 // ---------------------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
+// 32-bit finaliser (two 32-bit multiplies; "lowbias32")
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// the per-(seed, mask) key: one 64-bit finaliser of uniform values (hoisted out of the loops)
+struct DropKey {
+  uint32_t lo, hi;
+};
+__host__ __device__ __forceinline__ DropKey drop_key(uint64_t seed, uint32_t which) {
+  const uint64_t z = mix64(seed * 0x9E3779B97F4A7C15ull + ((uint64_t)which << 56) + 1);
+  return DropKey{(uint32_t)z, (uint32_t)(z >> 32)};
+}
+// the uniform draw of element idx: two 32-bit finalisers (the element index's high word first,
+// its low word through a bijection: distinct indices of one high word never collide) — the
+// 64-bit multiplies of a 64-bit finaliser per element are quarter rate on the vector ALU
+__host__ __device__ __forceinline__ float drop_u(DropKey k, uint64_t idx) {
+  const uint32_t h = mix32((uint32_t)idx ^ k.lo ^ mix32((uint32_t)(idx >> 32) ^ k.hi));
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
 // scale = 1/(1-p) when kept, 0 when dropped
 __device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t which, uint64_t idx, float p) {
-  uint64_t z = mix64(seed * 0x9E3779B97F4A7C15ull + ((uint64_t)which << 56) + idx * 0xD1B54A32D192ED03ull + 1);
-  float u = (float)(z >> 40) * (1.0f / 16777216.0f);
-  return u >= p ? 1.0f / (1.0f - p) : 0.0f;
+  return drop_u(drop_key(seed, which), idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
 // ---------------------------------------------------------------------------------

@@ -97,17 +97,16 @@ __global__ __launch_bounds__(kSbW * 64, 1) void sat_ln_bwd_fused_kernel(SatLnBwd
     for (int t = 0; t < kSbDT; ++t) ap[buf][t] = *reinterpret_cast<const float4*>(wrow + 16 * t * kSbK + 16 * ch);
   };
   // the dropout keep bits of the lane's 32 elements (bit 16 rt + 4 t + r), hashed between the
-  // matrix-core instructions of the k loop (drop_scale's hash and threshold; the 64-bit
-  // multiplies are quarter rate: after the loop they cost more than the product itself)
+  // matrix-core instructions of the k loop (drop_scale's hash and threshold; its multiplies
+  // are quarter rate: after the loop they cost more than the product itself)
   constexpr int NE = kSbRT * kSbDT * 4, NCH = kSbK / 16, PER = (NE + NCH - 1) / NCH;
   uint32_t keep = 0;
   const bool drop = a.drop_p > 0.f;
-  const uint64_t hbase = a.seed * 0x9E3779B97F4A7C15ull + 1;  // which = 0
+  const DropKey dk = drop_key(a.seed, 0);  // which = 0
   auto hash = [&](int k) {
     const int rt = k >> 4, t = (k >> 2) & 3, r = k & 3;
     const uint64_t idx = (uint64_t)row[rt] * kSbD + 16 * (kSbDT * w + t) + 4 * lq + r + a.drop_off;
-    const uint64_t z = mix64(hbase + idx * 0xD1B54A32D192ED03ull);
-    keep |= ((float)(z >> 40) * (1.0f / 16777216.0f) >= a.drop_p ? 1u : 0u) << k;
+    keep |= (drop_u(dk, idx) >= a.drop_p ? 1u : 0u) << k;
   };
   frag(0, 0);
 #pragma unroll
