@@ -607,6 +607,190 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd a) {
   }
 }
 
+// Rows of L = 256 V4 contiguous floats (the EmbedS LayerNorm over D = 512): the same
+// arithmetic with every load and store a float4 — lane l holds elements 4 (l + 64 q) .. + 3 —
+// so a row is V4 16-B loads per source per lane instead of 4 V4 dword loads (the wave-per-row
+// kernel above at L = 512 issued 32 loads and 16 stores per lane).  The row sums go over a
+// different partition of the row (within the fp32 rounding of the other kernel).
+__device__ __forceinline__ float l4at(const float4& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
+__device__ __forceinline__ void l4set(float4& v, int c, float x) {
+  if (c == 0) v.x = x; else if (c == 1) v.y = x; else if (c == 2) v.z = x; else v.w = x;
+}
+template <int V4, int NSRC>
+__global__ __launch_bounds__(256) void ln_fwd_v4_kernel(LnFwd a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.R) return;
+  constexpr int L = 256 * V4;
+  float4 xs[NSRC][V4], gv[V4], bv[V4], v[V4];
+#pragma unroll
+  for (int q = 0; q < V4; ++q) {
+    const int e4 = lane + 64 * q;
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s)
+      xs[s][q] = reinterpret_cast<const float4*>(a.src[s].p + ioff(a.src[s].row, row))[e4];
+    gv[q] = reinterpret_cast<const float4*>(a.g)[e4];
+    bv[q] = reinterpret_cast<const float4*>(a.b)[e4];
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int q = 0; q < V4; ++q) {
+    v[q] = xs[0][q];
+#pragma unroll
+    for (int s = 1; s < NSRC; ++s) {
+      v[q].x += xs[s][q].x; v[q].y += xs[s][q].y; v[q].z += xs[s][q].z; v[q].w += xs[s][q].w;
+    }
+    sum += (v[q].x + v[q].y) + (v[q].z + v[q].w);
+  }
+  const float mean = wave_sum(sum) / L;
+  float var = 0.f;
+#pragma unroll
+  for (int q = 0; q < V4; ++q)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float d = l4at(v[q], c) - mean;
+      var += d * d;
+    }
+  var = wave_sum(var) / L;
+  const float rs = rsqrtf(var + a.eps);
+  if (lane == 0) { a.mu[row] = mean; a.rs[row] = rs; }
+  const int64_t yo = ioff(a.yrow, row);
+  const DropKey dk = drop_key(a.seed, a.which);
+  const float dscale = 1.0f / (1.0f - a.drop_p);
+#pragma unroll
+  for (int q = 0; q < V4; ++q) {
+    const int e4 = lane + 64 * q;
+    if (a.u) reinterpret_cast<float4*>(a.u + (int64_t)row * L)[e4] = v[q];
+    float4 y;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float t = (l4at(v[q], c) - mean) * rs * l4at(gv[q], c) + l4at(bv[q], c);
+      if (a.drop_p > 0.f) t *= drop_u(dk, (uint64_t)row * L + 4 * e4 + c + a.drop_off) >= a.drop_p ? dscale : 0.0f;
+      l4set(y, c, t);
+    }
+    reinterpret_cast<float4*>(a.y + yo)[e4] = y;
+  }
+}
+
+// the backward of the same rows (ln_bwd_kernel's arithmetic; PART: per-workgroup partial slabs)
+template <int V4, bool PART>
+__global__ __launch_bounds__(256) void ln_bwd_v4_kernel(LnBwd a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int L = 256 * V4;
+  const int row = blockIdx.x * 4 + wv;
+  float4 gp[V4], bp[V4], xp[V4];
+#pragma unroll
+  for (int q = 0; q < V4; ++q) gp[q] = bp[q] = xp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (row < a.R) {
+    const int64_t yo = ioff(a.dyrow, row), xo = ioff(a.dxrow, row);
+    float4 dyl[V4], ul[V4], gl[V4], xin[V4];
+#pragma unroll
+    for (int q = 0; q < V4; ++q) {
+      const int e4 = lane + 64 * q;
+      dyl[q] = reinterpret_cast<const float4*>(a.dy + yo)[e4];
+      ul[q] = reinterpret_cast<const float4*>(a.u + (int64_t)row * L)[e4];
+      gl[q] = reinterpret_cast<const float4*>(a.g)[e4];
+      if (a.beta != 0.f) xin[q] = reinterpret_cast<const float4*>(a.dx + xo)[e4];
+    }
+    const float mean = a.mu[row], rs = a.rs[row];
+    const DropKey dk = drop_key(a.seed, a.which);
+    const float dscale = 1.0f / (1.0f - a.drop_p);
+    float4 dyv[V4], xh[V4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < V4; ++q) {
+      const int e4 = lane + 64 * q;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float dy = l4at(dyl[q], c);
+        if (a.drop_p > 0.f) dy *= drop_u(dk, (uint64_t)row * L + 4 * e4 + c + a.drop_off) >= a.drop_p ? dscale : 0.0f;
+        const float x = (l4at(ul[q], c) - mean) * rs;
+        l4set(dyv[q], c, dy);
+        l4set(xh[q], c, x);
+        const float dxh = dy * l4at(gl[q], c);
+        s1 += dxh;
+        s2 += dxh * x;
+        if (PART) {
+          l4set(gp[q], c, dy * x);
+          l4set(bp[q], c, dy);
+        } else {
+          if (a.gcontrib) a.gcontrib[(int64_t)row * L + 4 * e4 + c] = dy * x;
+          if (a.bcontrib) a.bcontrib[(int64_t)row * L + 4 * e4 + c] = dy;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / L;
+    s2 = wave_sum(s2) / L;
+#pragma unroll
+    for (int q = 0; q < V4; ++q) {
+      float4 d;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float t = rs * (l4at(dyv[q], c) * l4at(gl[q], c) - s1 - l4at(xh[q], c) * s2);
+        if (a.beta != 0.f) t += a.beta * l4at(xin[q], c);
+        l4set(d, c, t);
+      }
+      reinterpret_cast<float4*>(a.dx + xo)[lane + 64 * q] = d;
+      if (PART) xp[q] = d;
+    }
+  }
+  if constexpr (PART) {
+    __shared__ float4 red[2][4][64 * V4];
+#pragma unroll
+    for (int q = 0; q < V4; ++q) {
+      red[0][wv][lane + 64 * q] = gp[q];
+      red[1][wv][lane + 64 * q] = bp[q];
+    }
+    __syncthreads();
+    for (int e4 = threadIdx.x; e4 < L / 4; e4 += 256) {
+      float4 g = red[0][0][e4], b = red[1][0][e4];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float4 g2 = red[0][k][e4], b2 = red[1][k][e4];
+        g.x += g2.x; g.y += g2.y; g.z += g2.z; g.w += g2.w;
+        b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+      }
+      if (a.gpart) reinterpret_cast<float4*>(a.gpart + (int64_t)blockIdx.x * L)[e4] = g;
+      if (a.bpart) reinterpret_cast<float4*>(a.bpart + (int64_t)blockIdx.x * L)[e4] = b;
+    }
+    if (a.xpart) {  // the dx sums through the same LDS rows (workgroup-uniform branch)
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < V4; ++q) red[0][wv][lane + 64 * q] = xp[q];
+      __syncthreads();
+      for (int e4 = threadIdx.x; e4 < L / 4; e4 += 256) {
+        float4 x = red[0][0][e4];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          const float4 x2 = red[0][k][e4];
+          x.x += x2.x; x.y += x2.y; x.z += x2.z; x.w += x2.w;
+        }
+        reinterpret_cast<float4*>(a.xpart + (int64_t)blockIdx.x * L)[e4] = x;
+      }
+    }
+  }
+}
+
+// the float4 kernels' preconditions: L = 256 or 512 or 1024, unit element strides, every row
+// base and pointer 16-B aligned (row maps with strides that are multiples of 4 floats)
+static bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static bool map4(const Idx2& m) { return m.s0 % 4 == 0 && m.s1 % 4 == 0; }
+static bool ln_v4_env() {
+  static const bool on = !getenv("DSTAGNN_LN_V4") || atoi(getenv("DSTAGNN_LN_V4")) != 0;  // default on
+  return on;
+}
+static bool ln_fwd_v4_ok(const LnFwd& a) {
+  if (!ln_v4_env() || (a.L != 256 && a.L != 512 && a.L != 1024) || a.yes != 1 || !map4(a.yrow)) return false;
+  for (int s = 0; s < a.nsrc; ++s)
+    if (a.src[s].es != 1 || !map4(a.src[s].row) || !al16p(a.src[s].p)) return false;
+  return al16p(a.g) && al16p(a.b) && al16p(a.y) && al16p(a.u);
+}
+static bool ln_bwd_v4_ok(const LnBwd& a) {
+  return ln_v4_env() && (a.L == 256 || a.L == 512 || a.L == 1024) && a.dyes == 1 && a.dxes == 1 && map4(a.dyrow) &&
+         map4(a.dxrow) && al16p(a.dy) && al16p(a.u) && al16p(a.g) && al16p(a.dx) && al16p(a.gpart) &&
+         al16p(a.bpart) && al16p(a.xpart);
+}
+
 // Long rows (L > 1024: the TAt / EmbedT LayerNorm over N nodes at GAMBIA N = 2139 and SYN
 // N = 4096): a 256-thread WORKGROUP per row, element e = tid + 256 q (VPT <= 16 values per
 // thread, all loads in one round as above), the sums over the row by a wave reduction and the
@@ -1780,6 +1964,16 @@ static bool ln_wg_rows() {
 int op_ln_fwd(const LnFwd& a, hipStream_t st) {
   if (a.nsrc < 1 || a.nsrc > 3 || a.L < 1) { set_last_error("ln_fwd: 1..3 sources, L >= 1"); return DSTAGNN_E_ARG; }
   dim3 grid((unsigned)cdiv64(a.R, 4));
+  if (ln_fwd_v4_ok(a)) {  // float4 rows
+#define DS_LN4(V) \
+    if (a.nsrc == 1) hipLaunchKernelGGL((ln_fwd_v4_kernel<V, 1>), grid, dim3(256), 0, st, a); \
+    else if (a.nsrc == 2) hipLaunchKernelGGL((ln_fwd_v4_kernel<V, 2>), grid, dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((ln_fwd_v4_kernel<V, 3>), grid, dim3(256), 0, st, a);
+    if (a.L == 256) { DS_LN4(1) } else if (a.L == 512) { DS_LN4(2) } else { DS_LN4(4) }
+#undef DS_LN4
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   int vpt = (int)cdiv64(a.L, 64);
   if (vpt <= 1) launch_ln_fwd<1>(a, grid, st);
   else if (vpt <= 2) launch_ln_fwd<2>(a, grid, st);
@@ -1807,6 +2001,13 @@ int op_ln_bwd(const LnBwd& a, hipStream_t st) {
   if (a.gpart || a.bpart || a.xpart) {
     if (!ln_bwd_partials_ok(a.L)) { set_last_error("ln_bwd: partial slabs need L <= 1024"); return DSTAGNN_E_SHAPE; }
     dim3 grid((unsigned)ln_bwd_part_blocks(a.R));
+    if (kLnRowsPerWave == 1 && ln_bwd_v4_ok(a)) {  // float4 rows (one row per wave, as below)
+      if (a.L == 256) hipLaunchKernelGGL((ln_bwd_v4_kernel<1, true>), grid, dim3(256), 0, st, a);
+      else if (a.L == 512) hipLaunchKernelGGL((ln_bwd_v4_kernel<2, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((ln_bwd_v4_kernel<4, true>), grid, dim3(256), 0, st, a);
+      DS_CHECK_LAUNCH();
+      return 0;
+    }
     if (vpt <= 1) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, st, a);
     else if (vpt <= 2) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, st, a);
     else if (vpt <= 4) hipLaunchKernelGGL((ln_bwd_kernel<4, true>), grid, dim3(256), 0, st, a);
