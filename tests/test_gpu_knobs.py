@@ -27,6 +27,8 @@ a subprocess (the library reads its switches once per process):
                        gradient rows) instead of gtu_fused.hip's one kernel
   DSTAGNN_SATLN_FUSED=1  the SAt projection backward (dZd GEMM) and the EmbedS LayerNorm backward as one
                        kernel (sat_fused.hip) instead of a GEMM + ln_bwd
+  DSTAGNN_LN_V4=0      the LayerNorm rows of 256 / 512 / 1024 floats by the scalar wave-per-row kernels
+                       instead of the float4 ones
   DSTAGNN_DWP_MAIN=1   the pre_conv weight gradient on the main stream instead of the side stream
   DSTAGNN_DEBUG_STREAMS=1  the fork invariant asserted (block.hip Bwd::sq): no side-stream work
                        issued while a fork's signal is still pending
@@ -73,7 +75,8 @@ print("KNOB_OK")
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems08", 4),
                                        ("DSTAGNN_TAT_FUSED=0", "pems08", 4),
                                        ("DSTAGNN_TAIL_FOLD=1", "pems08", 4),
-                                       ("DSTAGNN_GTU_FUSED=0", "pems08", 4), ("DSTAGNN_GTU_FUSED_BWD=0", "pems08", 4), ("DSTAGNN_SATLN_FUSED=1", "pems08", 4),
+                                       ("DSTAGNN_GTU_FUSED=0", "pems08", 4), ("DSTAGNN_GTU_FUSED_BWD=0", "pems08", 4),
+                                       ("DSTAGNN_SATLN_FUSED=1", "pems08", 4), ("DSTAGNN_LN_V4=0", "pems08", 4),
                                        ("DSTAGNN_DWP_MAIN=1", "pems08", 4),
                                        ("DSTAGNN_DEBUG_STREAMS=1", "pems07+flash", 2)])
 def test_knob_path_vs_oracle(env, cfg, B):
