@@ -154,3 +154,25 @@ def dropout_masks(meta, x_shape, seed, sample_base=0):
     like = torch.empty(0, device="cuda")
     return ops.dropout_masks(like, list(x_shape), cfg_of(meta), float(meta.get("drop_p", 0.05)), int(seed),
                              int(sample_base))
+
+
+# dstagnn_block_paths bits (include/dstagnn.h DSTAGNN_PATH_*)
+PATH_BITS = {"sparse": 1, "flash": 2, "flash_small": 4, "cheb_agg": 8, "tat_fused_fwd": 16, "tat_fused_bwd": 32,
+             "gtu_fused_fwd": 64, "gtu_fused_bwd": 128, "sat_ln_fused": 256}
+
+
+def block_paths(blk, x, res_att, train=False):
+    """The set of kernel paths (PATH_BITS names) the library takes for this block module on
+    this input (dstagnn::block_paths over dstagnn_block_paths: decided from the call's dims and
+    the process's DSTAGNN_* knobs; launches nothing) — parity tests assert with it that the
+    kernels they hold to the oracle are the ones that ran."""
+    ops = _lib.load()
+    names, ps, slots = blk._param_list()
+    graph = blk._graph()
+    sparse = use_sparse(graph, blk.meta, x.shape[3])
+    fl = use_flash(graph, blk.meta, x.shape[3], blk.flash_cheb, x.shape[0])
+    if fl:
+        graph = blk._flash_graph(graph)
+    bits = ops.block_paths(x.detach().float().contiguous(), res_arg(res_att, x.shape[2]), list(ps), slots,
+                           graph_list(graph, sparse, fl), cfg_of(blk.meta), 0.05, 0, flags_of(train, sparse, False, fl))
+    return {n for n, b in PATH_BITS.items() if bits & b}

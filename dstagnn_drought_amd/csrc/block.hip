@@ -80,7 +80,7 @@ Dims mkdims(const dstagnn_block_dims& d) {
   m.tfused = tat_fused_fwd_ok(m.N, m.T, m.h, m.dk, m.dv);
   m.NP = m.tfused ? tat_fused_np(m.N) : 0;
   m.tfused_bwd = m.tfused && tat_fused_bwd_ok(m.N, m.T, m.h, m.dk, m.dv, m.F, d.res_mode);
-  m.tf_wg = m.tfused_bwd ? cdiv64(m.BFT, 48) : 0;
+  m.tf_wg = m.tfused_bwd ? tat_fused_bwd_wgs(m.BFT) : 0;
   m.gfused = gtu_fused_fwd_ok(m.C, m.T);
   m.gbfused = gtu_fused_bwd_ok(m.C, m.T);
   m.sfused = sat_ln_bwd_fused_ok(m.D, 2 * m.KD);
@@ -179,7 +179,8 @@ Scratch plan_scratch(const Dims& m, Arena& a) {
   s.part_side = a.take(kPart);
   s.dWqkv = a.take(m.QW * m.N);
   s.dWqk = a.take(2 * m.KD * m.D);
-  s.gcon_t = a.take(m.BN * m.CT);
+  // (the fused GTU backward's ticket-tree rows live here too: at small B they outgrow BN CT)
+  s.gcon_t = a.take(m.gbfused ? std::max<int64_t>(m.BN * m.CT, gtu_fused_bwd_part_floats(m.BN)) : m.BN * m.CT);
   s.bcon_t = a.take(m.BN * m.CT);
   s.dres_t = a.take(m.BN * m.CT);
   s.gcon_s = a.take(m.BN * m.D);
@@ -1182,7 +1183,7 @@ struct Bwd {
     // per-workgroup rows in gcon_t): no column sums on the side stream
     g.gout = gd.ln_g; g.bout = gd.ln_b; g.fwout = gd.fcmy_w; g.fbout = gd.fcmy_b;
     if (m.first) { g.rwout = gd.res_w; g.rbout = gd.res_b; }
-    g.part = w.gcon_t;  // (BN CT floats >= gtu_fused_bwd_part_floats)
+    g.part = w.gcon_t;  // (sized max(BN CT, gtu_fused_bwd_part_floats(BN)) by plan_scratch)
     // (a flag written by the kernel's last workgroup instead of this fork measured 20 us/step
     // SLOWER: the side's GTU weight-gradient GEMM then starts under the SDDMM and both stretch)
     DS_TRY(op_gtu_fused_bwd(g, st));
@@ -1729,7 +1730,7 @@ struct Bwd {
     return on;
   }
   // fused TAt backward: the beta slab's first row (gamma: level-1 rows, then the ticket tree's level-2 rows)
-  int64_t tat_bslab() const { return m.tf_wg + cdiv64(m.tf_wg, 16); }
+  int64_t tat_bslab() const { return tat_fused_bwd_part_rows(m.BFT); }  // the gamma slab's rows (tat_fused.hip)
   int tat_ln_colsums(bool on_main) {
     if (m.tfused_bwd)  // one gamma / beta partial row per fused-kernel workgroup
       return colsums({{w.gcon_a, gd.tat_ln_g}, {w.gcon_a + tat_bslab() * m.N, gd.tat_ln_b}}, m.tf_wg, m.N, 1, on_main);
@@ -1879,6 +1880,18 @@ int dstagnn_block_save_offset(const dstagnn_block_dims* d, int which, size_t* of
   const float* t = which == 0 ? s.X : (which == 1 ? s.tco : s.r);
   *offset_bytes = (size_t)((const char*)t - (char*)(uintptr_t)256);
   *count = (size_t)(m.BN * m.CT);
+  return 0;
+}
+
+int dstagnn_block_paths(const dstagnn_block_dims* d, uint32_t* bits) {
+  DS_TRY(check_dims(d));
+  if (!bits) return DSTAGNN_E_ARG;
+  const Dims m = mkdims(*d);
+  *bits = (m.sparse ? DSTAGNN_PATH_SPARSE : 0u) | (m.flash ? DSTAGNN_PATH_FLASH : 0u) |
+          (m.fsmall ? DSTAGNN_PATH_FLASH_SMALL : 0u) | (m.agg ? DSTAGNN_PATH_CHEB_AGG : 0u) |
+          (m.tfused ? DSTAGNN_PATH_TAT_FUSED_FWD : 0u) | (m.tfused_bwd ? DSTAGNN_PATH_TAT_FUSED_BWD : 0u) |
+          (m.gfused ? DSTAGNN_PATH_GTU_FUSED_FWD : 0u) | (m.gbfused ? DSTAGNN_PATH_GTU_FUSED_BWD : 0u) |
+          (m.sfused ? DSTAGNN_PATH_SAT_LN_FUSED : 0u);
   return 0;
 }
 

@@ -280,6 +280,8 @@ struct TatFusedArgs {
 };
 bool tat_fused_fwd_ok(int N, int T, int h, int dk, int dv);
 int tat_fused_np(int N);  // the padded node count of the re-laid Q|K|V weights
+int64_t tat_fused_bwd_wgs(int64_t BFT);        // the fused backward's workgroups (partial rows)
+int64_t tat_fused_bwd_part_rows(int64_t BFT);  // ... + its level-2 ticket-tree rows: one slab's rows
 int op_tat_fused_fwd(const TatFusedArgs& a, hipStream_t st);
 struct TatFusedBwdArgs {
   const float* dO = nullptr;  // O's [(f,t)][(b,n)] order

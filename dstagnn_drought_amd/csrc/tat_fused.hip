@@ -989,11 +989,19 @@ bool tat_fused_fwd_ok(int N, int T, int h, int dk, int dv) {
   // DSTAGNN_TAT_FUSED=0 (or DSTAGNN_TAT_MFMA=0, the VALU attention A/B): the unfused launches
   static const bool env = (!getenv("DSTAGNN_TAT_FUSED") || atoi(getenv("DSTAGNN_TAT_FUSED")) != 0) &&
                           (!getenv("DSTAGNN_TAT_MFMA") || atoi(getenv("DSTAGNN_TAT_MFMA")) != 0);
-  return env && h == kTfH && dk == kTfD && dv == kTfD && N >= 1 && N <= kTfNmax &&
-         (T == 4 || T == 8 || T == 12 || T == 16);
+  // (T >= 7 for any block — check_dims — so of the 48-row tilings only T = 8, 12, 16 occur)
+  return env && h == kTfH && dk == kTfD && dv == kTfD && N >= 1 && N <= kTfNmax && (T == 8 || T == 12 || T == 16);
 }
 
 int tat_fused_np(int N) { return (N + 15) / 16 * 16; }
+
+// the backward's grid (one gamma / beta partial row per workgroup) and the rows of its two-level
+// ticket tree (level-1 rows, then one level-2 row per kTfG1 workgroups): the caller's slab layout
+int64_t tat_fused_bwd_wgs(int64_t BFT) { return cdiv64(BFT, kTfRows); }
+int64_t tat_fused_bwd_part_rows(int64_t BFT) {
+  const int64_t nwg = tat_fused_bwd_wgs(BFT);
+  return nwg + cdiv64(nwg, kTfG1);
+}
 
 int op_tat_fused_fwd(const TatFusedArgs& a0, hipStream_t st) {
   if (!tat_fused_fwd_ok(a0.N, a0.T, a0.h, kTfD, kTfD) || a0.NP != tat_fused_np(a0.N) || a0.BFT % a0.T != 0) {
@@ -1023,7 +1031,6 @@ int op_tat_fused_fwd(const TatFusedArgs& a0, hipStream_t st) {
   }                                                       \
   break;
   switch (a.T) {
-    case 4: TF_T(4)
     case 8: TF_T(8)
     case 12: TF_T(12)
     default: TF_T(16)
@@ -1062,7 +1069,7 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
   }
   TatFusedBwdArgs a = a0;
   if (a.res_mode == DSTAGNN_RES_BCAST && !a.dres) a.res_mode = DSTAGNN_RES_NONE;  // nothing to fold
-  const int64_t nwg = cdiv64(a.BFT, kTfRows);
+  const int64_t nwg = tat_fused_bwd_wgs(a.BFT);
   a.B = (int)(a.BFT / a.FT);
   a.ln_fold = a.ln_fold && a.gpart && a.bpart && (a.gout || a.bout);
   if (a.res_mode == DSTAGNN_RES_BCAST || a.ln_fold) {
@@ -1094,7 +1101,6 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
   }                                                       \
   break;
   switch (a.T) {
-    case 4: TB_T(4)
     case 8: TB_T(8)
     case 12: TB_T(12)
     default: TB_T(16)

@@ -428,6 +428,15 @@ Tensor block_cheb_out(const Tensor& x, const c10::optional<Tensor>& res, at::Ten
   return block_relu_out(x, res, params, slots, graph, cfg, drop_p, seed, flags, 0);
 }
 
+// the kernel path (DSTAGNN_PATH_* bits) the block takes for this call's dims: launches nothing
+int64_t block_paths(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params, at::IntArrayRef slots,
+                    at::TensorList graph, at::IntArrayRef cfg, double drop_p, int64_t seed, int64_t flags) {
+  BlockCall c = make_call(x, res, params, slots, graph, cfg, drop_p, seed, flags);
+  uint32_t bits = 0;
+  check_rc(dstagnn_block_paths(&c.d, &bits), "dstagnn_block_paths");
+  return (int64_t)bits;
+}
+
 // HIP-event timing of one block stage (dstagnn_block_time_stage) after one forward:
 // mean milliseconds per launch on the current stream
 double block_time_stage(const Tensor& x, const c10::optional<Tensor>& res, at::TensorList params,
@@ -851,6 +860,7 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("block_time_stage(" DSTAGNN_BLK_ARGS ", int stage, int iters) -> float");
   m.def("block_cheb_out(" DSTAGNN_BLK_ARGS ") -> Tensor");
   m.def("block_relu_out(" DSTAGNN_BLK_ARGS ", int which) -> Tensor");
+  m.def("block_paths(" DSTAGNN_BLK_ARGS ") -> int");
 #undef DSTAGNN_BLK_ARGS
   m.def("dropout_masks(Tensor like, int[] shape, int[] cfg, float drop_p, int seed, int sample_base=0) -> (Tensor, Tensor)");
   m.def("cheb_sat_fwd(Tensor x, Tensor sat, Tensor theta_cat, Tensor mask_cat, Tensor[] graph, int C, bool sparse) "
@@ -887,6 +897,7 @@ TORCH_LIBRARY_IMPL(dstagnn, CUDA, m) {
   m.impl("dropout_masks", dropout_masks);
   m.impl("block_cheb_out", block_cheb_out);
   m.impl("block_relu_out", block_relu_out);
+  m.impl("block_paths", block_paths);
   m.impl("cheb_sat_fwd", cheb_sat_fwd);
   m.impl("cheb_sat_bwd", cheb_sat_bwd);
   m.impl("gemm_f32", gemm_f32);

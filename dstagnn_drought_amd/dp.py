@@ -30,7 +30,9 @@ def shard_batch(t, rank, world, model=None):
     """Disjoint contiguous slice of the leading (batch) dim for `rank` (ceil(B/world) samples per
     rank, the last shard shorter).  With `model`, its blocks' dropout sample base is set to the
     shard's true global offset (model.set_sample_base): the default base, rank * local_B, is
-    right only for equal shards (B=5 over 2 ranks: rank 1 starts at 3, not 2)."""
+    right only for equal shards (B=5 over 2 ranks: rank 1 starts at 3, not 2).  That base is
+    STICKY: it holds for every later call of the model until reset — pass `model` on every
+    sharded call, or use `sharded(...)` below, which restores the previous base on exit."""
     B = t.shape[0]
     per = (B + world - 1) // world
     start = shard_start(B, rank, world)
@@ -38,6 +40,26 @@ def shard_batch(t, rank, world, model=None):
         from .model import set_sample_base
         set_sample_base(model, start)
     return t[start:min(B, (rank + 1) * per)]
+
+
+class sharded:
+    """``with dp.sharded(x, rank, world, model) as xs:`` — shard_batch with the model's dropout
+    sample base set to the shard's global offset for the block only; on exit every block's
+    previous base comes back (None: the default rank * B), so a later full-batch or differently
+    sharded call cannot key its masks from a stale offset."""
+
+    def __init__(self, t, rank, world, model):
+        self.t, self.rank, self.world, self.model = t, rank, world, model
+
+    def __enter__(self):
+        from .model import DSTAGNN_block
+        self._saved = [(m, m.sample_base) for m in self.model.modules() if isinstance(m, DSTAGNN_block)]
+        return shard_batch(self.t, self.rank, self.world, model=self.model)
+
+    def __exit__(self, *exc):
+        for m, base in self._saved:
+            m.sample_base = base
+        return False
 
 
 class GradAllReducer:

@@ -75,8 +75,14 @@ def _reducer_for(optimizer):
 
 
 def reduce_gradients(optimizer, groups=None, pin_layout=True):
-    """Mean all-reduce of the optimiser's gradients over the replicas (no-op at world 1)."""
-    if xrt_world_size() > 1 and _dist_on():
+    """Mean all-reduce of the optimiser's gradients over the replicas (no-op at world 1).  With
+    WORLD_SIZE > 1 but no process group (xla_device() not called first, or called before the
+    launcher's environment was set) this raises: the replicas would otherwise step on their own
+    unreduced gradients and drift apart silently."""
+    if xrt_world_size() > 1:
+        if not _dist_on():
+            raise RuntimeError("xm.optimizer_step / reduce_gradients: WORLD_SIZE > 1 but the process group is not "
+                               "initialised (call xm.xla_device() first, as train_DSTAGNN_my.py:33 does)")
         _reducer_for(optimizer).all_reduce()
 
 
@@ -128,9 +134,11 @@ def _to_cpu(data):
 
 def save(data, file_or_path, master_only=True, global_master=False):
     """xm.save: tensors moved to the CPU, written by the master ordinal only (torch.save format;
-    the reference reloads it with torch.load, :184)."""
+    the reference reloads it with torch.load, :184).  No collective: the reference calls save
+    from inside `if xm.is_master_ordinal():` (train_DSTAGNN_my.py:173-180), so a barrier here
+    would pair the master's barrier with the other ranks' next gradient all-reduce (a hang, or a
+    mismatched RCCL collective).  Callers that need the file visible to every rank
+    synchronise themselves (xm.rendezvous)."""
     master = is_master_ordinal(local=not global_master)
     if master or not master_only:
         torch.save(_to_cpu(data), file_or_path)
-    if _dist_on():
-        dist.barrier()

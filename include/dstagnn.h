@@ -168,6 +168,22 @@ int dstagnn_block_forward(const dstagnn_block_dims* d, const dstagnn_block_param
  * layout (B,N,C,T) (:245/:247); 2: ReLU(residual + tco), layout (B,N,C,T) (:252). */
 int dstagnn_block_save_offset(const dstagnn_block_dims* d, int which, size_t* offset_bytes, size_t* count);
 
+/* Introspection for parity tests: the kernel path the block takes for these dims (and this
+ * process's DSTAGNN_* environment knobs) as a bit set — so a test can assert that the kernels it
+ * holds to the oracle are the ones that ran.  Pure function of its inputs; launches nothing. */
+enum {
+  DSTAGNN_PATH_SPARSE = 1,          /* cheb_conv_withSAt over the CSC/CSR union support          */
+  DSTAGNN_PATH_FLASH = 2,           /* fused Chebyshev attention (cheb_flash.hip)                */
+  DSTAGNN_PATH_FLASH_SMALL = 4,     /* ... its LDS-staged small-graph kernels (N <= 512)         */
+  DSTAGNN_PATH_CHEB_AGG = 8,        /* aggregate-first Chebyshev aggregation (cheb_agg.hip)      */
+  DSTAGNN_PATH_TAT_FUSED_FWD = 16,  /* temporal attention stage as one kernel (tat_fused.hip)    */
+  DSTAGNN_PATH_TAT_FUSED_BWD = 32,  /* ... and its backward                                      */
+  DSTAGNN_PATH_GTU_FUSED_FWD = 64,  /* GTU stage as one kernel (gtu_fused.hip)                   */
+  DSTAGNN_PATH_GTU_FUSED_BWD = 128, /* ... and its backward                                      */
+  DSTAGNN_PATH_SAT_LN_FUSED = 256   /* SAt projection bwd + EmbedS LN bwd fused (sat_fused.hip)  */
+};
+int dstagnn_block_paths(const dstagnn_block_dims* d, uint32_t* bits);
+
 /* Autograd backward of the block (replaces torch autograd over :225-253).
  *   d_out (B,N,C,T); d_re_at (B,F,h,T,T) or NULL (no gradient flows into re_At)
  *   d_x (B,N,F,T) written; d_res_att written per res_mode (NULL for mode 0)

@@ -187,20 +187,23 @@ def test_block_golden(golden_dir, name):
     """The block against the reference's own outputs and gradients (tests/golden/gen_golden.py,
     gen_golden_prod.py).  g13 / g14 are at the production geometry (N=170, F=C=32, T=12, K=3,
     d_k=32): the default path there is the one bench.py times — flash_small_* (fused small-graph
-    attention), cheb_agg_* (aggregate-first Chebyshev), gtu_tail_*_ct (C=32 / T=12 GTU tail) —
-    asserted below, so the timed kernels are pinned to reference-written vectors directly."""
+    attention), cheb_agg_* (aggregate-first Chebyshev), tat_fused_* (the temporal-attention stage
+    as one kernel per direction), gtu_*_fused (the GTU stage as one kernel per direction) —
+    asserted below through the library's own path query (dstagnn_block_paths), so the timed
+    kernels are pinned to reference-written vectors directly."""
     _need_gpu()
     from dstagnn_drought_amd import block_fn as bf
     g = load(golden_dir, name)
     m = json.loads(str(g["meta"]))
     blk = _block_from_golden(g, m, m["num_of_d"])
-    if "_prod" in name:
-        graph = blk._graph()
-        meta = dict(blk.meta)
-        assert bf.use_sparse(graph, meta, m["T"]) and bf.use_flash(graph, meta, m["T"], None, m["B"])
-        assert m["N"] <= bf.FLASH_SMALL_N and m["C"] == 32 and m["T"] == 12 and m["d_k"] == 32
     x = torch.from_numpy(g["x"]).cuda().requires_grad_(True)
     res = torch.from_numpy(g["res_att"]).cuda().requires_grad_(True) if "res_att" in g else 0
+    if "_prod" in name:
+        assert m["N"] <= bf.FLASH_SMALL_N and m["C"] == 32 and m["T"] == 12 and m["d_k"] == 32
+        took = bf.block_paths(blk, x, res)
+        want = {"sparse", "flash", "flash_small", "cheb_agg", "tat_fused_fwd", "tat_fused_bwd", "gtu_fused_fwd",
+                "gtu_fused_bwd"}
+        assert want <= took, f"{name}: kernel path {sorted(took)} lacks {sorted(want - took)}"
     out, re_at = blk(x, res)
     close(out, g["out"], what="out")
     close(re_at, g["re_at"], what="re_at")
@@ -370,6 +373,13 @@ CONFIGS = {
     # T = 8 / 16 with d_k = 32: the other tile fills of the matrix-core TAt kernels (T = 12 above)
     "t8": (40, 8, 3, 2, 64, 32, 32),
     "t16": (40, 16, 3, 2, 64, 32, 32),
+    # h = 3, d_k = 32 at every T the fused temporal-attention kernels admit (tat_fused.hip: the
+    # 48-row tile holds 48 / T problems), plus their LDS bound N = 320 and an odd N (no float2 /
+    # float4 row loads, a partial 16-node tile)
+    "t8h3": (40, 8, 3, 3, 64, 32, 32),
+    "t16h3": (40, 16, 3, 3, 64, 32, 32),
+    "n320": (320, 12, 3, 3, 64, 32, 32),
+    "n101": (101, 12, 3, 3, 64, 32, 32),
 }
 RELU_EPS = 1e-5  # ReLU decisions may differ from the fp64 oracle's only where |z| <= RELU_EPS * max|z|
 
@@ -446,11 +456,15 @@ def _train_seed():
 
 
 def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=RELU_EPS, errs=None, normwise=False,
-                          train=False, owns=None):
+                          train=False, owns=None, res_kind=None, paths=None):
+    """paths: a set of block_fn.PATH_BITS names the library must take for this case (asserted
+    before the comparison), or a (must, must_not) pair of sets."""
     import dstagnn_drought_amd as D_
-    from dstagnn_drought_amd.block_fn import dropout_masks
+    from dstagnn_drought_amd.block_fn import dropout_masks, block_paths
     N, T, K, h, D, dk, C = CONFIGS[name]
-    ref, p, x, res, cheb, apa, dims, gen = _oracle_case(B, N, T, K, h, D, dk, C, first, 0 if first else 1, seed=seed)
+    if res_kind is None:
+        res_kind = 0 if first else 1
+    ref, p, x, res, cheb, apa, dims, gen = _oracle_case(B, N, T, K, h, D, dk, C, first, res_kind, seed=seed)
     g_out = torch.randn(B, N, C, T, generator=gen)
     g_re = torch.randn(B, x.shape[2], h, T, T, generator=gen)
     F = x.shape[2]
@@ -460,6 +474,11 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
     blk.flash_cheb = flash
     xg = x.cuda().requires_grad_(True)
     rg = res.cuda().requires_grad_(True) if torch.is_tensor(res) else 0
+    if paths is not None:
+        must, must_not = paths if isinstance(paths, tuple) else (paths, set())
+        took = block_paths(blk, xg, rg, train=train)
+        assert must <= took and not (must_not & took), f"{name}: kernel path {sorted(took)}, expected " \
+                                                       f"{sorted(must)} and none of {sorted(must_not)}"
     dseed = _train_seed() if train else 0
     dm = None
     if train:
@@ -539,6 +558,33 @@ def test_block_vs_oracle_configs(name, first, B, flash):
     _need_gpu()
     flips = _run_config_vs_oracle(name, first, B, flash=flash)
     print(f"{name} B={B} flash={flash}: {flips} ReLU decision(s) within rounding of 0")
+
+
+TF_FWD, TF_BWD = "tat_fused_fwd", "tat_fused_bwd"
+
+
+@pytest.mark.parametrize("name,first,res_kind,B,train,fwd,bwd", [
+    # T = 8 / 16 (the other row tilings of the 48-row tile: 6 / 3 problems per workgroup)
+    ("t8h3", True, 0, 2, False, True, True), ("t8h3", False, 2, 2, False, True, True),
+    ("t8h3", False, 2, 3, True, True, True), ("t8h3", True, 0, 7, True, True, True),
+    ("t16h3", True, 0, 2, False, True, True), ("t16h3", False, 2, 2, False, True, True),
+    ("t16h3", False, 2, 3, True, True, True), ("t16h3", True, 0, 4, True, True, True),
+    # broadcast res_att at T = 8 / 16: F T is not a multiple of 48, so the in-kernel res_att fold
+    # cannot own whole samples — fused forward, unfused backward (the mixed pairing)
+    ("t8h3", False, 1, 2, False, True, False), ("t16h3", False, 1, 2, True, True, False),
+    # T = 12 at the LDS bound N = 320 and at an odd N (scalar row loads, partial node tile)
+    ("n320", False, 1, 2, False, True, True), ("n320", True, 0, 2, True, True, True),
+    ("n101", False, 1, 2, False, True, True), ("n101", False, 2, 2, True, True, True),
+    ("n101", True, 0, 3, False, True, True)])
+def test_tat_fused_variants_vs_oracle(name, first, res_kind, B, train, fwd, bwd):
+    """every fused temporal-attention instantiation the gate admits
+    (tat_fused_fwd_ok: h = 3, d_k = 32, T in {8, 12, 16}, N <= 320) held to the fp64 oracle,
+    first and inner block, eval and train, with the path asserted (block_fn.block_paths)."""
+    _need_gpu()
+    must = ({TF_FWD} if fwd else set()) | ({TF_BWD} if bwd else set())
+    must_not = set() if bwd else {TF_BWD}
+    flips = _run_config_vs_oracle(name, first, B, train=train, res_kind=res_kind, paths=(must, must_not))
+    print(f"{name} first={first} res={res_kind} B={B} train={train}: {flips} ReLU decision(s) within rounding of 0")
 
 
 @pytest.mark.parametrize("name,first,B,flash", [("pems08", False, 32, None), ("pems08", True, 32, None),

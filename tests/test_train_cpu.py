@@ -206,3 +206,26 @@ def test_shard_batch_sets_true_sample_base():
     part = shard_batch(t, 1, 2, model=blk)
     assert part.tolist() == [3, 4] and blk.sample_base == 3
     assert shard_batch(t, 0, 2, model=blk).tolist() == [0, 1, 2] and blk.sample_base == 0
+
+
+def test_sharded_scope_restores_default_sample_base():
+    """dp.sharded sets the shard's base for the block only and restores the previous
+    base (None: the default rank * B) on exit, exceptions included."""
+    from dstagnn_drought_amd.dp import sharded
+
+    from dstagnn_drought_amd import model as M
+    blk = M.DSTAGNN_block.__new__(M.DSTAGNN_block)
+    nn.Module.__init__(blk)
+    blk.sample_base = None
+    t = torch.arange(5)
+    with sharded(t, 1, 2, blk) as part:
+        assert part.tolist() == [3, 4] and blk.sample_base == 3
+    assert blk.sample_base is None
+    blk.sample_base = 7
+    try:
+        with sharded(t, 0, 2, blk):
+            assert blk.sample_base == 0
+            raise KeyError("x")
+    except KeyError:
+        pass
+    assert blk.sample_base == 7

@@ -2,7 +2,8 @@
 train_DSTAGNN_my.py:16-18, :25, :33, :113-115, :127, :148-161, :180, :195-197) on CPU: the
 reference's import lines resolve, the world-1 calls behave as torch_xla's, xla_device refuses
 a machine without a HIP device (no CPU fallback), and xmp.spawn + xm.optimizer_step form the
-data-parallel step over gloo (world 2: the reduced gradients are the mean).  The HIP-device
+data-parallel step over gloo (world 2: the reduced gradients are the mean, a master-only xm.save
+between steps as the reference does it, an unreduced step refused).  The HIP-device
 loop is tests/test_gpu_xla_adapter.py.  Subprocesses keep the top-level names out of the
 other tests."""
 import os
@@ -60,17 +61,28 @@ import torch_xla.distributed.xla_multiprocessing as xmp
 OUT = sys.argv[1]
 
 def fn(index, out):
-    dist.init_process_group("gloo")  # (on a GPU box xm.xla_device() does this on RCCL)
-    assert xm.xrt_world_size() == 2 and xm.get_ordinal() == index
     torch.manual_seed(0)
     lin = torch.nn.Linear(3, 1, bias=False)
     opt = torch.optim.SGD(lin.parameters(), lr=1.0)
+    try:  # WORLD_SIZE = 2 without a process group: the all-reduce must not be skipped silently
+        xm.optimizer_step(opt)
+        raise SystemExit("optimizer_step without a process group must raise")
+    except RuntimeError as e:
+        assert "not initialised" in str(e), e
+    dist.init_process_group("gloo")  # (on a GPU box xm.xla_device() does this on RCCL)
+    assert xm.xrt_world_size() == 2 and xm.get_ordinal() == index
     x = torch.full((1, 3), float(index + 1))   # rank 0: ones, rank 1: twos
-    lin(x).sum().backward()                     # grad = x
-    w0 = lin.weight.detach().clone()
-    xm.optimizer_step(opt)                      # mean all-reduce + step
+    deltas = []
+    for epoch in range(2):
+        opt.zero_grad()
+        lin(x).sum().backward()                     # grad = x
+        w0 = lin.weight.detach().clone()
+        xm.optimizer_step(opt)                      # mean all-reduce + step
+        deltas.append((w0 - lin.weight.detach()).tolist())
+        if xm.is_master_ordinal():                  # train_DSTAGNN_my.py:173-180: master-only save
+            xm.save(lin.state_dict(), os.path.join(out, f"epoch_{epoch}.params"))
     with open(os.path.join(out, f"r{index}.json"), "w") as f:
-        json.dump({"grad": lin.weight.grad.tolist(), "delta": (w0 - lin.weight.detach()).tolist()}, f)
+        json.dump({"grad": lin.weight.grad.tolist(), "delta": deltas}, f)
 
 if __name__ == "__main__":
     xmp.spawn(fn, args=(OUT,), nprocs=2, start_method="fork")
@@ -97,5 +109,7 @@ def test_xmp_spawn_optimizer_step_means_gradients(tmp_path):
     r = _run(SPAWN, str(tmp_path))
     assert r.returncode == 0 and "SPAWN_OK" in r.stdout, r.stderr[-3000:]
     recs = [json.loads((tmp_path / f"r{i}.json").read_text()) for i in (0, 1)]
-    for rec in recs:  # mean of ones and twos
-        assert rec["grad"] == [[1.5, 1.5, 1.5]] and rec["delta"] == [[1.5, 1.5, 1.5]], rec
+    for rec in recs:  # mean of ones and twos, in both epochs (the master's save between them is no collective)
+        assert rec["grad"] == [[1.5, 1.5, 1.5]], rec
+        assert all(abs(v - 1.5) < 1e-6 for d in rec["delta"] for v in d[0]) and len(rec["delta"]) == 2, rec
+    assert (tmp_path / "epoch_0.params").exists() and (tmp_path / "epoch_1.params").exists()
