@@ -21,7 +21,10 @@ EXT_LIBS := -L$(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip \
 # objects with block.o rebuilt under -DDSTAGNN_RACEBUG_NOFORK (never loaded by the package)
 RACEBUG := abtest/racebug/libdstagnn.so
 
-all: $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib $(RACEBUG)
+# hipcc-built host program driving the block through the C-ABI alone (tests/test_gpu_native_abi.py)
+ABI_TEST := tests/native/block_abi_test
+
+all: $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib $(RACEBUG) $(ABI_TEST)
 
 racebug: $(RACEBUG)
 
@@ -56,6 +59,9 @@ $(EXT): dstagnn_drought_amd/csrc/torch_ops.cpp include/dstagnn.h $(LIB)
 	$(HIPCC) $(EXT_FLAGS) -x c++ -c $< -o build/torch_ops.o
 	$(HIPCC) -shared -o $@ build/torch_ops.o $(EXT_LIBS)
 
+$(ABI_TEST): tests/native/block_abi_main.cpp include/dstagnn.h $(LIB)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Ldstagnn_drought_amd -ldstagnn -Wl,-rpath,'$$ORIGIN/../../dstagnn_drought_amd'
+
 $(EMD_HOST): tests/native/emd_host.cpp dstagnn_drought_amd/csrc/emd_simplex.hpp
 	g++ -O2 -std=c++17 -fPIC -shared -Wall -o $@ $<
 
@@ -67,6 +73,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 clean:
-	rm -rf build $(LIB) $(EXT) $(EMD_HOST) tools/fetch_calib abtest/racebug abtest/tftime
+	rm -rf build $(LIB) $(EXT) $(EMD_HOST) $(ABI_TEST) tools/fetch_calib abtest/racebug abtest/tftime
 
 .PHONY: all clean racebug tftime

@@ -802,7 +802,14 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     for (int r = 0; r < 4; ++r) {
       const int ii = 4 * q + r;
       if (ii >= T) continue;
-      float* row = Qp + ii * kTfLQ + c;
+      // the row offset made opaque to the compiler: at T = 16 (no predicate on these stores) the
+      // AMDGPU backend (ROCm 7.2 clang 22) merged the four rows' stores into rebased ds_write2
+      // pairs and encoded the dQ column-c store of row 4q+2 at +61 floats instead of +292 —
+      // writing into another head's Q columns (tests/test_gpu_parity.py t16h3 cases).  With an
+      // opaque per-row base every store's offset is <= 208 floats from it: no rebasing.
+      int off = ii * kTfLQ + c;
+      asm volatile("" : "+v"(off));
+      float* row = Qp + off;
       row[0] = gq0[r] * a.scale;
       row[16] = gq1[r] * a.scale;
       row[kTfHV] = gk0[r] * a.scale;
