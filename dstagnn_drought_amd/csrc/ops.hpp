@@ -303,6 +303,7 @@ struct TatFusedBwdArgs {
   int B = 0;  // (set by the launcher)
   float scale = 1.f;
   uint32_t* sig = nullptr; uint32_t sig_v = 0;
+  FastDiv fdN, fdH2, fdFT;  // (set by the launcher) magic divisions by N, N / 2, FT
 };
 bool tat_fused_bwd_ok(int N, int T, int h, int dk, int dv, int F, int res_mode);
 int op_tat_fused_bwd(const TatFusedBwdArgs& a, hipStream_t st);

@@ -128,27 +128,32 @@ __device__ __forceinline__ void tf_mma(floatx4 (&acc)[3][NJ], const float4 (&av)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[mt][j] = mf16(f4at(av[mt], s), f4at(bq[j], s), acc[mt][j]);
 }
-template <int NJ>
+// B fragments come from L2 (the re-laid weights): with one chunk of look-ahead every chunk waited
+// a full L2 round trip (the products ran at ~1/3 of the CU's MFMA rate, -DDSTAGNN_TF_TIMING).  A
+// ring of DB chunks keeps DB - 1 chunks of B loads in flight; A (LDS) is double-buffered.  Chunk
+// indices past NC are clamped (the redundant loads hit L2) and their products skipped.
+#ifndef DSTAGNN_TF_DB
+#define DSTAGNN_TF_DB 4  // (-DDSTAGNN_TF_DB=2: one chunk of look-ahead, the round-5 pipeline; A/B builds)
+#endif
+template <int NJ, int DB = DSTAGNN_TF_DB>
 __device__ __forceinline__ void tf_gemm_rows48(floatx4 (&acc)[3][NJ], const float* A, int LA, int NC, int i, int q,
                                                const float* const (&wp)[NJ]) {
-  float4 b0[NJ], b1[NJ], a0[3], a1[3];
-  tf_ld_b(b0, wp, 0);
-  tf_ld_a(a0, A, LA, 0, i, q);
-  int c = 0;
-  for (; c + 1 < NC; c += 2) {
-    tf_ld_b(b1, wp, 16 * (c + 1));
-    tf_ld_a(a1, A, LA, c + 1, i, q);
-    __builtin_amdgcn_sched_barrier(0);
-    tf_mma(acc, a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    const int cn = min(c + 2, NC - 1);
-    tf_ld_b(b0, wp, 16 * cn);
-    tf_ld_a(a0, A, LA, cn, i, q);
-    __builtin_amdgcn_sched_barrier(0);
-    tf_mma(acc, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
+  static_assert(DB % 2 == 0 && DB >= 2, "even ring: the A ping-pong slot is d % 2");
+  float4 b[DB][NJ], av[2][3];
+#pragma unroll
+  for (int d = 0; d < DB - 1; ++d) tf_ld_b(b[d], wp, 16 * min(d, NC - 1));
+  tf_ld_a(av[0], A, LA, 0, i, q);
+  for (int c0 = 0; c0 < NC; c0 += DB) {
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      const int c = c0 + d;
+      tf_ld_b(b[(d + DB - 1) % DB], wp, 16 * min(c + DB - 1, NC - 1));
+      tf_ld_a(av[(d + 1) % 2], A, LA, min(c + 1, NC - 1), i, q);
+      __builtin_amdgcn_sched_barrier(0);
+      if (c < NC) tf_mma(acc, av[d % 2], b[d]);  // (wave-uniform)
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
-  if (c < NC) tf_mma(acc, a0, b0);
 }
 
 // E tile (48 x NP, zero-padded) into LDS, every load of a thread issued before its first LDS
@@ -500,70 +505,34 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   TF_DECL;
   TF_MARK(0);
 
-  // ---- A0. every load of the first phases in one round, in order of use — the LayerNorm's
-  // u block (contiguous: float4) and dO rows (float2) into LDS, the softmax and d re_At of the
-  // wave's attention tasks, the Q|K|V rows (to LDS after the LayerNorm) — wide loads: with
-  // dword loads the 63-deep vmcnt queue held ~16 KB per wave in flight, latency-bound (23 us)
+  // ---- A0. every load of the first phases in ONE round, before any LDS store — the LayerNorm's
+  // u block (contiguous: float4) and dO rows (float2), the LayerNorm statistics, the softmax and
+  // d re_At of the wave's attention tasks, the Q|K|V rows (to LDS after the LayerNorm).  (With
+  // each group's LDS stores between the groups, the scheduler kept the program order and the
+  // phase paid three HBM round trips: 15-20 us of the kernel's ~50, -DDSTAGNN_TF_TIMING.)
+  // Native vector types throughout: HIP's float4 struct copies become memcpys that pin a
+  // staging array in scratch.
+  typedef float tf_f2 __attribute__((ext_vector_type(2)));
   float* Us = Qs;  // [48][LE] u (the Q|K|V + ctx regions, free until after the LayerNorm)
-  {
-    const int tot = nrows * N;
-    const float* gu = a.u + R0 * N;
-    constexpr int UV = 12;  // float4 per thread: 48 x 320 / 4 / 256 = 15 max -> two rounds at most
-    if ((tot & 3) == 0) {
-      for (int e0 = 0; e0 < tot / 4; e0 += 256 * UV) {
-        float4 v[UV];
+  constexpr int UV = 3 * NTW;  // float4 of u per thread: 48 N / 4 / 256 <= 3 NTW (one round)
+  constexpr int DV = 6 * NTW;  // float2 of dO per thread: 48 N / 2 / 256 <= 6 NTW
+  const int tot = nrows * N, h2 = N / 2, tot2 = nrows * h2;
+  const bool vec = (tot & 3) == 0 && (N & 1) == 0;  // else: dword loads (odd N), the slow path below
+  const float* gu = a.u + R0 * N;
+  floatx4 uv[UV];
+  tf_f2 dv[DV];
+  if (vec) {
 #pragma unroll
-        for (int u = 0; u < UV; ++u) v[u] = reinterpret_cast<const float4*>(gu)[min(e0 + u * 256 + tid, tot / 4 - 1)];
+    for (int u = 0; u < UV; ++u) uv[u] = reinterpret_cast<const floatx4*>(gu)[min(u * 256 + tid, tot / 4 - 1)];
 #pragma unroll
-        for (int u = 0; u < UV; ++u) {
-          const int e4 = e0 + u * 256 + tid;
-          if (e4 >= tot / 4) continue;
-          const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-          for (int z = 0; z < 4; ++z) {
-            const int e = 4 * e4 + z, r = e / N, n = e - r * N;
-            Us[r * LE + n] = vv[z];
-          }
-        }
-      }
-    } else {
-      for (int e = tid; e < tot; e += 256) {
-        const int r = e / N, n = e - r * N;
-        Us[r * LE + n] = gu[e];
-      }
-    }
-    const int h2 = N / 2;  // dO rows: float2 (row offsets are even when N is)
-    if ((N & 1) == 0) {
-      constexpr int DV = 16;
-      const int tot2 = nrows * h2;
-      for (int e0 = 0; e0 < tot2; e0 += 256 * DV) {
-        float2 v[DV];
-#pragma unroll
-        for (int u = 0; u < DV; ++u) {
-          const int e = min(e0 + u * 256 + tid, tot2 - 1), r = e / h2, c2 = e - r * h2;
-          const int64_t R = R0 + r;
-          const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
-          v[u] = *reinterpret_cast<const float2*>(a.dO + (int64_t)ft * a.BN + (int64_t)bb * N + 2 * c2);
-        }
-#pragma unroll
-        for (int u = 0; u < DV; ++u) {
-          const int e = e0 + u * 256 + tid;
-          if (e >= tot2) continue;
-          const int r = e / h2, c2 = e - r * h2;
-          DUs[r * LE + 2 * c2] = v[u].x;
-          DUs[r * LE + 2 * c2 + 1] = v[u].y;
-        }
-      }
-    } else {
-      for (int e = tid; e < nrows * N; e += 256) {
-        const int r = e / N, n = e - r * N;
-        const int64_t R = R0 + r;
-        const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
-        DUs[r * LE + n] = a.dO[(int64_t)ft * a.BN + (int64_t)bb * N + n];
-      }
+    for (int u = 0; u < DV; ++u) {  // (magic divisions: runtime-divisor ones cost ~40 VALU each)
+      const int e = min(u * 256 + tid, tot2 - 1), r = (int)fdiv((uint32_t)e, a.fdH2), c2 = e - r * h2;
+      const uint32_t R = (uint32_t)(R0 + r);
+      const uint32_t bb = fdiv(R, a.fdFT), ft = R - bb * (uint32_t)a.FT;
+      dv[u] = *reinterpret_cast<const tf_f2*>(a.dO + (int64_t)ft * a.BN + (int64_t)bb * N + 2 * c2);
     }
   }
-  // the LayerNorm statistics of the wave's rows (lane k < 12: row w + 4k) and gamma, early
+  // the LayerNorm statistics of the wave's rows (lane k < 12: row w + 4k) and gamma
   float mu_l, rs_l, gl[NTW];
   {
     const int64_t R = R0 + min(w + 4 * min(l, kTfRPW - 1), nrows - 1);
@@ -587,12 +556,41 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
   constexpr int QV4 = kTfRows * kTfQW / 4 / 256;  // 13.5 -> 14 float4 per thread
-  float4 qv[QV4 + 1];
+  floatx4 qv[QV4 + 1];
   {
-    const float4* gq = reinterpret_cast<const float4*>(a.qkv + R0 * kTfQW);
-    const int tot = nrows * (kTfQW / 4);
+    const floatx4* gq = reinterpret_cast<const floatx4*>(a.qkv + R0 * kTfQW);
+    const int totq = nrows * (kTfQW / 4);
 #pragma unroll
-    for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * 256 + tid, tot - 1)];
+    for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * 256 + tid, totq - 1)];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // (every load above is issued before the first LDS store)
+  if (vec) {
+#pragma unroll
+    for (int u = 0; u < UV; ++u) {
+      const int e4 = u * 256 + tid;
+      if (e4 >= tot / 4) continue;
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int e = 4 * e4 + z, r = (int)fdiv((uint32_t)e, a.fdN), n = e - r * N;
+        Us[r * LE + n] = uv[u][z];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DV; ++u) {
+      const int e = u * 256 + tid;
+      if (e >= tot2) continue;
+      const int r = (int)fdiv((uint32_t)e, a.fdH2), c2 = e - r * h2;
+      DUs[r * LE + 2 * c2] = dv[u][0];
+      DUs[r * LE + 2 * c2 + 1] = dv[u][1];
+    }
+  } else {
+    for (int e = tid; e < tot; e += 256) {
+      const int r = e / N, n = e - r * N;
+      Us[r * LE + n] = gu[e];
+      const int64_t R = R0 + r;
+      const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
+      DUs[r * LE + n] = a.dO[(int64_t)ft * a.BN + (int64_t)bb * N + n];
+    }
   }
   __syncthreads();  // the u / dO tiles
   TF_MARK(1);
@@ -657,7 +655,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       const int e = u * 256 + tid;
       if (e < tot) {
         const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
-        *reinterpret_cast<float4*>(Qs + r * kTfLQ + 4 * c4) = qv[u];
+        *reinterpret_cast<floatx4*>(Qs + r * kTfLQ + 4 * c4) = qv[u];
       }
     }
   }
@@ -716,7 +714,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt) {
         const int64_t R = R0 + min(mt * 16 + 4 * q, nrows - 4);
-        const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
+        const uint32_t bb = fdiv((uint32_t)R, a.fdFT), ft = (uint32_t)R - bb * (uint32_t)a.FT;
         dxo[mt][j] = *reinterpret_cast<const float4*>(a.dx + (int64_t)bb * a.dxb + (int64_t)n * a.FT + ft);
       }
     }
@@ -847,7 +845,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
         for (int r = 0; r < 4; ++r) v[r] = acc[mt][j][r] + DUs[(r0 + r) * LE + n];
         const int64_t R = R0 + r0;
         if (a.dx) {  // inner block: rows R..R+3 are four consecutive ft of one b (FT % 4 == 0)
-          const uint32_t bb = (uint32_t)R / (uint32_t)a.FT, ft = (uint32_t)R - bb * (uint32_t)a.FT;
+          const uint32_t bb = fdiv((uint32_t)R, a.fdFT), ft = (uint32_t)R - bb * (uint32_t)a.FT;
           float4* dp = reinterpret_cast<float4*>(a.dx + (int64_t)bb * a.dxb + (int64_t)n * a.FT + ft);
           const float4 o = dxo[mt][j];
           *dp = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
@@ -868,7 +866,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       float vv[4];
 #pragma unroll
       for (int z = 0; z < 4; ++z) {
-        const int e = 4 * e4 + z, r = e / N, n = e - r * N;
+        const int e = 4 * e4 + z, r = (int)fdiv((uint32_t)e, a.fdN), n = e - r * N;
         vv[z] = DUs[r * LE + n];
       }
       g4[e4] = make_float4(vv[0], vv[1], vv[2], vv[3]);
@@ -1078,6 +1076,9 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
   if (a.res_mode == DSTAGNN_RES_BCAST && !a.dres) a.res_mode = DSTAGNN_RES_NONE;  // nothing to fold
   const int64_t nwg = tat_fused_bwd_wgs(a.BFT);
   a.B = (int)(a.BFT / a.FT);
+  a.fdN = make_fastdiv((uint32_t)a.N);
+  a.fdH2 = make_fastdiv((uint32_t)std::max(1, a.N / 2));
+  a.fdFT = make_fastdiv((uint32_t)a.FT);
   a.ln_fold = a.ln_fold && a.gpart && a.bpart && (a.gout || a.bout);
   if (a.res_mode == DSTAGNN_RES_BCAST || a.ln_fold) {
     // [B] res_att tickets, then the gamma / beta tree's [ng] level-1 tickets and one level-2 ticket
