@@ -706,7 +706,7 @@ __global__ __launch_bounds__(256) void flash_small_mask_kernel(ChebFl a) {
   }
   const int j = (int)(o % a.N), pt = a.apa2t[q];
   float s = 0.f;
-  constexpr int kBB = 8;  // batch elements per round of loads (fixed summation order)
+  constexpr int kBB = 8;  // batch elements per round of loads (fixed summation order; 32 measured no faster)
   for (int b0 = 0; b0 < a.B; b0 += kBB) {
     float dz[kBB], pp[kBB], cv[kBB];
 #pragma unroll

@@ -178,7 +178,12 @@ __device__ __forceinline__ float4 sk_fold_rows(const float* src, int nrows, int 
   return tot;
 }
 
-template <int MT, int NT, int U>  // 16-row / 16-column accumulator tiles, k-quads per load round
+// A4: A's k map takes every aligned quad of k to 4 contiguous, 16-B aligned floats (the
+// aggregate-first dTheta: A = agg[b,j,k,f,t], k = (b,j,t), T % 4 == 0) — each lane then loads
+// a float4 of A per 4 MFMA steps (contraction index 16 v + 4 q + s of round v, step s, lane
+// group q) instead of one dword per step: 4x fewer A load instructions and 16-B row pieces
+// instead of 4-B ones (was 26 us for the PEMS08 dTheta, ~1.3 TB/s).
+template <int MT, int NT, int U, bool A4 = false>  // 16-row / 16-column accumulator tiles, MFMA steps per load round
 __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
   constexpr int kS = MT > 2 ? 4 : 8;  // LDS fold slots (waves fold in 16 / kS rounds)
   static_assert(kS * MT * 16 * 33 >= 4096, "the final fold's 1024 float4 sums live in red");
@@ -202,7 +207,6 @@ __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
     ones[nt] = n == g.nload && g.nload < g.N;
     bo[nt] = (uint32_t)g.bbias + (bcol[nt] ? (uint32_t)koff(g.bn, n) : 0u);
   }
-  typedef float floatx4 __attribute__((ext_vector_type(4)));
   floatx4 acc[MT][NT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -210,15 +214,36 @@ __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
   for (int kb = k0; kb < k1; kb += 4 * U) {
     float av[U][MT], bv[U][NT];
+    if constexpr (A4) {
+      static_assert(U % 4 == 0, "rounds of 16 k");
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = kb + 4 * u + q4;
-      const bool ok = k < k1;
+      for (int v = 0; v < U / 4; ++v) {
+        const int kq = kb + 16 * v + 4 * q4;  // this lane's k quad (all valid or all past k1)
+        const bool ok = kq < k1;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) av[u][mt] = ok && arow[mt] ? g.A[ao[mt] + (uint32_t)koff(g.ak, k)] : 0.f;
+        for (int mt = 0; mt < MT; ++mt) {
+          const floatx4 x = ok && arow[mt] ? *reinterpret_cast<const floatx4*>(g.A + ao[mt] + (uint32_t)koff(g.ak, kq))
+                                           : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        bv[u][nt] = ok && bcol[nt] ? g.B[bo[nt] + (uint32_t)koff(g.bk, k)] : (ok && ones[nt] ? 1.f : 0.f);
+          for (int sq = 0; sq < 4; ++sq) av[4 * v + sq][mt] = x[sq];
+        }
+#pragma unroll
+        for (int sq = 0; sq < 4; ++sq)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            bv[4 * v + sq][nt] = ok && bcol[nt] ? g.B[bo[nt] + (uint32_t)koff(g.bk, kq + sq)] : (ok && ones[nt] ? 1.f : 0.f);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = kb + 4 * u + q4;
+        const bool ok = k < k1;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) av[u][mt] = ok && arow[mt] ? g.A[ao[mt] + (uint32_t)koff(g.ak, k)] : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          bv[u][nt] = ok && bcol[nt] ? g.B[bo[nt] + (uint32_t)koff(g.bk, k)] : (ok && ones[nt] ? 1.f : 0.f);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -289,11 +314,28 @@ __global__ __launch_bounds__(1024) void skinny_dw_kernel(SkinnyK s) {
   }
 }
 
+// A's k map sends every aligned k quad to 4 contiguous, 16-B aligned floats (skinny_dw_kernel A4)
+bool skinny_a4(const SkinnyK& s) {
+  static const bool on = !getenv("DSTAGNN_SKINNY_A4") || atoi(getenv("DSTAGNN_SKINNY_A4")) != 0;
+  const GemmK& g = s.g;
+  const bool quads = g.ak.s0 == 1 && (g.ak.d == 0x80000000u || g.ak.d % 4 == 0) && g.ak.s1 % 4 == 0;
+  bool rows = reinterpret_cast<uintptr_t>(g.A) % 16 == 0 && g.abias % 4 == 0 && g.K % 4 == 0 && s.kpw % 4 == 0;
+  for (int m = 0; m < g.M && rows; ++m) {  // every row's offset a multiple of 4 (host-side koff)
+    const uint32_t q = g.am.d == 0x80000000u ? 0u : (uint32_t)m / g.am.d, r = (uint32_t)m - q * g.am.d;
+    rows = ((int64_t)r * g.am.s0 + (int64_t)q * g.am.s1) % 4 == 0;
+  }
+  return on && quads && rows;
+}
+
 void launch_skinny(const SkinnyK& s, hipStream_t st) {
   const dim3 grid((unsigned)s.nwg), blk(64 * kSkWaves);
   const int mt = (s.g.M + 15) / 16, nt = s.g.N > 16 ? 2 : 1;
-#define SK_L(MT_, U_)                                                                       \
-  if (nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<MT_, 1, U_>), grid, blk, 0, st, s);   \
+  const bool a4 = skinny_a4(s);
+#define SK_L(MT_, U_)                                                                                       \
+  if (a4) {                                                                                                 \
+    if (nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<MT_, 1, U_, true>), grid, blk, 0, st, s);          \
+    else hipLaunchKernelGGL((skinny_dw_kernel<MT_, 2, U_, true>), grid, blk, 0, st, s);                  \
+  } else if (nt == 1) hipLaunchKernelGGL((skinny_dw_kernel<MT_, 1, U_>), grid, blk, 0, st, s);            \
   else hipLaunchKernelGGL((skinny_dw_kernel<MT_, 2, U_>), grid, blk, 0, st, s);
   if (mt == 1) { SK_L(1, 16) }
   else if (mt == 2) { SK_L(2, 16) }
