@@ -143,6 +143,56 @@ def load_pmc(stamp):
     return pmc
 
 
+FAM_FILE = "profiles/family_rocprof.json"
+PROF_KINDS = {0: "gemm_f32 (one call + split-K fold)", 1: "skinny_dw_kernel", 2: "tat_fused_fwd_kernel",
+              3: "tat_fused_bwd_kernel", 4: "gtu_fwd_fused_kernel", 5: "gtu_bwd_fused_kernel", 6: "gtu_tconv_kernel",
+              7: "sat_ln_bwd_fused_kernel"}
+
+
+def dominant_kernel(recs, steps):
+    """The single kernel (call site) with the most time per serialised step, from the per-call
+    HIP-event records of dstagnn::prof_records ([kind, flops, bytes, ms] * n, in issue order; a
+    call site = its position in the step): its own FLOP, bytes, duration and both roofline
+    fractions (reported beside the family)."""
+    groups = {}
+    n_rec = len(recs) // 4
+    per_step = max(1, n_rec // max(1, steps))  # the step's call sites in issue order (the same every step)
+    for i in range(0, 4 * n_rec, 4):
+        kind, fl, by, ms = int(recs[i]), recs[i + 1], recs[i + 2], recs[i + 3]
+        key = (kind, (i // 4) % per_step)
+        g = groups.setdefault(key, [0, 0.0, 0.0, 0.0])
+        g[0] += 1
+        g[1] += fl
+        g[2] += by
+        g[3] += ms
+    if not groups:
+        return None
+    (kind, _), (n, fl, by, ms) = max(groups.items(), key=lambda kv: kv[1][3])
+    tf = fl / (ms * 1e-3) / 1e12
+    gbs = by / (ms * 1e-3) / 1e9
+    return {"kernel": PROF_KINDS.get(kind, str(kind)), "launches_per_step": round(n / steps, 2),
+            "avg_launch_us": round(ms / n * 1e3, 3), "gflop_per_launch": round(fl / n / 1e9, 4),
+            "alg_mbytes_per_launch": round(by / n / 1e6, 3), "achieved_tflops": round(tf, 3),
+            "mfma_frac": round(tf / PEAK_FP32_TFLOPS, 4), "achieved_GBs": round(gbs, 1),
+            "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+            "bound": "mfma" if fl / max(by, 1.0) > PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9) else "hbm",
+            "timing": "HIP events around each launch on its stream, serialised steps (dstagnn::prof_records)"}
+
+
+def load_family_rocprof(stamp):
+    """profiles/family_rocprof.json (tools/step_kernels.py --json) when it measured this build."""
+    try:
+        with open(os.path.join(ROOT, FAM_FILE)) as f:
+            fr = json.load(f)
+    except (OSError, ValueError):
+        return None
+    stale = (fr.get("build") or {}).get("lib_sha256") != stamp["lib_sha256"]
+    fam = fr.get("family") or {}
+    return {"file": FAM_FILE, "stale": stale, "achieved": None if stale else fam.get("achieved_tflops"),
+            "frac": None if stale else fam.get("frac"), "us_per_step": fam.get("us"), "gflop_per_step": fam.get("gflop"),
+            "kernels": fam.get("kernels"), "dominant_kernel": fr.get("dominant_kernel"), "build": fr.get("build")}
+
+
 def algorithmic_flops_per_sample(c=CFG):
     """SURVEY.md §8(d) formula (sparse-T_k count, fwd; fwd+bwd = 3x)."""
     B, N, F, T, h, dk, D, K, C = 1, c["N"], c["C"], c["T"], c["n_heads"], c["d_k"], c["d_model"], c["K"], c["C"]
@@ -356,8 +406,12 @@ def main():
         P = args.prof_steps
         fam = dict(launches=launches / P, flops=flops / P, bytes=gbytes / P, ms=gms / P, max_ms=gmax,
                    serial_step_ms=t_ser * 1e3, dropped=dropped)
+        dominant = dominant_kernel(ops.prof_records(), P)
+    else:
+        dominant = None
     stamp = _lib.build_stamp()
     pmc = load_pmc(stamp)
+    rocprof_fam = load_family_rocprof(stamp)
     fresh = pmc is not None and not pmc["stale"]
     if fam is not None:
         achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
@@ -373,7 +427,10 @@ def main():
                 "ms_per_step": round(fam["ms"], 4), "avg_launch_us": round(fam["ms"] / fam["launches"] * 1e3, 3),
                 "share_of_serial_step": round(fam["ms"] / fam["serial_step_ms"], 3),
                 "min_bytes_per_step": int(fam["bytes"]),
-                "timing": f"HIP events around each call, {args.prof_steps} serialised steps"}
+                "timing": f"HIP events around each call, {args.prof_steps} serialised steps",
+                # the same family from the committed rocprofv3 trace of a serialised step
+                # (tools/step_trace.sh -> tools/step_kernels.py --json), when it measured this build
+                "rocprof": rocprof_fam}
     else:
         roof = None
     # the single longest-running GEMM call site of round 1, kept for continuity: the pre_conv
@@ -446,6 +503,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "algorithmic_tflops": round(algorithmic_flops_per_sample() * value / 1e12, 3),
             "roofline": roof,
+            "dominant_kernel": dominant,
             "hot_kernel": hot,
             "block_roofline": block_roof,
             "hbm_roofline": hbm_roof,

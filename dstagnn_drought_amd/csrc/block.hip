@@ -1862,6 +1862,7 @@ int dstagnn_prof_start(int capacity) { return gemm_prof_start(capacity); }
 int dstagnn_set_splitk_target(int target) { return gemm_set_splitk_target(target); }
 int dstagnn_set_gemm_bf16(int on) { return gemm_set_bf16(on); }
 int dstagnn_prof_stop(dstagnn_prof_stats* stats) { return gemm_prof_stop(stats); }
+int dstagnn_prof_records(dstagnn_prof_record* out, int cap) { return gemm_prof_records(out, cap < 0 ? 0 : cap); }
 int dstagnn_version(void) { return 1; }
 
 int dstagnn_block_sizes(const dstagnn_block_dims* d, size_t* save_bytes, size_t* scratch_bytes) {

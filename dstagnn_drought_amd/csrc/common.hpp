@@ -324,7 +324,8 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st);
 // overlap) so every recorded GEMM duration is its own
 bool gemm_prof_on();
 // a GEMM-family product computed by another kernel, timed into the same records (or null)
-void* gemm_prof_begin(double flops, double bytes, hipStream_t st);
+void* gemm_prof_begin(double flops, double bytes, hipStream_t st, int kind = DSTAGNN_PROF_GEMM);
+int gemm_prof_records(dstagnn_prof_record* out, int cap);
 void gemm_prof_end(void* rec, hipStream_t st);
 int gemm_prof_start(int capacity);
 int gemm_prof_stop(dstagnn_prof_stats* out);

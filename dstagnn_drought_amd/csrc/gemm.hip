@@ -375,10 +375,12 @@ int dma_width(const float* base, const Idx2& rowmap, int rows, const Idx2& kmap,
 struct ProfRec {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   double flops = 0, bytes = 0;
+  int kind = DSTAGNN_PROF_GEMM;  // DSTAGNN_PROF_* (include/dstagnn.h)
+  float ms = 0.f;                // set by gemm_prof_stop
 };
 struct Prof {
   bool on = false;
-  int n = 0, cap = 0, dropped = 0;
+  int n = 0, cap = 0, dropped = 0, last = 0;
   ProfRec* rec = nullptr;
 };
 Prof g_prof;
@@ -395,11 +397,14 @@ int g_bf16 = 0;
 
 }  // namespace
 
+namespace { bool gemm_log_on(); }
 bool gemm_prof_on() { return g_prof.on; }
 
 // the same event pair around a non-GEMM kernel that computes a GEMM-family product (the
 // sliding-window GTU input gradient, gtu_tconv.hip): counted with its algorithmic FLOP / bytes
-void* gemm_prof_begin(double flops, double bytes, hipStream_t st) {
+void* gemm_prof_begin(double flops, double bytes, hipStream_t st, int kind) {
+  if (gemm_log_on() && kind != DSTAGNN_PROF_GEMM)  // (tools/step_kernels.py pairs these with the trace)
+    fprintf(stderr, "[fused] kind=%d flops=%.0f bytes=%.0f\n", kind, flops, bytes);
   if (!g_prof.on) return nullptr;
   if (g_prof.n >= g_prof.cap) {
     ++g_prof.dropped;
@@ -408,6 +413,7 @@ void* gemm_prof_begin(double flops, double bytes, hipStream_t st) {
   ProfRec* r = &g_prof.rec[g_prof.n++];
   r->flops = flops;
   r->bytes = bytes;
+  r->kind = kind;
   (void)hipEventRecord(r->e0, st);
   return r;
 }
@@ -457,6 +463,7 @@ int gemm_prof_stop(dstagnn_prof_stats* out) {
     if (hipEventSynchronize(r.e1) != hipSuccess) { set_last_error("prof: event sync failed"); return DSTAGNN_E_ARG; }
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, r.e0, r.e1) != hipSuccess) { set_last_error("prof: elapsed failed"); return DSTAGNN_E_ARG; }
+    r.ms = ms;
     s.launches += 1;
     s.flops += r.flops;
     s.bytes += r.bytes;
@@ -464,9 +471,22 @@ int gemm_prof_stop(dstagnn_prof_stats* out) {
     s.max_ms = std::max(s.max_ms, (double)ms);
   }
   s.dropped = g_prof.dropped;
+  g_prof.last = g_prof.n;  // the window's records stay readable (gemm_prof_records) until the next start
   g_prof.n = 0;
   if (out) *out = s;
   return 0;
+}
+
+int gemm_prof_records(dstagnn_prof_record* out, int cap) {
+  const int n = std::min(cap, g_prof.last);
+  for (int i = 0; i < n && out; ++i) {
+    const ProfRec& r = g_prof.rec[i];
+    out[i].flops = r.flops;
+    out[i].bytes = r.bytes;
+    out[i].ms = r.ms;
+    out[i].kind = r.kind;
+  }
+  return g_prof.last;
 }
 
 namespace {
@@ -780,6 +800,7 @@ int run_gemm_group(const Gemm* gs, int n, float* ws, size_t ws_floats, hipStream
       prec = &g_prof.rec[g_prof.n++];
       prec->flops = flops;
       prec->bytes = bytes;
+      prec->kind = nl == 1 && live[0]->skinny ? DSTAGNN_PROF_SKINNY : DSTAGNN_PROF_GEMM;
       (void)hipEventRecord(prec->e0, st);
     } else {
       ++g_prof.dropped;
@@ -865,6 +886,7 @@ int run_gemm_kcat(const Gemm* gs, int n, hipStream_t st) {
       prec = &g_prof.rec[g_prof.n++];
       prec->flops = flops;
       prec->bytes = bytes;
+      prec->kind = DSTAGNN_PROF_GEMM;
       (void)hipEventRecord(prec->e0, st);
     } else {
       ++g_prof.dropped;

@@ -846,7 +846,7 @@ int op_gtu_fused_fwd(const GtuFusedArgs& a, hipStream_t st) {
   // the three convolutions' algorithmic FLOP (the GEMM family's accounting)
   const double flops = 2.0 * a.BN * (2.0 * kGC) * kGC * ((kGT - 2) * 3 + (kGT - 4) * 5 + (kGT - 6) * 7);
   const double bytes = 4.0 * a.BN * (kGCT * 6.0 + 2 * kGC * 24.0 + kGC * kGS);
-  void* rec = gemm_prof_begin(flops, bytes, st);
+  void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_GTU_FUSED_FWD);
   hipLaunchKernelGGL(k, dim3((unsigned)cdiv64(a.BN, kGNB)), dim3(kGW * 64), lds, st, a);
   DS_CHECK_LAUNCH();
   gemm_prof_end(rec, st);
@@ -897,7 +897,7 @@ int op_gtu_fused_bwd(const GtuFusedBwdArgs& a, hipStream_t st) {
     set_last_error("gtu_fused_bwd: no ticket counters");
     return DSTAGNN_E_ARG;
   }
-  void* rec = gemm_prof_begin(flops, bytes, st);
+  void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_GTU_FUSED_BWD);
   hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(kGW * 64), lds, st, b);
   DS_CHECK_LAUNCH();
   gemm_prof_end(rec, st);

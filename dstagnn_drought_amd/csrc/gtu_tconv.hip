@@ -246,7 +246,7 @@ int op_gtu_conv_fwd(GconvArgs a, hipStream_t st) {
   int rmax = 0;
   for (int q = 0; q < 3; ++q) rmax = std::max(rmax, gconv_rows_max(a.T, a.Tg[q], a.ks[q]));
   const size_t lds = (size_t)rmax * kGcRow * sizeof(float);  // <= 42 KB
-  void* rec = gemm_prof_begin(flops, bytes, st);
+  void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_GTU_TCONV);
   hipLaunchKernelGGL(gtu_conv_fwd_kernel, dim3((unsigned)at), dim3(256), lds, st, a);
   DS_CHECK_LAUNCH();
   gemm_prof_end(rec, st);
@@ -281,7 +281,7 @@ int op_gtu_tconv(const TconvArgs& a, hipStream_t st) {
   const StreamSig sg = peek_stream_sig(st);
   b.sig = sg.p;
   b.sig_v = sg.v;
-  void* rec = gemm_prof_begin(flops, bytes, st);
+  void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_GTU_TCONV);
   hipLaunchKernelGGL(gtu_tconv_kernel, dim3((unsigned)cdiv64(a.M, kTcBM)), dim3(256), 0, st, b);
   DS_CHECK_LAUNCH();
   if (sg.p) DS_TRY(stream_sig_sent(st, sg));

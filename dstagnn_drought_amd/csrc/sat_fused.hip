@@ -230,7 +230,7 @@ int op_sat_ln_bwd_fused(const SatLnBwdArgs& a, hipStream_t st) {
   }
   const double flops = 2.0 * a.R * kSbD * kSbK;
   const double bytes = 4.0 * ((double)a.R * (kSbK + 2.0 * kSbD) + (double)kSbD * kSbK);
-  void* rec = gemm_prof_begin(flops, bytes, st);
+  void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_SAT_FUSED);
   hipLaunchKernelGGL(sat_ln_bwd_fused_kernel, dim3((unsigned)cdiv64(a.R, kSbRows)), dim3(kSbW * 64), 0, st, a);
   DS_CHECK_LAUNCH();
   gemm_prof_end(rec, st);

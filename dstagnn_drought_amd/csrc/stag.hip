@@ -11,6 +11,8 @@
 //    fast_stag_dist_kernel  windowed cosine distance, symmetric, zero diagonal, fp64
 //    topk_rows_kernel       per row the k smallest keys (ties: lower index), bitonic sort of
 //                           (key, index) in LDS -> A (0/1), R, neighbour list
+#include <cstring>
+
 #include "common.hpp"
 #include "emd_simplex.hpp"
 
@@ -89,7 +91,13 @@ __global__ __launch_bounds__(kPrepThreads) void stag_prep_kernel(const double* _
   if (threadIdx.x == 0) psum[n] = tot;
 }
 
-// one wave per pair (grid-stride over pairs); dynamic LDS = emd::work_bytes(T, F)
+// one wave per pair (grid-stride over pairs); dynamic LDS = emd::work_bytes(T, GX ? 0 : F).
+// GX: the pair's unit rows stay in global memory (read through L1 / L2 by the pricing scan; a
+// node's rows serve all N - 1 of its pairs) instead of an LDS copy — at the GAMBIA shape the copy
+// is 18 of the 39 KB of a pair's workspace, so LDS admits 4 pairs per CU with it and 7 without:
+// the solver's serial tree walks are LDS-latency chains of one wave, so more resident pairs
+// per CU is the throughput lever (tools/bench_stag.py).
+template <bool GX>
 __global__ __launch_bounds__(64) void stag_emd_kernel(const double* __restrict__ xhat, const double* __restrict__ p,
                                                       const double* __restrict__ psum, int T, int F,
                                                       const int32_t* __restrict__ pairs, int64_t P,
@@ -98,7 +106,8 @@ __global__ __launch_bounds__(64) void stag_emd_kernel(const double* __restrict__
   extern __shared__ double smem[];
   const int lane = threadIdx.x;
   emd::Work w;
-  emd::carve(w, (char*)smem, T, F);
+  emd::carve(w, (char*)smem, T, GX ? 0 : F);
+  w.F = F;
   for (int64_t k = blockIdx.x; k < P; k += gridDim.x) {
     const int i = pairs[2 * k], j = pairs[2 * k + 1];
     if (!emd::balanced(psum[i], psum[j])) {
@@ -106,9 +115,14 @@ __global__ __launch_bounds__(64) void stag_emd_kernel(const double* __restrict__
       continue;
     }
     const int64_t tf = (int64_t)T * F;
-    for (int64_t e = lane; e < tf; e += 64) {
-      ((double*)w.xh)[e] = xhat[(int64_t)i * tf + e];
-      ((double*)w.yh)[e] = xhat[(int64_t)j * tf + e];
+    if (GX) {
+      w.xh = xhat + (int64_t)i * tf;
+      w.yh = xhat + (int64_t)j * tf;
+    } else {
+      for (int64_t e = lane; e < tf; e += 64) {
+        ((double*)w.xh)[e] = xhat[(int64_t)i * tf + e];
+        ((double*)w.yh)[e] = xhat[(int64_t)j * tf + e];
+      }
     }
     for (int t = lane; t < T; t += 64) {
       ((double*)w.p)[t] = p[(int64_t)i * T + t];
@@ -295,12 +309,19 @@ int dstagnn_stag_emd_pairs(const double* xhat, const double* p, const double* ps
   if (!xhat || !p || !psum || !pairs || !out || !status) { set_last_error("stag_emd: null argument"); return DSTAGNN_E_ARG; }
   if (T <= 0 || N <= 0 || F <= 0 || P < 0) { set_last_error("stag_emd: bad dimension"); return DSTAGNN_E_SHAPE; }
   if (2 * (int64_t)T + 1 > 32767) { set_last_error("stag_emd: T too large (node ids are int16)"); return DSTAGNN_E_SHAPE; }
-  const int64_t lds = emd::work_bytes(T, F);
+  // DSTAGNN_STAG_XH=lds keeps the unit rows in LDS (the round-1 layout); default: global
+  static const bool gx = !getenv("DSTAGNN_STAG_XH") || strcmp(getenv("DSTAGNN_STAG_XH"), "lds") != 0;
+  const int64_t lds = emd::work_bytes(T, gx ? 0 : F);
   if (lds > kLdsMax) { set_last_error("stag_emd: T*F too large for LDS"); return DSTAGNN_E_SHAPE; }
   if (P == 0) return 0;
-  if (int rc = set_lds((const void*)stag_emd_kernel, lds)) return rc;
-  hipLaunchKernelGGL(stag_emd_kernel, dim3(emd_grid(P, lds)), dim3(64), lds, (hipStream_t)stream, xhat, p, psum, T, F,
-                     pairs, P, out, status, pivots);
+  const void* kern = gx ? (const void*)stag_emd_kernel<true> : (const void*)stag_emd_kernel<false>;
+  if (int rc = set_lds(kern, lds)) return rc;
+  if (gx)
+    hipLaunchKernelGGL(stag_emd_kernel<true>, dim3(emd_grid(P, lds)), dim3(64), lds, (hipStream_t)stream, xhat, p, psum,
+                       T, F, pairs, P, out, status, pivots);
+  else
+    hipLaunchKernelGGL(stag_emd_kernel<false>, dim3(emd_grid(P, lds)), dim3(64), lds, (hipStream_t)stream, xhat, p,
+                       psum, T, F, pairs, P, out, status, pivots);
   DS_CHECK_LAUNCH();
   return 0;
 }

@@ -1051,7 +1051,7 @@ int op_tat_fused_fwd(const TatFusedArgs& a0, hipStream_t st) {
       done.insert(k);
     }
   }
-  void* rec = gemm_prof_begin(flops, bytes, st);
+  void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_TAT_FUSED_FWD);
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
   DS_CHECK_LAUNCH();
   if (sg.p) DS_TRY(stream_sig_sent(st, sg));
@@ -1124,7 +1124,7 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
       done.insert(k);
     }
   }
-  void* rec = gemm_prof_begin(flops, bytes, st);
+  void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_TAT_FUSED_BWD);
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
   DS_CHECK_LAUNCH();
   if (sg.p) DS_TRY(stream_sig_sent(st, sg));

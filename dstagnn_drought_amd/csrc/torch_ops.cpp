@@ -843,6 +843,21 @@ std::vector<double> prof_stop() {
   check_rc(dstagnn_prof_stop(&s), "dstagnn_prof_stop");
   return {s.launches, s.flops, s.bytes, s.ms, s.max_ms, s.dropped};
 }
+// the last window's records one by one: [kind, flops, bytes, ms] * n
+std::vector<double> prof_records() {
+  const int n = dstagnn_prof_records(nullptr, 0);
+  std::vector<dstagnn_prof_record> r((size_t)std::max(n, 0));
+  if (n > 0) dstagnn_prof_records(r.data(), n);
+  std::vector<double> out;
+  out.reserve(4 * r.size());
+  for (const auto& x : r) {
+    out.push_back((double)x.kind);
+    out.push_back(x.flops);
+    out.push_back(x.bytes);
+    out.push_back(x.ms);
+  }
+  return out;
+}
 
 }  // namespace
 
@@ -885,6 +900,7 @@ TORCH_LIBRARY(dstagnn, m) {
   m.def("set_splitk_target(int target) -> int", set_splitk_target);
   m.def("set_gemm_bf16(int on) -> int", set_gemm_bf16);
   m.def("prof_stop() -> float[]", prof_stop);
+  m.def("prof_records() -> float[]", prof_records);
 }
 
 // PyTorch-ROCm dispatches HIP device tensors under the CUDA key

@@ -351,6 +351,27 @@ typedef struct dstagnn_prof_stats {
 } dstagnn_prof_stats;
 int dstagnn_prof_start(int capacity);
 int dstagnn_prof_stop(dstagnn_prof_stats* stats);
+/* The recorded calls of the last start/stop window one by one (what the family sums are made of):
+ * kind says which kernel computed the product, so the benchmark can report the dominant single
+ * kernel (its own FLOP, bytes and duration) beside the family.  Returns the window's record
+ * count; copies min(count, cap) records into out (may be NULL to query). */
+enum {
+  DSTAGNN_PROF_GEMM = 0,           /* gemm_f32 kernel(s) of one call + split-K fold             */
+  DSTAGNN_PROF_SKINNY = 1,         /* skinny_dw_kernel (long skinny weight-gradient reduction)  */
+  DSTAGNN_PROF_TAT_FUSED_FWD = 2,  /* tat_fused_fwd_kernel                                      */
+  DSTAGNN_PROF_TAT_FUSED_BWD = 3,  /* tat_fused_bwd_kernel                                      */
+  DSTAGNN_PROF_GTU_FUSED_FWD = 4,  /* gtu_fwd_fused_kernel                                      */
+  DSTAGNN_PROF_GTU_FUSED_BWD = 5,  /* gtu_bwd_fused_kernel                                      */
+  DSTAGNN_PROF_GTU_TCONV = 6,      /* gtu_tconv / gtu_conv_fwd sliding-window convolutions      */
+  DSTAGNN_PROF_SAT_FUSED = 7       /* sat_ln_bwd_fused kernel                                   */
+};
+typedef struct dstagnn_prof_record {
+  double flops;  /* algorithmic FLOP of the call   */
+  double bytes;  /* algorithmic (minimum) bytes    */
+  double ms;     /* HIP-event duration             */
+  int kind;      /* DSTAGNN_PROF_*                 */
+} dstagnn_prof_record;
+int dstagnn_prof_records(dstagnn_prof_record* out, int cap);
 
 /* Split-K policy of the GEMMs: a GEMM with a grid below 128 workgroups splits its K range
  * over about `target` workgroups (default 448).  target = 1 never splits a tiled GEMM, so those

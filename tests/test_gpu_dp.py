@@ -9,6 +9,7 @@ Checked: the hook fired with the block's flat buffer (one in-flight reduction af
 backward, none without attach), the reduced gradients equal the non-overlapped path's, and
 every rank holds the same mean."""
 import json
+from pathlib import Path
 import os
 import subprocess
 import sys
@@ -82,6 +83,10 @@ def test_rccl_world1_reducer(tmp_path):
     _launch("rccl_worker.py", tmp_path, nproc=1)
     rec = json.loads((tmp_path / "rccl_world1.json").read_text())
     print("rccl world 1:", rec)
+    keep = os.environ.get("DSTAGNN_PROFILE_OUT")  # (tools/gpu_check.sh: kept as profiles/<round>_rccl_world1.json)
+    if keep:
+        os.makedirs(keep, exist_ok=True)
+        (Path(keep) / "rccl_world1.json").write_text(json.dumps(rec))
     assert rec["backend"] == "nccl" and rec["world"] == 1, rec
     assert rec["hook_inflight"] == 1, rec   # the node's post-hook issued the async all-reduce
     assert rec["exact"] and rec["collective_ok"], rec

@@ -25,7 +25,7 @@ echo "steps: $STEPS"
 IFS=',' read -ra S <<< "$STEPS"
 for s in "${S[@]}"; do
   case $s in
-    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu --maxfail=8 -q -rf --timeout 180 --timeout-method thread ;;
+    pytest) DSTAGNN_PROFILE_OUT=gpurun_out run pytest_gpu 900 python -u -m pytest tests -m gpu --maxfail=8 -q -rf --timeout 180 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;

@@ -41,5 +41,9 @@ done
 if [ -f gpurun_out/pmcb_summary.txt ]; then
   { echo "# build (measured): $(cat gpurun_out/pmcb/build.json 2>/dev/null)  git: $HEAD"; cat gpurun_out/pmcb_summary.txt; } > "profiles/${R}_step_sq_pmc.txt"
 fi
+[ -f gpurun_out/rccl_world1.json ] && cp gpurun_out/rccl_world1.json "profiles/${R}_rccl_world1.json"
+[ -f gpurun_out/trace_final/family_rocprof.json ] && { cp gpurun_out/trace_final/family_rocprof.json profiles/family_rocprof.json;
+  cp gpurun_out/trace_final/family_rocprof.json "profiles/${R}_family_rocprof.json"; }
+[ -f gpurun_out/trace_final/gemm.log ] && grep -h '^\[gemm\]\|^\[fused\]' gpurun_out/trace_final/gemm.log > "profiles/${R}_step_family_calls.log"
 [ -f gpurun_out/configs.log ] && grep -h '^{' gpurun_out/configs.log | tail -1 > "profiles/${R}_configs_bench.json"
 ls -la profiles | grep "$R"

@@ -17,5 +17,5 @@ rc=$?
 echo "== trace $TAG rc=$rc"
 [ $rc -ne 0 ] && { tail -5 $OUT/gemm.log; exit $rc; }
 python3 tools/step_kernels.py "$(ls $OUT/*/*kernel_trace.csv $OUT/*kernel_trace.csv 2>/dev/null | head -1)" $OUT/gemm.log 2 \
-  > $OUT/step_kernels.txt
+  --json $OUT/family_rocprof.json > $OUT/step_kernels.txt
 tail -25 $OUT/step_kernels.txt
