@@ -592,7 +592,14 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       DUs[r * LE + n] = a.dO[(int64_t)ft * a.BN + (int64_t)bb * N + n];
     }
   }
-  __syncthreads();  // the u / dO tiles
+  // the u / dO tiles: a raw barrier behind the LDS stores only — __syncthreads() would also
+  // drain vmcnt, i.e. wait here for the 55 KB of Q|K|V rows (and the softmax / d re_At
+  // operands) that are first used after the LayerNorm phase; they stay in flight through it
+#ifdef DSTAGNN_TF_SYNC_A0
+  __syncthreads();  // (A/B builds: the round-5 barrier)
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
   TF_MARK(1);
   TF_MARK(2);
   // ---- A1. LayerNorm(N) backward of the wave's 12 rows at once (ln_bwd_kernel's arithmetic) --
