@@ -36,7 +36,7 @@ constexpr int kTfHV = kTfH * kTfD;      // 96
 constexpr int kTfLQ = kTfQW + 4;        // LDS row stride of the Q|K|V tile
 constexpr int kTfLC = kTfHV + 4;        // ... of the ctx tile
 constexpr int kTfQT = kTfQW / 16;       // 18 column tiles of Q|K|V
-constexpr int kTfQTW = (kTfQT + 3) / 4; // 5 per wave (the last of waves 2, 3 is a discarded duplicate)
+constexpr int kTfQTW = (kTfQT + 3) / 4; // 5 per GEMM wave (the last of waves 2, 3 is a discarded duplicate)
 constexpr int kTfNmax = 320;            // N <= 320 (LDS: <= 156 KB)
 constexpr int kTfRPW = kTfRows / 4;     // LayerNorm rows per wave
 constexpr int kTfDsMax = 2304;          // (48 / T) h T^2 at T = 16
@@ -88,10 +88,11 @@ __device__ __forceinline__ void tf_wave_sync() {  // LDS hand-off inside one wav
 // a contiguous block of n floats from LDS (row stride ls, row length rl, both multiples of 4)
 // to global memory, float4 per lane (the stores of a kernel go out at its end: stores count in
 // vmcnt on gfx9, so a store issued before a k loop would hold up that loop's operand waits)
+template <int NTH = 256>  // threads of the workgroup
 __device__ __forceinline__ void tf_copy_out(float* g, const float* l, int rows, int rl, int ls, int tid) {
   const int q4 = rl / 4;
   float4* g4 = reinterpret_cast<float4*>(g);
-  for (int e = tid; e < rows * q4; e += 256) {
+  for (int e = tid; e < rows * q4; e += NTH) {
     const int r = e / q4, c4 = e - r * q4;
     g4[e] = *reinterpret_cast<const float4*>(l + r * ls + 4 * c4);
   }
@@ -159,24 +160,26 @@ __device__ __forceinline__ void tf_gemm_rows48(floatx4 (&acc)[3][NJ], const floa
 // E tile (48 x NP, zero-padded) into LDS, every load of a thread issued before its first LDS
 // store.  x (B,N,F,T) with the 48 rows inside one sample: a node's 48 values are contiguous —
 // float4 per lane; otherwise (E row-major, first block) scalar loads along the nodes.
+template <int NTH = 256>  // threads of the workgroup
 __device__ __forceinline__ void tf_load_e_tile(const TatFusedArgs& a, int64_t R0, int nrows, float* Es, int LE,
                                                int NP, int N, int tid, int64_t* roff) {
+  constexpr int UE = 2048 / NTH;  // loads in flight per thread (2048 per workgroup round)
   const uint32_t ft0 = (uint32_t)R0 % (uint32_t)a.FT;
   if (a.sN != 1 && a.s0 == 1 && nrows == kTfRows && ft0 + kTfRows <= (uint32_t)a.FT) {
     const float* base = a.src + tf_row(a, R0);
     constexpr int Q4 = kTfRows / 4;  // 12 float4 per node
     const int total = N * Q4;
-    for (int e0 = 0; e0 < total; e0 += 256 * 8) {
-      float4 v[8];
+    for (int e0 = 0; e0 < total; e0 += NTH * UE) {
+      float4 v[UE];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = min(e0 + u * 256 + tid, total - 1);
+      for (int u = 0; u < UE; ++u) {
+        const int e = min(e0 + u * NTH + tid, total - 1);
         const int n = e / Q4, c4 = e - n * Q4;
         v[u] = *reinterpret_cast<const float4*>(base + (int64_t)n * a.sN + 4 * c4);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u * 256 + tid;
+      for (int u = 0; u < UE; ++u) {
+        const int e = e0 + u * NTH + tid;
         if (e < total) {
           const int n = e / Q4, r = 4 * (e - n * Q4);
           Es[r * LE + n] = v[u].x;
@@ -186,7 +189,7 @@ __device__ __forceinline__ void tf_load_e_tile(const TatFusedArgs& a, int64_t R0
         }
       }
     }
-    for (int e = tid; e < kTfRows * (NP - N); e += 256) {  // pad columns
+    for (int e = tid; e < kTfRows * (NP - N); e += NTH) {  // pad columns
       const int r = e / (NP - N), n = N + e - r * (NP - N);
       Es[r * LE + n] = 0.f;
     }
@@ -195,11 +198,11 @@ __device__ __forceinline__ void tf_load_e_tile(const TatFusedArgs& a, int64_t R0
   if (tid < kTfRows) roff[tid] = tf_row(a, R0 + min(tid, max(nrows - 1, 0)));
   __syncthreads();
   const int total = kTfRows * NP;
-  for (int e0 = 0; e0 < total; e0 += 256 * 8) {
-    float v[8];
+  for (int e0 = 0; e0 < total; e0 += NTH * UE) {
+    float v[UE];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + u * 256 + tid;
+    for (int u = 0; u < UE; ++u) {
+      const int e = e0 + u * NTH + tid;
       int r, n;
       if (a.sN == 1) { r = e / NP; n = e - r * NP; }
       else { n = e / kTfRows; r = e - n * kTfRows; }
@@ -207,8 +210,8 @@ __device__ __forceinline__ void tf_load_e_tile(const TatFusedArgs& a, int64_t R0
       v[u] = ok ? a.src[roff[min(r, kTfRows - 1)] + (int64_t)min(n, N - 1) * a.sN] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + u * 256 + tid;
+    for (int u = 0; u < UE; ++u) {
+      const int e = e0 + u * NTH + tid;
       if (e < total) {
         int r, n;
         if (a.sN == 1) { r = e / NP; n = e - r * NP; }
@@ -225,12 +228,24 @@ __device__ __forceinline__ void tf_load_e_tile(const TatFusedArgs& a, int64_t R0
 // =====================================================================================
 // LDS (floats): Es [48][NP+4] (E, then u = fc + E) | Qs [48][292] Q|K|V | Cs [48][100] ctx |
 // RA [PW h T^2] re_At | AT [PW h T^2] softmax — re_At / A / Q|K|V / ctx go out at the end
-template <int T, int NTW>  // NTW: fc column tiles per wave = LayerNorm values per lane (ceil(NP / 64))
-__global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
+// W waves (4: one per SIMD; 8: two per SIMD — each phase's work split over twice the waves, so
+// one wave's latency (LDS fragment loads, L2 weight loads, shuffles) hides behind its SIMD twin's)
+template <int T, int NTW, int W>  // NTW: LayerNorm values per lane (ceil(NP / 64))
+__global__ __launch_bounds__(64 * W, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
   static_assert(T % 4 == 0 && T <= 16 && kTfRows % T == 0, "whole problems per workgroup, one 16 x 16 tile");
+  static_assert(W == 4 || W == 8, "four or eight waves");
+  constexpr int NTH = 64 * W;
   constexpr int PW = kTfRows / T;                  // problems per workgroup
   constexpr int NTASK = PW * kTfH;                 // (problem, head) attention tasks
-  constexpr int TPW = (NTASK + 3) / 4;             // per wave
+  constexpr int TPW = (NTASK + W - 1) / W;         // per wave
+  // the two products run on waves 0-3 only (the 4-wave column tiling, one wave per SIMD): with
+  // 8 waves on them both an 8-way column split (a third of the Q|K|V tiles duplicates) and a
+  // contraction split (partials added through LDS) measured slower — 15 / 19 us for the Q|K|V
+  // product against 12.5 on four waves (-DDSTAGNN_TF_TIMING); the latency-bound phases
+  // (E tile, attention, LayerNorm, stores) use all W waves
+  constexpr int QTW = kTfQTW;                      // Q|K|V column tiles per wave
+  constexpr int NFC = NTW;                         // fc column tiles per wave (NP / 16 <= 4 NTW tiles)
+  constexpr int RPW = kTfRows / W;                 // LayerNorm rows per wave
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   const int NP = a.NP, LE = NP + 4, N = a.N;
@@ -252,7 +267,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
     rr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int task = w + 4 * k, p = task / kTfH, hd = task - p * kTfH;
+    const int task = w + W * k, p = task / kTfH, hd = task - p * kTfH;
     if (task < NTASK && p * T < nrows && i < T && q < T / 4 && a.res_mode != DSTAGNN_RES_NONE) {
       const int64_t P = P0 + p;
       const int64_t bP = (uint32_t)P / (uint32_t)a.F;
@@ -270,29 +285,31 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
     bv[j] = a.bta[n];
   }
   // ---- 1. E tile --------------------------------------------------------------------------
-  tf_load_e_tile(a, R0, nrows, Es, LE, NP, N, tid, reinterpret_cast<int64_t*>(Qs));
+  tf_load_e_tile<NTH>(a, R0, nrows, Es, LE, NP, N, tid, reinterpret_cast<int64_t*>(Qs));
   __syncthreads();
   TF_MARK(1);
 
   // ---- 2. Q | K | V = E Wqkv^T ------------------------------------------------------------
   {
-    floatx4 acc[3][kTfQTW];
+    floatx4 acc[3][QTW];
 #pragma unroll
     for (int mt = 0; mt < 3; ++mt)
 #pragma unroll
-      for (int j = 0; j < kTfQTW; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* wp[kTfQTW];
+      for (int j = 0; j < QTW; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (w < 4) {  // (wave-uniform)
+      const float* wp[QTW];
 #pragma unroll
-    for (int j = 0; j < kTfQTW; ++j) wp[j] = a.wqkv + (int64_t)(min(w + 4 * j, kTfQT - 1) * 16 + i) * NP + 4 * q;
-    tf_gemm_rows48(acc, Es, LE, NP / 16, i, q, wp);
+      for (int j = 0; j < QTW; ++j) wp[j] = a.wqkv + (int64_t)(min(w + 4 * j, kTfQT - 1) * 16 + i) * NP + 4 * q;
+      tf_gemm_rows48(acc, Es, LE, NP / 16, i, q, wp);
 #pragma unroll
-    for (int j = 0; j < kTfQTW; ++j) {
-      const int nt = w + 4 * j;
-      if (nt < kTfQT) {
+      for (int j = 0; j < QTW; ++j) {
+        const int nt = w + 4 * j;
+        if (nt < kTfQT) {
 #pragma unroll
-        for (int mt = 0; mt < 3; ++mt)
+          for (int mt = 0; mt < 3; ++mt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) Qs[(mt * 16 + 4 * q + r) * kTfLQ + nt * 16 + i] = acc[mt][j][r];
+            for (int r = 0; r < 4; ++r) Qs[(mt * 16 + 4 * q + r) * kTfLQ + nt * 16 + i] = acc[mt][j][r];
+        }
       }
     }
   }
@@ -302,7 +319,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
   // ---- 3. attention per (problem, head) (tat_fwd_mfma_kernel's math, operands from LDS) ----
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
-    const int task = w + 4 * k;
+    const int task = w + W * k;
     // (continue, not break: a break leaves the loop not fully unrolled and the per-task register
     // arrays rr / at / dr dynamically indexed — readlane / cndmask chains, measured 2x slower)
     if (task >= NTASK || (task / kTfH) * T >= nrows) continue;  // (wave-uniform)
@@ -372,17 +389,18 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
   // ---- 4. u = ctx W_fc^T + E, in the E tile -------------------------------------------------
   {
     const int NT = NP / 16;
-    floatx4 acc[3][NTW];
+    floatx4 acc[3][NFC];
 #pragma unroll
     for (int mt = 0; mt < 3; ++mt)
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* wp[NTW];
+      for (int j = 0; j < NFC; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (w < 4) {  // (wave-uniform)
+    const float* wp[NFC];
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) wp[j] = a.wfc + (int64_t)min(min(w + 4 * j, NT - 1) * 16 + i, N - 1) * kTfHV + 4 * q;
+    for (int j = 0; j < NFC; ++j) wp[j] = a.wfc + (int64_t)min(min(w + 4 * j, NT - 1) * 16 + i, N - 1) * kTfHV + 4 * q;
     tf_gemm_rows48(acc, Cs, kTfLC, kTfHV / 16, i, q, wp);
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
+    for (int j = 0; j < NFC; ++j) {
       const int nt = w + 4 * j;
       if (nt < NT) {
 #pragma unroll
@@ -394,6 +412,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
           }
       }
     }
+    }
   }
   __syncthreads();
   TF_MARK(4);
@@ -401,11 +420,11 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
   // ---- 5. LayerNorm over N, the wave's 12 rows at once (ln_fwd_kernel's two-pass statistics;
   // the row sums of all 12 rows in one multi-value reduction instead of 12 dependent chains) ----
   {
-    float v[kTfRPW][NTW];
-    float s16[kTfRPW];
+    float v[RPW][NTW];
+    float s16[RPW];
 #pragma unroll
-    for (int k = 0; k < kTfRPW; ++k) {
-      const float* row = Es + (w + 4 * k) * LE;
+    for (int k = 0; k < RPW; ++k) {
+      const float* row = Es + (w + W * k) * LE;
       float sum = 0.f;
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
@@ -416,11 +435,11 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
       s16[k] = sum;
     }
     tf_wave_sums(s16);
-    float mean[kTfRPW];
+    float mean[RPW];
 #pragma unroll
-    for (int k = 0; k < kTfRPW; ++k) mean[k] = s16[k] / N;
+    for (int k = 0; k < RPW; ++k) mean[k] = s16[k] / N;
 #pragma unroll
-    for (int k = 0; k < kTfRPW; ++k) {
+    for (int k = 0; k < RPW; ++k) {
       float var = 0.f;
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
@@ -434,8 +453,8 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
     }
     tf_wave_sums(s16);
 #pragma unroll
-    for (int k = 0; k < kTfRPW; ++k) {
-      const int r = w + 4 * k;
+    for (int k = 0; k < RPW; ++k) {
+      const int r = w + W * k;
       if (r >= nrows) continue;
       const int64_t R = R0 + r;
       const float rs = rsqrtf(s16[k] / N + a.eps);
@@ -458,11 +477,11 @@ __global__ __launch_bounds__(256, 1) void tat_fused_fwd_kernel(TatFusedArgs a) {
   }
   TF_MARK(5);
   // ---- 6. the saved tiles: Q|K|V, ctx, re_At, A (contiguous blocks for the workgroup) --------
-  tf_copy_out(a.qkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
-  tf_copy_out(a.ctx + R0 * kTfHV, Cs, nrows, kTfHV, kTfLC, tid);
+  tf_copy_out<NTH>(a.qkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
+  tf_copy_out<NTH>(a.ctx + R0 * kTfHV, Cs, nrows, kTfHV, kTfLC, tid);
   const int np = nrows / T;
-  tf_copy_out(a.re_at + P0 * kTfH * T * T, RA, 1, np * kTfH * T * T, 0, tid);
-  tf_copy_out(a.att + P0 * kTfH * T * T, AT, 1, np * kTfH * T * T, 0, tid);
+  tf_copy_out<NTH>(a.re_at + P0 * kTfH * T * T, RA, 1, np * kTfH * T * T, 0, tid);
+  tf_copy_out<NTH>(a.att + P0 * kTfH * T * T, AT, 1, np * kTfH * T * T, 0, tid);
   TF_MARK(6);
   TF_PRINT("tat_fused_fwd", 7);
 }
@@ -1033,14 +1052,18 @@ int op_tat_fused_fwd(const TatFusedArgs& a0, hipStream_t st) {
   const double bytes = 4.0 * a.BFT * (a.N + kTfQW + kTfHV + 2.0 * a.N + 2.0 * kTfH * a.T) + 4.0 * kTfQW * a.NP;
   using Kern = void (*)(TatFusedArgs);
   Kern k = nullptr;
-#define TF_T(TT)                                          \
-  switch (ntw) {                                          \
-    case 1: k = tat_fused_fwd_kernel<TT, 1>; break;       \
-    case 2: k = tat_fused_fwd_kernel<TT, 2>; break;       \
-    case 3: k = tat_fused_fwd_kernel<TT, 3>; break;       \
-    case 4: k = tat_fused_fwd_kernel<TT, 4>; break;       \
-    default: k = tat_fused_fwd_kernel<TT, 5>; break;      \
-  }                                                       \
+  // DSTAGNN_TF_WAVES=4|8: the forward's workgroup size (A/B)
+  static const int waves = getenv("DSTAGNN_TF_WAVES") && atoi(getenv("DSTAGNN_TF_WAVES")) == 4 ? 4 : 8;
+#define TF_NTW(TT, WW)                                        \
+  switch (ntw) {                                              \
+    case 1: k = tat_fused_fwd_kernel<TT, 1, WW>; break;       \
+    case 2: k = tat_fused_fwd_kernel<TT, 2, WW>; break;       \
+    case 3: k = tat_fused_fwd_kernel<TT, 3, WW>; break;       \
+    case 4: k = tat_fused_fwd_kernel<TT, 4, WW>; break;       \
+    default: k = tat_fused_fwd_kernel<TT, 5, WW>; break;      \
+  }
+#define TF_T(TT)                                              \
+  if (waves == 8) { TF_NTW(TT, 8) } else { TF_NTW(TT, 4) }   \
   break;
   switch (a.T) {
     case 8: TF_T(8)
@@ -1048,6 +1071,7 @@ int op_tat_fused_fwd(const TatFusedArgs& a0, hipStream_t st) {
     default: TF_T(16)
   }
 #undef TF_T
+#undef TF_NTW
   if (lds > 64 * 1024) {  // once per instantiation: dynamic LDS above 64 KB needs the opt-in
     static std::mutex mu;
     static std::set<Kern> done;
@@ -1059,7 +1083,7 @@ int op_tat_fused_fwd(const TatFusedArgs& a0, hipStream_t st) {
     }
   }
   void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_TAT_FUSED_FWD);
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * waves), lds, st, a);
   DS_CHECK_LAUNCH();
   if (sg.p) DS_TRY(stream_sig_sent(st, sg));
   gemm_prof_end(rec, st);
