@@ -499,15 +499,21 @@ size_t tat_fused_lds(int NP) {
 // Saved for the weight gradients (issued after it): dU (fc) and dqkv (Q|K|V); the LayerNorm's
 // gamma / beta as one partial row per workgroup; the broadcast res_att gradient sum_f dS folded
 // in-kernel (fixed chunk order, tat_bwd_mfma's ticket hand-off).
-// LDS (floats): DUs [48][NP+4] | Qs [48][292] Q|K|V then dQ|dK|dV | Cs [48][100] dctx (first the
-// gamma / beta wave partials) | TRs [4][16][17] | DSs [PW h T^2] dS (+ one int)
+// LDS (floats): DUs [48][NP+4] | Qs [48][292] u, then the gamma / beta wave partials, then Q|K|V,
+// then dQ|dK|dV | Cs [48][100] dctx | TRs [W][16][17] | DSs [PW h T^2] dS (+ one int)
 // =====================================================================================
-template <int T, int NTW>
-__global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a) {
+// W waves as in the forward: the two products (dctx, dE) on waves 0-3 (one per SIMD), the load,
+// LayerNorm, attention and store phases on all W
+template <int T, int NTW, int W>
+__global__ __launch_bounds__(64 * W, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a) {
   static_assert(T % 4 == 0 && T <= 16 && kTfRows % T == 0, "whole problems per workgroup, one 16 x 16 tile");
+  static_assert(W == 4 || W == 8, "four or eight waves");
+  constexpr int NTH = 64 * W;
   constexpr int PW = kTfRows / T;
   constexpr int NTASK = PW * kTfH;
-  constexpr int TPW = (NTASK + 3) / 4;
+  constexpr int TPW = (NTASK + W - 1) / W;
+  constexpr int RPW = kTfRows / W;            // LayerNorm rows per wave
+  constexpr int GJ = (512 + NTH - 1) / NTH;   // gamma / beta columns per thread (N <= 320 < 512)
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   const int NP = a.NP, LE = NP + 4, N = a.N;
@@ -515,7 +521,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   float* Qs = DUs + kTfRows * LE;
   float* Cs = Qs + kTfRows * kTfLQ;
   float* TRs = Cs + kTfRows * kTfLC;
-  float* DSs = TRs + 4 * 16 * 17;
+  float* DSs = TRs + W * 16 * 17;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, i = l & 15, q = l >> 4;
   const int64_t R0 = (int64_t)blockIdx.x * kTfRows;
   const int nrows = (int)min<int64_t>(kTfRows, a.BFT - R0);
@@ -533,8 +539,8 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   // staging array in scratch.
   typedef float tf_f2 __attribute__((ext_vector_type(2)));
   float* Us = Qs;  // [48][LE] u (the Q|K|V + ctx regions, free until after the LayerNorm)
-  constexpr int UV = 3 * NTW;  // float4 of u per thread: 48 N / 4 / 256 <= 3 NTW (one round)
-  constexpr int DV = 6 * NTW;  // float2 of dO per thread: 48 N / 2 / 256 <= 6 NTW
+  constexpr int UV = (12 * NTW + W - 1) / W;  // float4 of u per thread: 48 N / 4 / NTH (one round)
+  constexpr int DV = (24 * NTW + W - 1) / W;  // float2 of dO per thread: 48 N / 2 / NTH
   const int tot = nrows * N, h2 = N / 2, tot2 = nrows * h2;
   const bool vec = (tot & 3) == 0 && (N & 1) == 0;  // else: dword loads (odd N), the slow path below
   const float* gu = a.u + R0 * N;
@@ -542,19 +548,19 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   tf_f2 dv[DV];
   if (vec) {
 #pragma unroll
-    for (int u = 0; u < UV; ++u) uv[u] = reinterpret_cast<const floatx4*>(gu)[min(u * 256 + tid, tot / 4 - 1)];
+    for (int u = 0; u < UV; ++u) uv[u] = reinterpret_cast<const floatx4*>(gu)[min(u * NTH + tid, tot / 4 - 1)];
 #pragma unroll
     for (int u = 0; u < DV; ++u) {  // (magic divisions: runtime-divisor ones cost ~40 VALU each)
-      const int e = min(u * 256 + tid, tot2 - 1), r = (int)fdiv((uint32_t)e, a.fdH2), c2 = e - r * h2;
+      const int e = min(u * NTH + tid, tot2 - 1), r = (int)fdiv((uint32_t)e, a.fdH2), c2 = e - r * h2;
       const uint32_t R = (uint32_t)(R0 + r);
       const uint32_t bb = fdiv(R, a.fdFT), ft = R - bb * (uint32_t)a.FT;
       dv[u] = *reinterpret_cast<const tf_f2*>(a.dO + (int64_t)ft * a.BN + (int64_t)bb * N + 2 * c2);
     }
   }
-  // the LayerNorm statistics of the wave's rows (lane k < 12: row w + 4k) and gamma
+  // the LayerNorm statistics of the wave's rows (lane k < RPW: row w + W k) and gamma
   float mu_l, rs_l, gl[NTW];
   {
-    const int64_t R = R0 + min(w + 4 * min(l, kTfRPW - 1), nrows - 1);
+    const int64_t R = R0 + min(w + W * min(l, RPW - 1), nrows - 1);
     mu_l = a.mu[R];
     rs_l = a.rs[R];
 #pragma unroll
@@ -563,7 +569,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   float at[TPW][4], dr[TPW][4];
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
-    const int task = w + 4 * k, p = task / kTfH, hd = task - p * kTfH;
+    const int task = w + W * k, p = task / kTfH, hd = task - p * kTfH;
     const bool live = task < NTASK && p * T < nrows;
     const int64_t sbase = ((P0 + p) * kTfH + hd) * T * T;
 #pragma unroll
@@ -574,19 +580,19 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       dr[k][s] = ok && a.dre ? a.dre[sbase + ii * T + i] : 0.f;
     }
   }
-  constexpr int QV4 = kTfRows * kTfQW / 4 / 256;  // 13.5 -> 14 float4 per thread
+  constexpr int QV4 = kTfRows * kTfQW / 4 / NTH;  // 13.5 -> 14 (6.75 -> 7) float4 per thread
   floatx4 qv[QV4 + 1];
   {
     const floatx4* gq = reinterpret_cast<const floatx4*>(a.qkv + R0 * kTfQW);
     const int totq = nrows * (kTfQW / 4);
 #pragma unroll
-    for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * 256 + tid, totq - 1)];
+    for (int u = 0; u <= QV4; ++u) qv[u] = gq[min(u * NTH + tid, totq - 1)];
   }
   __builtin_amdgcn_sched_barrier(0);  // (every load above is issued before the first LDS store)
   if (vec) {
 #pragma unroll
     for (int u = 0; u < UV; ++u) {
-      const int e4 = u * 256 + tid;
+      const int e4 = u * NTH + tid;
       if (e4 >= tot / 4) continue;
 #pragma unroll
       for (int z = 0; z < 4; ++z) {
@@ -596,14 +602,14 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
 #pragma unroll
     for (int u = 0; u < DV; ++u) {
-      const int e = u * 256 + tid;
+      const int e = u * NTH + tid;
       if (e >= tot2) continue;
       const int r = (int)fdiv((uint32_t)e, a.fdH2), c2 = e - r * h2;
       DUs[r * LE + 2 * c2] = dv[u][0];
       DUs[r * LE + 2 * c2 + 1] = dv[u][1];
     }
   } else {
-    for (int e = tid; e < tot; e += 256) {
+    for (int e = tid; e < tot; e += NTH) {
       const int r = e / N, n = e - r * N;
       Us[r * LE + n] = gu[e];
       const int64_t R = R0 + r;
@@ -621,8 +627,8 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 #endif
   TF_MARK(1);
   TF_MARK(2);
-  // ---- A1. LayerNorm(N) backward of the wave's 12 rows at once (ln_bwd_kernel's arithmetic) --
-  float gp[NTW], bp[NTW], gsum[2], bsum[2];
+  // ---- A1. LayerNorm(N) backward of the wave's RPW rows at once (ln_bwd_kernel's arithmetic) --
+  float gp[NTW], bp[NTW], gsum[GJ], bsum[GJ];
   {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
@@ -630,11 +636,11 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       bp[j] = 0.f;
       if (l + 64 * j >= N) gl[j] = 0.f;
     }
-    float s32[2 * kTfRPW], xh[kTfRPW][NTW], dyv[kTfRPW][NTW];
-    float mean[kTfRPW], rsv[kTfRPW];
+    float s32[2 * RPW], xh[RPW][NTW], dyv[RPW][NTW];
+    float mean[RPW], rsv[RPW];
 #pragma unroll
-    for (int k = 0; k < kTfRPW; ++k) {
-      const int r = w + 4 * k;
+    for (int k = 0; k < RPW; ++k) {
+      const int r = w + W * k;
       mean[k] = __shfl(mu_l, k, 64);
       rsv[k] = __shfl(rs_l, k, 64);
       const bool live = r < nrows;
@@ -658,14 +664,14 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
         bp[j] += dyv[k][j];
       }
       s32[k] = s1;
-      s32[kTfRPW + k] = s2;
+      s32[RPW + k] = s2;
     }
     tf_wave_sums(s32);
 #pragma unroll
-    for (int k = 0; k < kTfRPW; ++k) {
-      const int r = w + 4 * k;
+    for (int k = 0; k < RPW; ++k) {
+      const int r = w + W * k;
       float* dur = DUs + r * LE;
-      const float s1 = s32[k] / N, s2 = s32[kTfRPW + k] / N;
+      const float s1 = s32[k] / N, s2 = s32[RPW + k] / N;
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
         const int n = l + 64 * j;
@@ -673,12 +679,37 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       }
     }
   }
-  __syncthreads();  // (every wave's reads of the u tile, which the Q|K|V tile overwrites)
+  __syncthreads();  // (every wave's reads of the u tile: its region takes the partials, then Q|K|V)
+  {  // gamma / beta: the W waves' partials summed in wave order (kept for the end)
+    float* red = Us;  // [2][W][NP] in the u tile's region (free now; <= 5 120 of its 14 016 floats)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = l + 64 * j;
+      if (n < NP) {
+        red[(0 * W + w) * NP + n] = gp[j];
+        red[(1 * W + w) * NP + n] = bp[j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) {  // n = tid + NTH j (N <= 320 < 512)
+      const int n = min(tid + NTH * j, NP - 1);
+      float g = red[n], b = red[W * NP + n];
+#pragma unroll
+      for (int v = 1; v < W; ++v) {
+        g += red[v * NP + n];
+        b += red[(W + v) * NP + n];
+      }
+      gsum[j] = g;
+      bsum[j] = b;
+    }
+    __syncthreads();
+  }
   {
     const int tot = nrows * (kTfQW / 4);
 #pragma unroll
     for (int u = 0; u <= QV4; ++u) {
-      const int e = u * 256 + tid;
+      const int e = u * NTH + tid;
       if (e < tot) {
         const int r = e / (kTfQW / 4), c4 = e - r * (kTfQW / 4);
         *reinterpret_cast<floatx4*>(Qs + r * kTfLQ + 4 * c4) = qv[u];
@@ -686,29 +717,10 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
   TF_MARK(3);
-  {  // gamma / beta: the four waves' partials summed in wave order (kept for the end)
-    float* red = Cs;  // [2][4][NP] (Cs is free until phase B's epilogue)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int n = l + 64 * j;
-      if (n < NP) {
-        red[(0 * 4 + w) * NP + n] = gp[j];
-        red[(1 * 4 + w) * NP + n] = bp[j];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {  // n = tid + 256 j (N <= 320 < 512)
-      const int n = min(tid + 256 * j, NP - 1);
-      gsum[j] = ((red[0 * NP + n] + red[1 * NP + n]) + red[2 * NP + n]) + red[3 * NP + n];
-      bsum[j] = ((red[4 * NP + n] + red[5 * NP + n]) + red[6 * NP + n]) + red[7 * NP + n];
-    }
-    __syncthreads();
-  }
   TF_MARK(4);
 
   // ---- B. dctx = dU W_fc  (48 x h dv, contraction over the NP nodes) -----------------------
-  {
+  if (w < 4) {  // (wave-uniform)
     constexpr int CT = kTfHV / 16;          // 6 column tiles x 3 row tiles
     floatx4 acc[3][2];                      // wave w: columns {w, w + 4} (waves 2, 3: one + a duplicate)
 #pragma unroll
@@ -733,7 +745,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 
   // the dx tile of D1's epilogue (inner block), issued now: it lands during C and D1
   float4 dxo[3][NTW];
-  if (a.dx) {
+  if (a.dx && w < 4) {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int n = min((w + 4 * j) * 16 + i, N - 1);
@@ -749,7 +761,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   // ---- C. attention backward per (problem, head) (tat_bwd_mfma_kernel's math) ---------------
 #pragma unroll
   for (int k = 0; k < TPW; ++k) {
-    const int task = w + 4 * k;
+    const int task = w + W * k;
     // (continue, not break: a break leaves the loop not fully unrolled and the per-task register
     // arrays rr / at / dr dynamically indexed — readlane / cndmask chains, measured 2x slower)
     if (task >= NTASK || (task / kTfH) * T >= nrows) continue;  // (wave-uniform)
@@ -846,7 +858,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   TF_MARK(6);
 
   // ---- D1. dE = dU + dqkv [Wq; Wk; Wv] ---------------------------------------------------
-  {
+  if (w < 4) {  // (wave-uniform)
     const int NT = NP / 16;
     floatx4 acc[3][NTW];
 #pragma unroll
@@ -885,10 +897,10 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
 
   TF_MARK(8);
   // ---- E. the saved tiles and partials (stores last: see tf_copy_out) ----------------------
-  tf_copy_out(a.dqkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
+  tf_copy_out<NTH>(a.dqkv + R0 * kTfQW, Qs, nrows, kTfQW, kTfLQ, tid);
   if (((nrows * N) & 3) == 0) {  // dU: the workgroup's rows are one contiguous block (float4)
     float4* g4 = reinterpret_cast<float4*>(a.dU + R0 * N);
-    for (int e4 = tid; e4 < nrows * N / 4; e4 += 256) {
+    for (int e4 = tid; e4 < nrows * N / 4; e4 += NTH) {
       float vv[4];
 #pragma unroll
       for (int z = 0; z < 4; ++z) {
@@ -898,15 +910,15 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
       g4[e4] = make_float4(vv[0], vv[1], vv[2], vv[3]);
     }
   } else {
-    for (int e = tid; e < nrows * N; e += 256) {
+    for (int e = tid; e < nrows * N; e += NTH) {
       const int r = e / N, n = e - r * N;
       a.dU[R0 * N + e] = DUs[r * LE + n];
     }
   }
   const bool lnf = a.ln_fold != 0;  // gamma / beta summed in-kernel by a two-level ticket tree
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = tid + 256 * j;
+  for (int j = 0; j < GJ; ++j) {
+    const int n = tid + NTH * j;
     if (n < N) {
       if (lnf) {
         tf_st_agent(a.gpart + (int64_t)blockIdx.x * N + n, gsum[j]);
@@ -918,11 +930,11 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
     }
   }
   const int np = nrows / T;
-  if (a.res_mode == DSTAGNN_RES_FULL && a.dres) tf_copy_out(a.dres + P0 * kTfH * T * T, DSs, 1, np * kTfH * T * T, 0, tid);
+  if (a.res_mode == DSTAGNN_RES_FULL && a.dres) tf_copy_out<NTH>(a.dres + P0 * kTfH * T * T, DSs, 1, np * kTfH * T * T, 0, tid);
   const int nch = (int)(a.FT / kTfRows);
   const int64_t bwg = (uint32_t)R0 / (uint32_t)a.FT, chw = ((uint32_t)R0 - (uint32_t)bwg * (uint32_t)a.FT) / kTfRows;
   if (a.res_mode == DSTAGNN_RES_BCAST) {
-    for (int e = tid; e < kTfH * T * T; e += 256) {
+    for (int e = tid; e < kTfH * T * T; e += NTH) {
       float v = 0.f;
       for (int p = 0; p < PW; ++p) v += DSs[p * kTfH * T * T + e];  // problems in order
       tf_st_agent(a.dpart + (bwg * nch + chw) * kTfH * T * T + e, v);
@@ -959,7 +971,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   __syncthreads();
   const bool lb = flag[0] != 0, lg = flag[1] != 0;
   if (lb) {
-    for (int e = tid; e < kTfH * T * T; e += 256) {
+    for (int e = tid; e < kTfH * T * T; e += NTH) {
       float v = 0.f;
       for (int ch = 0; ch < nch; ++ch) v += tf_ld_agent(a.dpart + (bwg * nch + ch) * kTfH * T * T + e);
       a.dres[bwg * kTfH * T * T + e] = v;
@@ -968,7 +980,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   if (!lg) return;
   float* l2g = a.gpart + (int64_t)nwg * N;  // level-2 rows [ng][N] after the level-1 rows (slab of BFT x N)
   float* l2b = a.bpart + (int64_t)nwg * N;
-  for (int e = tid; e < 2 * N; e += 256) {  // (column, gamma | beta): the group's rows in order
+  for (int e = tid; e < 2 * N; e += NTH) {  // (column, gamma | beta): the group's rows in order
     const int n = e % N, wh = e / N;
     const float* src = (wh ? a.bpart : a.gpart) + (int64_t)g1 * kTfG1 * N + n;
     float u[kTfG1];
@@ -992,7 +1004,7 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   }
   __syncthreads();
   if (!flag[2]) return;
-  for (int e = tid; e < 2 * N; e += 256) {
+  for (int e = tid; e < 2 * N; e += NTH) {
     const int n = e % N, wh = e / N;
     float* out = wh ? a.bout : a.gout;
     if (!out) continue;
@@ -1009,9 +1021,9 @@ __global__ __launch_bounds__(256, 1) void tat_fused_bwd_kernel(TatFusedBwdArgs a
   }
 }
 
-size_t tat_fused_bwd_lds(int NP) {
-  return sizeof(float) * ((size_t)kTfRows * (NP + 4) + (size_t)kTfRows * kTfLQ + (size_t)kTfRows * kTfLC + 4 * 16 * 17 +
-                          kTfDsMax + 4);
+size_t tat_fused_bwd_lds(int NP, int W) {
+  return sizeof(float) * ((size_t)kTfRows * (NP + 4) + (size_t)kTfRows * kTfLQ + (size_t)kTfRows * kTfLC +
+                          (size_t)W * 16 * 17 + kTfDsMax + 4);
 }
 
 }  // namespace
@@ -1123,21 +1135,27 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
   a.sig = sg.p;
   a.sig_v = sg.v;
   const int64_t grid = cdiv64(a.BFT, kTfRows);
-  const size_t lds = tat_fused_bwd_lds(a.NP);
+  // DSTAGNN_TF_BWD_WAVES=4|8: the backward's workgroup size (A/B)
+  static const int waves = getenv("DSTAGNN_TF_BWD_WAVES") && atoi(getenv("DSTAGNN_TF_BWD_WAVES")) == 4 ? 4 : 8;
+  // (NP > 256 stays on four waves: eight would spill — 256 VGPRs each at two waves per SIMD)
+  const int wv = waves == 8 && (a.NP / 16 + 3) / 4 < 5 ? 8 : 4;
+  const size_t lds = tat_fused_bwd_lds(a.NP, wv);
   const int ntw = (a.NP / 16 + 3) / 4;
   const double flops = 2.0 * a.BFT * (double)a.N * kTfHV + 2.0 * a.BFT * (double)kTfQW * a.N +
                        8.0 * (a.BFT / a.T) * kTfH * (double)a.T * a.T * kTfD;
   const double bytes = 4.0 * a.BFT * (4.0 * a.N + 2.0 * kTfQW + 2.0 * kTfH * a.T) + 8.0 * kTfQW * a.NP;
   using Kern = void (*)(TatFusedBwdArgs);
   Kern k = nullptr;
-#define TB_T(TT)                                          \
-  switch (ntw) {                                          \
-    case 1: k = tat_fused_bwd_kernel<TT, 1>; break;       \
-    case 2: k = tat_fused_bwd_kernel<TT, 2>; break;       \
-    case 3: k = tat_fused_bwd_kernel<TT, 3>; break;       \
-    case 4: k = tat_fused_bwd_kernel<TT, 4>; break;       \
-    default: k = tat_fused_bwd_kernel<TT, 5>; break;      \
-  }                                                       \
+#define TB_NTW(TT, WW)                                        \
+  switch (ntw) {                                              \
+    case 1: k = tat_fused_bwd_kernel<TT, 1, WW>; break;       \
+    case 2: k = tat_fused_bwd_kernel<TT, 2, WW>; break;       \
+    case 3: k = tat_fused_bwd_kernel<TT, 3, WW>; break;       \
+    case 4: k = tat_fused_bwd_kernel<TT, 4, WW>; break;       \
+    default: k = tat_fused_bwd_kernel<TT, 5, WW>; break;      \
+  }
+#define TB_T(TT)                                              \
+  if (wv == 8) { TB_NTW(TT, 8) } else { TB_NTW(TT, 4) }   \
   break;
   switch (a.T) {
     case 8: TB_T(8)
@@ -1145,6 +1163,7 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
     default: TB_T(16)
   }
 #undef TB_T
+#undef TB_NTW
   if (lds > 64 * 1024) {
     static std::mutex mu;
     static std::set<Kern> done;
@@ -1156,7 +1175,7 @@ int op_tat_fused_bwd(const TatFusedBwdArgs& a0, hipStream_t st) {
     }
   }
   void* rec = gemm_prof_begin(flops, bytes, st, DSTAGNN_PROF_TAT_FUSED_BWD);
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wv), lds, st, a);
   DS_CHECK_LAUNCH();
   if (sg.p) DS_TRY(stream_sig_sent(st, sg));
   gemm_prof_end(rec, st);
