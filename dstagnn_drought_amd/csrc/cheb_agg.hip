@@ -331,6 +331,132 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<k
 }
 
 // ---------------------------------------------------------------------------------------
+// backward SDDMM for T <= 16 (F T <= 512): one wave per (sample PAIR, j).  The two samples' g_j
+// rows stack into one 32-row MFMA operand (m = bsel T + t: 2 T <= 32 rows of the 32 x 32 tile,
+// where a single sample used T of them), so one chain of 16 MFMAs per order makes both samples'
+// dagg_k; the column's support indices and weights are loaded once for both.  The support walk
+// runs over virtual entries v = 2 e + bsel (sample bsel of entry e; batches of kE = 4 start at
+// multiples of 4, so a value's sample is e & 1 at compile time).  Half the waves of the one-
+// sample kernel, each with the same dependent load chain: PEMS08 B = 32 gives 2 720 waves, one
+// round at 3 waves per SIMD, where 5 440 took two.  Same arithmetic per entry and order as the
+// one-sample kernel (same dot-product order, same reduction): results bit-identical.
+// ---------------------------------------------------------------------------------------
+template <int kNQ, int KM>  // kNQ >= F * T / 64 (<= 8)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sddmm_wpe<kNQ, KM, true>(), 8))) void cheb_agg_sddmm2_kernel(ChebAg a) {
+  static_assert(kNQ <= 8, "F T <= 512");
+  extern __shared__ float Dg[];  // [waves][2][K][F * T]
+  stream_sig_store(a.sig, a.sig_v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
+  const int npair = (a.B + 1) >> 1;
+  if (wv >= (int64_t)npair * a.N) return;
+  const int bp = (int)(wv / a.N), j = (int)(wv % a.N), b0 = 2 * bp, nb = min(2, a.B - b0);
+  const int T = a.T, FT = a.F * T;
+  float* dg = Dg + (int64_t)w * 2 * a.K * FT;
+  const int64_t NN = (int64_t)a.N * a.N;
+  const int p0 = a.csc_ptr[j], p1 = a.csc_ptr[j + 1];
+  {
+    // A[m][kk = c] = g_{b0 + bsel}[t][c], m = bsel T + t, kk = 16h + s
+    const int bs = l32 >= T ? 1 : 0, tl = l32 - bs * T;
+    const bool mv = l32 < nb * T;
+    float gv[16];
+    row16(a.g + (((int64_t)(b0 + (mv ? bs : 0)) * a.N + j) * T + (mv ? tl : 0)) * a.C + 16 * h, mv && 16 * h < a.C, gv);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k >= a.K) break;
+      float bt[16];  // B[kk = c][n = f] = Theta_k[f][c]
+      row16(a.thcat + (int64_t)min(l32, a.F - 1) * a.KC + k * a.C + 16 * h, l32 < a.F && 16 * h < a.C, bt);
+      floatx16 acc = zero16();
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(gv[s], bt[s], acc, 0, 0, 0);
+      if (l32 < a.F) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = frow(r, h), ms = m >= T ? 1 : 0, mt = m - ms * T;
+          if (m < nb * T) dg[(int64_t)(ms * a.K + k) * FT + l32 * T + mt] = acc[r];  // [bsel][k][f][t]
+        }
+      }
+    }
+  }
+  wave_lds_sync();
+  const float* xb0 = a.x + (int64_t)b0 * a.N * FT;
+  const float* xb1 = a.x + (int64_t)(b0 + nb - 1) * a.N * FT;
+  constexpr int NV0 = KM * kE, NV = NV0 <= 16 ? 16 : (NV0 <= 32 ? 32 : 64);
+  constexpr int LG = NV == 16 ? 4 : (NV == 32 ? 5 : 6);
+  const int jl = (lane >> (6 - LG)) & (NV - 1), kl = jl / kE, el = jl - kl * kE, bsl = el & 1;
+  const bool owner = (lane & ((64 >> LG) - 1)) == 0 && jl < NV0 && kl < a.K && bsl < nb;
+  float csum = 0.f;  // this lane's share of c_j for (order kl, sample b0 + bsl)
+  for (int c0 = p0; c0 < p1; c0 += 32) {  // 32 entries = 64 virtual entries per chunk
+    const int nc = min(32, p1 - c0), nv = 2 * nc;
+    const int rowl = a.csc_row[c0 + min(lane, nc - 1)];
+    auto gather = [&](int e0, float (&dst)[kE][kNQ]) {
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const int ve = min(e0 + e, nv - 1);  // (e0 even: ve & 1 == e & 1 unless clamped)
+        const float* xr = ((e & 1) ? xb1 : xb0) + (int64_t)rl_i(rowl, ve >> 1) * FT;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) dst[e][q] = xr[min(lane + 64 * q, FT - 1)];
+      }
+    };
+    float v[kE][kNQ];
+    gather(0, v);
+    for (int e0 = 0; e0 < nv; e0 += kE) {
+      float vn[kE][kNQ];
+      gather(e0 + kE, vn);  // the next batch, in flight meanwhile
+      float sf[NV];
+#pragma unroll
+      for (int jj = 0; jj < NV; ++jj) sf[jj] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        if (k >= a.K) break;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) {
+          const int el2 = lane + 64 * q;
+          const float d0 = el2 < FT ? dg[(int64_t)k * FT + el2] : 0.f;
+          const float d1 = el2 < FT ? dg[(int64_t)(a.K + k) * FT + el2] : 0.f;
+#pragma unroll
+          for (int e = 0; e < kE; ++e) sf[k * kE + e] = fmaf(v[e][q], (e & 1) ? d1 : d0, sf[k * kE + e]);
+        }
+      }
+      const int ve = e0 + el, p = c0 + (ve >> 1);
+      const bool mine = owner && ve < nv;
+      const int64_t zk = ((int64_t)(b0 + bsl) * a.K + kl) * a.nnz;
+      float ps = 0.f, ts = 0.f;
+      if (mine && a.dzs) {
+        ps = a.psupp[zk + p];
+        ts = a.tsupp[(int64_t)kl * a.nnz + p];
+      }
+      const float sv = wave_sum_many<NV>(sf);
+      if (mine) {
+        if (a.dzs) {
+          const float dd = ps * (ts * sv);
+          csum += dd;
+          a.dzs[zk + p] = dd;
+          if (a.dzs_r) a.dzs_r[zk + a.csc2csr[p]] = dd;
+        } else {
+          a.dW[((int64_t)(b0 + bsl) * a.K + kl) * NN + (int64_t)a.csc_row[p] * a.N + j] = sv;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < kE; ++e)
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) v[e][q] = vn[e][q];
+    }
+  }
+  if (a.dzs) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k >= a.K) break;
+#pragma unroll
+      for (int bs = 0; bs < 2; ++bs) {
+        const float c = wave_sum(owner && kl == k && bsl == bs ? csum : 0.f);
+        if (lane == 0 && bs < nb) a.cc[((int64_t)(b0 + bs) * a.K + k) * a.N + j] = c;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // backward transposed SpMM: one wave per (b, i, time chunk).  The row's neighbours g_j are
 // gathered once: h_k = sum_{j in supp_row(i)} W_k[i,j] g_j (Tc x C) for every k, then
 // dx_i[f, t'] += sum_k sum_c Theta_k[f][c] h_k[t'][c] on the matrix cores.
@@ -511,6 +637,22 @@ struct SddmmL {
   }
 };
 template <int NQ, int KM>
+struct Sddmm2L {
+  static void run(const Launch& l) {
+    if constexpr (NQ <= 8) {
+      if (l.lds > (64u << 10)) {
+        static bool done = false;
+        if (!done) {
+          (void)hipFuncSetAttribute((const void*)cheb_agg_sddmm2_kernel<NQ, KM>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+          done = true;
+        }
+      }
+      hipLaunchKernelGGL((cheb_agg_sddmm2_kernel<NQ, KM>), l.grid, dim3(256), l.lds, l.st, l.a);
+    }
+  }
+};
+template <int NQ, int KM>
 struct SpmmTL {
   static void run(const Launch& l) {
     hipLaunchKernelGGL((cheb_agg_spmm_t_kernel<NQ, KM>), l.grid, dim3(256), 0, l.st, l.a);
@@ -555,8 +697,18 @@ int op_cheb_agg_sddmm(const ChebAg& a0, hipStream_t st) {
   a.sig = sg.p;
   a.sig_v = sg.v;
   const int FT = a.F * a.T;
-  const size_t lds = sddmm_lds_bytes(a.K, a.F, a.T);
-  dispatch<SddmmL>(nq_of(std::min(FT, 1024)), km_of(a.K), Launch{a, dim3(grid_rows((int64_t)a.B * a.N)), lds, st});
+  // T <= 16: sample pairs per wave (cheb_agg_sddmm2_kernel; DSTAGNN_SDDMM_PAIR=0: one sample)
+  // (DSTAGNN_SDDMM_NOPF=1 names a variant of the one-sample kernel: it implies PAIR=0)
+  static const bool pair_env = (!getenv("DSTAGNN_SDDMM_PAIR") || atoi(getenv("DSTAGNN_SDDMM_PAIR")) != 0) &&
+                               !(getenv("DSTAGNN_SDDMM_NOPF") && atoi(getenv("DSTAGNN_SDDMM_NOPF")) != 0);
+  const bool pair = pair_env && a.T <= 16 && FT <= 512 && 2 * sddmm_lds_bytes(a.K, a.F, a.T) <= (160u << 10);
+  if (pair) {
+    dispatch<Sddmm2L>(nq_of(FT), km_of(a.K),
+                      Launch{a, dim3(grid_rows((int64_t)((a.B + 1) / 2) * a.N)), 2 * sddmm_lds_bytes(a.K, a.F, a.T), st});
+  } else {
+    const size_t lds = sddmm_lds_bytes(a.K, a.F, a.T);
+    dispatch<SddmmL>(nq_of(std::min(FT, 1024)), km_of(a.K), Launch{a, dim3(grid_rows((int64_t)a.B * a.N)), lds, st});
+  }
   DS_CHECK_LAUNCH();
   if (sg.p) DS_TRY(stream_sig_sent(st, sg));
   return 0;
