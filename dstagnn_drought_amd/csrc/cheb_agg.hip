@@ -201,6 +201,127 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<
 }
 
 // ---------------------------------------------------------------------------------------
+// forward for T <= 16 (F T <= 512): one wave per (sample PAIR, j), as the pair SDDMM below.  The
+// support walk runs over virtual entries v = 2 e + bsel (sample bsel of entry e), accumulating
+// sample bsel's aggregates ag[bsel]; the two samples' agg_k then stack into one MFMA A operand
+// (m = bsel T + t), so the Theta_k chain of 16 MFMAs serves both.  Per sample the same sums in
+// the same order as cheb_agg_fwd_kernel (entries in support order, orders k separately).
+// ---------------------------------------------------------------------------------------
+template <int kNQ, int KM>  // kNQ >= F * T / 64 (<= 8), KM >= K
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<kNQ, 2 * KM>(), 8))) void cheb_agg_fwd2_kernel(ChebAg a) {
+  static_assert(kNQ <= 8, "F T <= 512");
+  __shared__ float As[4][32 * kAs];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
+  const int npair = (a.B + 1) >> 1;
+  if (wv >= (int64_t)npair * a.N) return;
+  const int bp = (int)(wv / a.N), j = (int)(wv % a.N), b0 = 2 * bp, nb = min(2, a.B - b0);
+  const int T = a.T, FT = a.F * T;
+  const int64_t NN = (int64_t)a.N * a.N;
+  float* at = As[w];
+  // this lane's elements e = lane + 64 q of a sample's (F x T) block: (f, t), x offset = e
+  int lo[kNQ];
+#pragma unroll
+  for (int q = 0; q < kNQ; ++q) {
+    const int e = min(lane + 64 * q, FT - 1), f = e / T, tl = e - f * T;
+    lo[q] = f * kAs + tl;  // LDS tile [f][m], m = bsel T + t (+ T for sample 1)
+  }
+  const int p0 = a.csc_ptr[j], p1 = a.csc_ptr[j + 1];
+  const float* xb0 = a.x + (int64_t)b0 * a.N * FT;
+  const float* xb1 = a.x + (int64_t)(b0 + nb - 1) * a.N * FT;
+  float ag[2][KM][kNQ];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q) ag[s][k][q] = 0.f;
+  for (int c0 = p0; c0 < p1; c0 += 32) {  // 32 entries = 64 virtual entries per chunk
+    const int nc = min(32, p1 - c0), nv = 2 * nc, pl = c0 + min(lane, nc - 1);
+    const int rowl = a.csc_row[pl];
+    float wl[2][KM];  // W_k[row, j] of this lane's entry for each sample (0 past the chunk)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        float ww = 0.f;
+        if (k < a.K) {
+          const int b = b0 + min(s, nb - 1);
+          const int64_t o = (int64_t)rowl * a.N + j;
+          ww = a.wsupp ? a.wsupp[((int64_t)b * a.K + k) * a.nnz + pl]
+                       : a.cheb[(int64_t)k * NN + o] * a.P[((int64_t)b * a.K + k) * NN + o];
+        }
+        wl[s][k] = lane < nc ? ww : 0.f;
+      }
+    auto gather = [&](int e0, float (&dst)[kE][kNQ]) {
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const int ve = min(e0 + e, nv - 1);  // (e0 even: ve & 1 == e & 1 unless clamped)
+        const float* xr = ((e & 1) ? xb1 : xb0) + (int64_t)rl_i(rowl, ve >> 1) * FT;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) dst[e][q] = xr[min(lane + 64 * q, FT - 1)];
+      }
+    };
+    float v[kE][kNQ];
+    gather(0, v);
+    for (int e0 = 0; e0 < nv; e0 += kE) {
+      float vn[kE][kNQ];
+      gather(e0 + kE, vn);  // the next batch (clamped: harmless re-reads past the chunk)
+#pragma unroll
+      for (int k = 0; k < KM; ++k)
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          // entry (e0 + e) / 2 of sample e & 1; past the chunk: lane >= nc holds 0 (e0 + e <= 63)
+          const float wk = rl_f(wl[e & 1][k], min((e0 + e) >> 1, 31));
+          const float wz = e0 + e < nv ? wk : 0.f;
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) ag[e & 1][k][q] = fmaf(wz, v[e][q], ag[e & 1][k][q]);
+        }
+#pragma unroll
+      for (int e = 0; e < kE; ++e)
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) v[e][q] = vn[e][q];
+    }
+  }
+  floatx16 acc = zero16();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (k >= a.K) break;
+    float bt[16];  // Theta_k as the B operand: B[kk = f][n = c], f = 2s + h (zero past F / C)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int f = 2 * s + h;
+      bt[s] = (f < a.F && l32 < a.C) ? a.thcat[(int64_t)f * a.KC + k * a.C + l32] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s >= nb) break;
+      float* sv = a.agg + (((int64_t)(b0 + s) * a.N + j) * a.K + k) * FT;  // agg_k[j], saved for dTheta
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q)
+        if (lane + 64 * q < FT) {
+          sv[lane + 64 * q] = ag[s][k][q];
+          at[lo[q] + s * T] = ag[s][k][q];
+        }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {  // D[m][n = c] += sum_f agg_k[f][m] Theta_k[f][c]
+      const int f = 2 * s + h;
+      const float av = (f < a.F && l32 < nb * T) ? at[f * kAs + l32] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bt[s], acc, 0, 0, 0);
+    }
+    wave_lds_sync();
+  }
+  if (l32 >= a.C) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = frow(r, h), ms = m >= T ? 1 : 0, mt = m - ms * T;
+    if (m < nb * T) a.X[(((int64_t)(b0 + ms) * a.N + j) * T + mt) * a.C + l32] = fmaxf(acc[r], 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // backward SDDMM: one wave per (b, j).  dagg_k = Theta_k g_j^T (F x T) for every k on the
 // wave's matrix cores into LDS, then the column's support rows x_i gathered ONCE and dotted
 // with all K: dW_k[i, j] = <x_i, dagg_k> (flash path: the softmax backward's support terms
@@ -560,6 +681,121 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// transposed SpMM for T <= 16 (T C <= 512): one wave per (sample PAIR, i), as the pair forward:
+// h_k of sample bsel accumulated over virtual entries v = 2 e + bsel of the row's support, the
+// two samples' h_k stacked into one MFMA A operand (m = bsel T + t) for the Theta_k chain.
+// ---------------------------------------------------------------------------------------
+template <int kNQ, int KM>  // kNQ >= T * C / 64 (<= 8)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_wpe<kNQ, 2 * KM>(), 8))) void cheb_agg_spmm_t2_kernel(ChebAg a) {
+  static_assert(kNQ <= 8, "T C <= 512");
+  __shared__ float Hs[4][32 * kAs];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int64_t wv = xcd_block(a.xcd_order) * 4 + w;
+  const int npair = (a.B + 1) >> 1;
+  if (wv >= (int64_t)npair * a.N) return;
+  const int bp = (int)(wv / a.N), i = (int)(wv % a.N), b0 = 2 * bp, nb = min(2, a.B - b0);
+  const int T = a.T, TC = T * a.C;
+  const int64_t NN = (int64_t)a.N * a.N;
+  float* hs = Hs[w];
+  int lo[kNQ];  // element e = lane + 64 q of a g row (t, c): LDS slot [m = t][c] (+ T rows for sample 1)
+#pragma unroll
+  for (int q = 0; q < kNQ; ++q) {
+    const int e = min(lane + 64 * q, TC - 1), tl = e / a.C, c = e - tl * a.C;
+    lo[q] = tl * kAs + c;
+  }
+  const int q0 = a.csr_ptr[i], q1 = a.csr_ptr[i + 1];
+  const float* gb0 = a.g + (int64_t)b0 * a.N * TC;
+  const float* gb1 = a.g + (int64_t)(b0 + nb - 1) * a.N * TC;
+  float hv[2][KM][kNQ];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q) hv[s][k][q] = 0.f;
+  for (int c0 = q0; c0 < q1; c0 += 32) {
+    const int nc = min(32, q1 - c0), nv = 2 * nc, pl = c0 + min(lane, nc - 1);
+    const int coll = a.csr_col[pl];
+    float wl[2][KM];
+    {
+      const int ci = a.wsupp ? a.csr2csc[pl] : 0;
+      const int64_t o = (int64_t)i * a.N + coll;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          float ww = 0.f;
+          if (k < a.K) {
+            const int b = b0 + min(s, nb - 1);
+            ww = a.wsupp ? a.wsupp[((int64_t)b * a.K + k) * a.nnz + ci]
+                         : a.cheb[(int64_t)k * NN + o] * a.P[((int64_t)b * a.K + k) * NN + o];
+          }
+          wl[s][k] = lane < nc ? ww : 0.f;
+        }
+    }
+    auto gather = [&](int e0, float (&dst)[kE][kNQ]) {
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const int ve = min(e0 + e, nv - 1);
+        const float* gr = ((e & 1) ? gb1 : gb0) + (int64_t)rl_i(coll, ve >> 1) * TC;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) dst[e][q] = gr[min(lane + 64 * q, TC - 1)];
+      }
+    };
+    float v[kE][kNQ];
+    gather(0, v);
+    for (int e0 = 0; e0 < nv; e0 += kE) {
+      float vn[kE][kNQ];
+      gather(e0 + kE, vn);
+#pragma unroll
+      for (int k = 0; k < KM; ++k)
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          const float wk = rl_f(wl[e & 1][k], min((e0 + e) >> 1, 31));
+          const float wz = e0 + e < nv ? wk : 0.f;
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) hv[e & 1][k][q] = fmaf(wz, v[e][q], hv[e & 1][k][q]);
+        }
+#pragma unroll
+      for (int e = 0; e < kE; ++e)
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) v[e][q] = vn[e][q];
+    }
+  }
+  floatx16 acc = zero16();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (k >= a.K) break;
+    float bt[16];  // B[kk = c][n = f] = Theta_k[f][c], kk = 16h + s
+    row16(a.thcat + (int64_t)min(l32, a.F - 1) * a.KC + k * a.C + 16 * h, l32 < a.F && 16 * h < a.C, bt);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s >= nb) break;
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q)
+        if (lane + 64 * q < TC) hs[lo[q] + s * T * kAs] = hv[s][k][q];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {  // D[m][n = f] += sum_c h_k[m][c] Theta_k[f][c]
+      const int c = 16 * h + s;
+      const float av = (c < a.C && l32 < nb * T) ? hs[l32 * kAs + c] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bt[s], acc, 0, 0, 0);
+    }
+    wave_lds_sync();
+  }
+  if (l32 >= a.F) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = frow(r, h), ms = m >= T ? 1 : 0, mt = m - ms * T;
+    if (m < nb * T) {
+      float* d = a.dx + ((int64_t)(b0 + ms) * a.N + i) * a.F * T + (int64_t)l32 * T + mt;
+      *d = a.dx_beta * *d + acc[r];
+    }
+  }
+}
+
 int nq_of(int n) { return n <= 64 ? 1 : n <= 128 ? 2 : n <= 256 ? 4 : n <= 384 ? 6 : n <= 512 ? 8 : n <= 768 ? 12 : 16; }
 int km_of(int K) { return K <= 2 ? 2 : K <= 3 ? 3 : K <= 5 ? 5 : 8; }
 
@@ -608,6 +844,12 @@ struct FwdL {
   }
 };
 template <int NQ, int KM>
+struct Fwd2L {
+  static void run(const Launch& l) {
+    if constexpr (NQ <= 8) hipLaunchKernelGGL((cheb_agg_fwd2_kernel<NQ, KM>), l.grid, dim3(256), 0, l.st, l.a);
+  }
+};
+template <int NQ, int KM>
 struct SddmmL {
   static void run(const Launch& l) {
     if (l.lds > (64u << 10)) {
@@ -653,6 +895,12 @@ struct Sddmm2L {
   }
 };
 template <int NQ, int KM>
+struct SpmmT2L {
+  static void run(const Launch& l) {
+    if constexpr (NQ <= 8) hipLaunchKernelGGL((cheb_agg_spmm_t2_kernel<NQ, KM>), l.grid, dim3(256), 0, l.st, l.a);
+  }
+};
+template <int NQ, int KM>
 struct SpmmTL {
   static void run(const Launch& l) {
     hipLaunchKernelGGL((cheb_agg_spmm_t_kernel<NQ, KM>), l.grid, dim3(256), 0, l.st, l.a);
@@ -684,8 +932,13 @@ bool cheb_agg_ok(int F, int C, int K, int T) {
 int op_cheb_agg_fwd(const ChebAg& a0, hipStream_t st) {
   DS_TRY(check(a0));
   const ChebAg a = with_order(a0);
-  dispatch<FwdL>(nq_of(a.F * std::min(32, a.T)), km_of(a.K),
-                 Launch{a, dim3(grid_rows((int64_t)a.B * a.N), (unsigned)cdiv64(a.T, 32)), 0, st});
+  // T <= 16: sample pairs per wave (cheb_agg_fwd2_kernel; DSTAGNN_AGG_PAIR=0: one sample)
+  static const bool pair_env = !getenv("DSTAGNN_AGG_PAIR") || atoi(getenv("DSTAGNN_AGG_PAIR")) != 0;
+  if (pair_env && a.T <= 16 && a.F * a.T <= 512)
+    dispatch<Fwd2L>(nq_of(a.F * a.T), km_of(a.K), Launch{a, dim3(grid_rows((int64_t)((a.B + 1) / 2) * a.N)), 0, st});
+  else
+    dispatch<FwdL>(nq_of(a.F * std::min(32, a.T)), km_of(a.K),
+                   Launch{a, dim3(grid_rows((int64_t)a.B * a.N), (unsigned)cdiv64(a.T, 32)), 0, st});
   DS_CHECK_LAUNCH();
   return 0;
 }
@@ -717,6 +970,12 @@ int op_cheb_agg_sddmm(const ChebAg& a0, hipStream_t st) {
 int op_cheb_agg_spmm_t(const ChebAg& a0, hipStream_t st) {
   DS_TRY(check(a0));
   const ChebAg a = with_order(a0);
+  static const bool pair_env = !getenv("DSTAGNN_AGG_PAIR") || atoi(getenv("DSTAGNN_AGG_PAIR")) != 0;
+  if (pair_env && a.T <= 16 && a.T * a.C <= 512) {  // sample pairs per wave (cheb_agg_spmm_t2_kernel)
+    dispatch<SpmmT2L>(nq_of(a.T * a.C), km_of(a.K), Launch{a, dim3(grid_rows((int64_t)((a.B + 1) / 2) * a.N)), 0, st});
+    DS_CHECK_LAUNCH();
+    return 0;
+  }
   dispatch<SpmmTL>(nq_of(std::min(32, a.T) * a.C), km_of(a.K),
                    Launch{a, dim3(grid_rows((int64_t)a.B * a.N), (unsigned)cdiv64(a.T, 32)), 0, st});
   DS_CHECK_LAUNCH();

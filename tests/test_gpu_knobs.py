@@ -9,6 +9,8 @@ a subprocess (the library reads its switches once per process):
   DSTAGNN_SDDMM_NOPF=1 the aggregate-first SDDMM without its batch prefetch (4 waves per SIMD)
   DSTAGNN_SDDMM_PAIR=0 the aggregate-first SDDMM one sample per wave instead of sample pairs
                        (=1 with B = 3: the default pair kernel with an odd batch, a lone last sample)
+  DSTAGNN_AGG_PAIR=0   the aggregate-first forward and transposed SpMM one sample per wave instead
+                       of sample pairs (=1 with B = 3: the pair kernels with a lone last sample)
   DSTAGNN_TF_WAVES=4 / DSTAGNN_TF_BWD_WAVES=4  the fused temporal-attention kernels on four waves
                        instead of eight
   DSTAGNN_GTU_TCONV=0  the GTU input gradient as the K-concatenated GEMM (run_gemm_kcat)
@@ -69,6 +71,7 @@ print("KNOB_OK")
                                        ("DSTAGNN_SIDE_CUMASK=0x11111111", "pems08", 4),
                                        ("DSTAGNN_SDDMM_NOPF=1", "pems08", 4), ("DSTAGNN_GTU_TCONV=0", "pems08", 4),
                                        ("DSTAGNN_SDDMM_PAIR=0", "pems08", 4), ("DSTAGNN_SDDMM_PAIR=1", "pems08", 3),
+                                       ("DSTAGNN_AGG_PAIR=0", "pems08", 4), ("DSTAGNN_AGG_PAIR=1", "pems08", 3),
                                        ("DSTAGNN_TF_WAVES=4", "pems08", 4), ("DSTAGNN_TF_BWD_WAVES=4", "pems08", 4),
                                        ("DSTAGNN_GTU_GCONV=1", "pems08", 4), ("DSTAGNN_GTU_GCONV=1", "t24", 2),
                                        ("DSTAGNN_TAIL_CT24=0", "t24", 2), ("DSTAGNN_KSIG=0", "pems08", 4),
