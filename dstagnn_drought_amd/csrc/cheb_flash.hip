@@ -688,6 +688,161 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
+// the same dK' / dQ' for N <= 192 (nt <= 6) with TWO strips per workgroup: waves 2 hw + s take
+// strip s's tiles hw, hw + 2, ... (nt / 2 each at nt = 6: 3 tile units per wave, where one strip
+// over four waves left two waves with 2 tiles and two with 1).  The staged rows (all N rows of
+// Q' resp. K' of the (b, k)) serve both strips.  Half the workgroups: PEMS08's 576 fit one
+// wave round (3 per CU) where 1 152 took two.  Per strip the same products and the same
+// summation order as flash_small_dqk_kernel except the dense partials, summed over the strip's
+// two waves instead of four (tile order hw, hw + 2, ... per wave).
+constexpr int kStripE2 = 1024;  // sparse entries of a strip pair staged in LDS
+template <int TPW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flash_small_dqk2_kernel(ChebFl a) {
+  stream_sig_store(a.sig, a.sig_v);
+  extern __shared__ float X[];  // [(32 nt)][32] operand rows (>= kRedF floats), lse [32 nt], c [32 nt],
+                                // the pair's sparse entries, the pair's 65 row pointers
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int s = w & 1, hw = w >> 1;  // this wave's strip of the pair and its half of the tiles
+  const int nt = (a.N + 31) >> 5, NP = nt * 32, ns = (nt + 1) >> 1;
+  const int64_t half = (int64_t)a.B * a.K * ns;
+  const bool dq = blockIdx.x >= half;
+  const int64_t wg = dq ? blockIdx.x - half : blockIdx.x;
+  const int sp = (int)(wg % ns), bk = (int)(wg / ns), k = bk % a.K, b = bk / a.K;
+  const int r0 = sp * 64;                      // the pair's first row (dQ) / column (dK)
+  const int nr = min(64, a.N - r0);            // its rows
+  const bool live = s * 32 < nr;               // (wave-uniform: the pair's second strip may not exist)
+  const float* Q = a.qk + (int64_t)b * a.N * a.ld + k * 32;
+  const float* Kp = Q + a.kd;
+  const float* AM = a.am + (int64_t)k * a.N * a.N;
+  const float* AMT = a.amt + (int64_t)k * a.N * a.N;
+  const float* lseb = a.lse + (int64_t)bk * a.N;
+  const float* cb = a.cc + (int64_t)bk * a.N;
+  const int64_t zb = (int64_t)bk * a.nnz;
+  float* Ls = X + max(NP * 32, kRedF);
+  float (*red)[32][33] = reinterpret_cast<float (*)[32][33]>(X);  // [w]: after the last read of the rows
+  float* Cs = Ls + NP;
+  float* Ed = Cs + NP;
+  int* Ec = reinterpret_cast<int*>(Ed + kStripE2);
+  int* Pp = Ec + kStripE2;                     // row pointers r0 .. r0 + nr
+  const int own = min(r0 + 32 * s + l32, a.N - 1);
+  const int d = threadIdx.x & 31;
+  const int* ptr = dq ? a.csr_ptr : a.csc_ptr;
+  const int* eidx = dq ? a.csr_col : a.csc_row;
+  const float* edz = (dq ? a.dzs_r : a.dzs) + zb;
+  const int sbeg = ptr[r0], send = ptr[r0 + nr];
+  const bool staged = send - sbeg <= kStripE2;
+  int ec[kStripE2 / 256] = {};
+  float ed[kStripE2 / 256] = {};
+  if (staged && send > sbeg) {
+#pragma unroll
+    for (int u = 0; u < kStripE2 / 256; ++u) {
+      const int p = min(sbeg + (int)threadIdx.x + 256 * u, send - 1);
+      ec[u] = eidx[p];
+      ed[u] = edz[p];
+    }
+  }
+  const int pv0 = threadIdx.x <= nr ? ptr[r0 + (int)threadIdx.x] : 0;
+  float bv[16], am[TPW][16];
+  float lse_own = 0.f;
+  load16((dq ? Q : Kp) + (int64_t)own * a.ld + h * 16, bv);
+#pragma unroll
+  for (int q = 0; q < TPW; ++q) {
+    const int tt = hw + 2 * q;
+    if (tt < nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t o = (int64_t)min(tt * 32 + frag_row(r, h), a.N - 1) * a.N + own;
+        am[q][r] = dq ? AMT[o] : AM[o];
+      }
+  }
+  if (dq) {
+    stage_rows<2 * TPW>(Kp, a.ld, a.N, NP, X);  // (kIt >= NP 8 / 256 = nt; TPW = nt / 2 rounded up)
+    constexpr int LV = (TPW * 64 + 255) / 256;
+    float lv[LV], cv[LV];
+#pragma unroll
+    for (int u = 0; u < LV; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      lv[u] = e < a.N ? lseb[e] : INFINITY;
+      cv[u] = e < a.N ? cb[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < LV; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < NP) { Ls[e] = lv[u]; Cs[e] = cv[u]; }
+    }
+  } else {
+    lse_own = lseb[own];
+    stage_rows<2 * TPW>(Q, a.ld, a.N, NP, X);
+  }
+  if (staged) {
+#pragma unroll
+    for (int u = 0; u < kStripE2 / 256; ++u) {
+      const int p = sbeg + (int)threadIdx.x + 256 * u;
+      if (p < send) { Ec[p - sbeg] = ec[u]; Ed[p - sbeg] = ed[u]; }
+    }
+  }
+  if (threadIdx.x <= nr) Pp[threadIdx.x] = pv0;
+  __syncthreads();
+  floatx16 O = zero16();
+  if (live) {
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+      const int tt = hw + 2 * q;
+      if (tt >= nt) break;
+      float av[16];
+      lds16(X, tt * 32 + l32, h * 16, av);
+      floatx16 S = zero16();
+#pragma unroll
+      for (int st = 0; st < 16; ++st) S = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st], bv[st], S, 0, 0, 0);
+      float pv[16];
+      if (dq) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int jj = tt * 32 + frag_row(r, h);
+          pv[r] = __expf(S[r] * a.scale + am[q][r] - Ls[jj]) * Cs[jj];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          pv[r] = tt * 32 + frag_row(r, h) < a.N ? __expf(S[r] * a.scale + am[q][r] - lse_own) : 0.f;
+      }
+#pragma unroll
+      for (int st = 0; st < 16; ++st)
+        O = __builtin_amdgcn_mfma_f32_32x32x2f32(pv[st], X[xo(tt * 32 + frag_row(st, h), l32)], O, 0, 0, 0);
+    }
+  }
+  // the sparse term (the last reads of the staged rows): thread -> rows (tid >> 5) + 8 u of the pair
+  constexpr int RU = 8;
+  float spv[RU];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int rl = (threadIdx.x >> 5) + 8 * u;
+    float v = 0.f;
+    if (rl < nr) {
+      const int p0 = Pp[rl], p1 = Pp[rl + 1];
+      if (staged) {
+        for (int p = p0 - sbeg; p < p1 - sbeg; ++p) v = fmaf(Ed[p], X[xo(Ec[p], d)], v);
+      } else {
+        for (int p = p0; p < p1; ++p) v = fmaf(edz[p], X[xo(eidx[p], d)], v);
+      }
+    }
+    spv[u] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[w][frag_row(r, h)][l32] = O[r];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int rl = (threadIdx.x >> 5) + 8 * u, row = r0 + rl;
+    if (rl >= nr) continue;
+    const int ss = rl >> 5, rr = rl & 31;
+    const float dense = red[ss][rr][d] + red[2 + ss][rr][d];  // the strip's waves, hw = 0 then 1
+    if (dq) a.dqk[((int64_t)b * a.N + row) * a.ld + k * 32 + d] = (spv[u] - dense) * a.scale;
+    else a.dqk[((int64_t)b * a.N + row) * a.ld + a.kd + k * 32 + d] = (spv[u] - cb[row] * dense) * a.scale;
+  }
+}
+
 // backward, small graphs: dM_k[i,j] = A_pa[i,j] sum_b (dzs_b[i,j] - P_b[i,j] c_b[j]), every
 // element of the K (N,N) gradients written by one thread (0 off the A_pa support), P on the
 // support kept by the forward (papa), the T-support position of the entry from apa2t.
@@ -834,6 +989,23 @@ int op_flash_dqk(const ChebFl& a0, hipStream_t st) {
   a.sig = sg.p;
   a.sig_v = sg.v;
   const int nt = (a.N + 31) >> 5;
+  // N <= 192: two strips per workgroup (flash_small_dqk2_kernel; DSTAGNN_FLASH_DQK2=0: one)
+  static const bool dqk2 = !getenv("DSTAGNN_FLASH_DQK2") || atoi(getenv("DSTAGNN_FLASH_DQK2")) != 0;
+  if (a.am && dqk2 && nt <= 6) {
+    const int ns = (nt + 1) / 2;
+    const size_t lds = (std::max<size_t>((size_t)nt * 32 * 32, kRedF) + 2 * (size_t)nt * 32 + 2 * (size_t)kStripE2 + 65) *
+                       sizeof(float);
+    const dim3 grid((unsigned)(2 * (int64_t)a.B * a.K * ns));
+    switch (ns) {
+#define DS_DQK2(T) case T: DS_TRY(allow_lds(flash_small_dqk2_kernel<T>, lds)); \
+      hipLaunchKernelGGL((flash_small_dqk2_kernel<T>), grid, dim3(256), lds, st, a); break;
+      DS_DQK2(1) DS_DQK2(2) DS_DQK2(3)
+#undef DS_DQK2
+    }
+    DS_CHECK_LAUNCH();
+    if (sg.p) DS_TRY(stream_sig_sent(st, sg));
+    return 0;
+  }
   if (a.am) {  // small graphs (flash_small): dK' and dQ' strips in one launch
     const size_t lds = (std::max<size_t>((size_t)nt * 32 * 32, kRedF) + 2 * (size_t)nt * 32 + 2 * (size_t)kStripE) *
                        sizeof(float);
