@@ -81,10 +81,11 @@ FLASH_SMALL_N = 512  # cheb_flash.hip kSmallN: graphs up to this size take the L
 def use_flash(graph, meta, T, force=None, B=0):
     """Fused (flash-style) Chebyshev attention (cheb_flash.hip): the (B,K,N,N) scores, softmax
     and score gradient are never written; on the sparse path with d_k == 32 (the MFMA tile),
-    automatically for small graphs (N <= 512: one workgroup per 32-column strip, operands
-    staged once) and large ones (N >= 1024: one wave per strip, streamed tiles);
-    DSTAGNN_FLASH=0/1 overrides, as does `force`; batches up to 128 per call (the
-    mask-gradient kernel's lanes)."""
+    automatically: small graphs (N <= 512) take the LDS-staged kernels (one workgroup per
+    32-column strip, operands staged once), larger ones the streamed kernels (one wave per strip)
+    — at PEMS07's N = 883 as well (1.40 -> 1.31 ms per step against the dense (B,K,N,N) softmax
+    path, same box, round 6); DSTAGNN_FLASH=0/1 overrides, as does `force`; batches up to 128
+    per call (the mask-gradient kernel's lanes)."""
     if not use_sparse(graph, meta, T) or meta["d_k"] != 32 or B > 128:
         return False
     if force is not None:
@@ -92,8 +93,7 @@ def use_flash(graph, meta, T, force=None, B=0):
     env = os.environ.get("DSTAGNN_FLASH")
     if env is not None:
         return env == "1"
-    N = graph["adj_pa"].shape[0]
-    return N <= FLASH_SMALL_N or N >= 1024
+    return True
 
 
 def cfg_of(meta):

@@ -241,8 +241,8 @@ class DSTAGNN_block(nn.Module):
         self.num_of_d = num_of_d
         self.nb_time_filter = nb_time_filter
         self.sparse_cheb = True  # use the CSC/CSR support path when the support is sparse
-        # fused (flash-style) Chebyshev attention for large graphs: None = automatic (sparse
-        # path, d_k == 32, N >= 1024), True / False force it (block_fn.use_flash)
+        # fused (flash-style) Chebyshev attention: None = automatic (sparse path, d_k == 32),
+        # True / False force it (block_fn.use_flash)
         self.flash_cheb = None
         self.direct_grads = False  # see set_direct_grads
         self.grads_ready = None    # DP hook: called with the block once its gradients are final

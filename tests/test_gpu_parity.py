@@ -539,11 +539,11 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
 @pytest.mark.parametrize("name,first,B,flash", [
     ("pems04", False, 1, None), ("pems07", False, 1, None), ("gambia", True, 1, None), ("gambia", False, 1, None),
     ("syn", False, 1, None), ("t24", True, 1, None), ("t24", False, 1, None), ("pems08", False, 32, None),
-    # the fused (flash) Chebyshev attention is automatic for N <= 512 (the LDS-staged small-graph
-    # kernels: pems08, pems04, t24 above) and N >= 1024 (gambia, syn: the streamed kernels);
-    # forced on at PEMS07 (N = 883, streamed) and forced off at small and large N, so both
-    # paths are held to the oracle everywhere
-    ("pems07", False, 2, True), ("pems08", False, 4, False), ("pems08", True, 2, False), ("pems04", False, 2, False),
+    # the fused (flash) Chebyshev attention is automatic on the sparse path: N <= 512 the
+    # LDS-staged small-graph kernels (pems08, pems04, t24 above), larger N the streamed kernels
+    # (pems07, gambia, syn); forced off at small, middle and large N, so the dense softmax path
+    # is held to the oracle everywhere too
+    ("pems07", False, 2, False), ("pems08", False, 4, False), ("pems08", True, 2, False), ("pems04", False, 2, False),
     ("t24", False, 2, False), ("gambia", False, 1, False), ("t144k3", False, 2, None), ("t144k3", True, 1, None),
     ("t8", False, 3, None), ("t16", False, 2, None), ("t16", True, 2, None)])
 def test_block_vs_oracle_configs(name, first, B, flash):
