@@ -812,21 +812,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     }
   }
   // the sparse term (the last reads of the staged rows): thread -> rows (tid >> 5) + 8 u of the pair
-  constexpr int RU = 8;
+  // staged: the first kSpB entries of every row in one batch of independent LDS reads (the
+  // index, then the row element) instead of two dependent LDS round trips per entry; the rest
+  // (rows longer than kSpB) in order after them — the same summation order either way
+  constexpr int RU = 8, kSpB = 4;
   float spv[RU];
+  int pr0[RU], pr1[RU];
 #pragma unroll
   for (int u = 0; u < RU; ++u) {
     const int rl = (threadIdx.x >> 5) + 8 * u;
-    float v = 0.f;
-    if (rl < nr) {
-      const int p0 = Pp[rl], p1 = Pp[rl + 1];
-      if (staged) {
-        for (int p = p0 - sbeg; p < p1 - sbeg; ++p) v = fmaf(Ed[p], X[xo(Ec[p], d)], v);
-      } else {
-        for (int p = p0; p < p1; ++p) v = fmaf(edz[p], X[xo(eidx[p], d)], v);
+    pr0[u] = rl < nr ? Pp[rl] : 0;
+    pr1[u] = rl < nr ? Pp[rl + 1] : 0;
+  }
+  if (staged) {
+    int ci[RU][kSpB];
+    float cw[RU][kSpB];
+#pragma unroll
+    for (int u = 0; u < RU; ++u)
+#pragma unroll
+      for (int t = 0; t < kSpB; ++t) {
+        const int p = pr0[u] + t;
+        const bool ok = p < pr1[u];
+        ci[u][t] = ok ? Ec[p - sbeg] : 0;
+        cw[u][t] = ok ? Ed[p - sbeg] : 0.f;
       }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      float xv[kSpB];
+#pragma unroll
+      for (int t = 0; t < kSpB; ++t) xv[t] = X[xo(ci[u][t], d)];
+      float v = 0.f;
+#pragma unroll
+      for (int t = 0; t < kSpB; ++t) v = fmaf(cw[u][t], xv[t], v);  // (0 x row 0 past the row's end)
+      for (int p = pr0[u] + kSpB; p < pr1[u]; ++p) v = fmaf(Ed[p - sbeg], X[xo(Ec[p - sbeg], d)], v);
+      spv[u] = v;
     }
-    spv[u] = v;
+  } else {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      float v = 0.f;
+      for (int p = pr0[u]; p < pr1[u]; ++p) v = fmaf(edz[p], X[xo(eidx[p], d)], v);
+      spv[u] = v;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -876,6 +903,44 @@ __global__ __launch_bounds__(256) void flash_small_mask_kernel(ChebFl a) {
       if (b0 + u < a.B) s += dz[u] - pp[u] * cv[u];
   }
   dM[o] = a.apa[o] * s;
+}
+
+// the same gradient with the batch sum spread over the wave's lanes: the elements stay one per
+// lane (zeros off the support, coalesced), and the wave walks its own support entries (a ballot
+// over its 64 elements; ~1.5 per wave at PEMS08) one at a time, lane b loading sample b's
+// (dzs, P, c) — one load round per entry and a wave sum, where the per-thread loop paid B / 8
+// dependent rounds in its slowest lane.  B <= 128 (two samples per lane).  A fixed reduction
+// tree: deterministic, but not flash_small_mask_kernel's sequential order.
+__global__ __launch_bounds__(256) void flash_small_mask2_kernel(ChebFl a) {
+  const int64_t NN = (int64_t)a.N * a.N;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool in = e < (int64_t)a.K * NN;
+  const int k = in ? (int)(e / NN) : 0;
+  const int64_t o = in ? e - (int64_t)k * NN : 0;
+  float* dM = in ? a.dmask[k] : nullptr;
+  const int q = in ? a.apa_idx[o] : -1;
+  if (dM && q < 0) dM[o] = 0.f;
+  uint64_t mine = __ballot(dM != nullptr && q >= 0);
+  while (mine) {  // (wave-uniform)
+    const int src = __builtin_ctzll(mine);
+    mine &= mine - 1;
+    const int qs = __shfl(q, src, 64), ks = __shfl(k, src, 64);
+    const int64_t os = ((int64_t)__shfl((int)(o >> 32), src, 64) << 32) | (uint32_t)__shfl((int)o, src, 64);
+    const int j = (int)(os % a.N), pt = a.apa2t[qs];
+    float s = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b = lane + 64 * h;
+      if (b < a.B) {
+        const int64_t bk = (int64_t)b * a.K + ks;
+        const float dz = pt >= 0 ? a.dzs[bk * a.nnz + pt] : 0.f;
+        s += dz - a.papa[bk * a.apa_nnz + qs] * a.cc[bk * a.N + j];
+      }
+    }
+    s = wave_sum(s);
+    if (lane == src) dM[o] = a.apa[o] * s;
+  }
 }
 
 // backward: dM_k[i, :] for one (k, row i) per wave, every N entries written: zeros off the A_pa
@@ -1044,8 +1109,14 @@ int op_flash_mask_grad(const ChebFl& a, hipStream_t st) {
   // DSTAGNN_FLASH_MASK_COLS=1 keeps the column-wise kernel + zeroing pass (A/B)
   static const bool cols = getenv("DSTAGNN_FLASH_MASK_COLS") && atoi(getenv("DSTAGNN_FLASH_MASK_COLS")) != 0;
   if (a.papa && a.apa_idx && !cols) {  // small graphs: one thread per element, P from the forward
-    hipLaunchKernelGGL(flash_small_mask_kernel, dim3((unsigned)cdiv64((int64_t)a.K * a.N * a.N, 256)), dim3(256), 0,
-                       st, a);
+    // the batch sum over the wave's lanes (B <= 128; DSTAGNN_FLASH_MASK2=0: one thread per sum)
+    static const bool m2 = !getenv("DSTAGNN_FLASH_MASK2") || atoi(getenv("DSTAGNN_FLASH_MASK2")) != 0;
+    if (m2 && a.B <= 128)
+      hipLaunchKernelGGL(flash_small_mask2_kernel, dim3((unsigned)cdiv64((int64_t)a.K * a.N * a.N, 256)), dim3(256), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL(flash_small_mask_kernel, dim3((unsigned)cdiv64((int64_t)a.K * a.N * a.N, 256)), dim3(256), 0,
+                         st, a);
     DS_CHECK_LAUNCH();
     return 0;
   }

@@ -13,6 +13,8 @@ a subprocess (the library reads its switches once per process):
                        of sample pairs (=1 with B = 3: the pair kernels with a lone last sample)
   DSTAGNN_FLASH_DQK2=0 the small-graph dQ' / dK' kernel one strip per workgroup instead of two
                        (N <= 192)
+  DSTAGNN_FLASH_MASK2=0 the small-graph mask gradient summing the batch per thread instead of
+                       over a wave's lanes
   DSTAGNN_TF_WAVES=4 / DSTAGNN_TF_BWD_WAVES=4  the fused temporal-attention kernels on four waves
                        instead of eight
   DSTAGNN_GTU_TCONV=0  the GTU input gradient as the K-concatenated GEMM (run_gemm_kcat)
@@ -74,7 +76,7 @@ print("KNOB_OK")
                                        ("DSTAGNN_SDDMM_NOPF=1", "pems08", 4), ("DSTAGNN_GTU_TCONV=0", "pems08", 4),
                                        ("DSTAGNN_SDDMM_PAIR=0", "pems08", 4), ("DSTAGNN_SDDMM_PAIR=1", "pems08", 3),
                                        ("DSTAGNN_AGG_PAIR=0", "pems08", 4), ("DSTAGNN_AGG_PAIR=1", "pems08", 3),
-                                       ("DSTAGNN_FLASH_DQK2=0", "pems08", 4),
+                                       ("DSTAGNN_FLASH_DQK2=0", "pems08", 4), ("DSTAGNN_FLASH_MASK2=0", "pems08", 4),
                                        ("DSTAGNN_TF_WAVES=4", "pems08", 4), ("DSTAGNN_TF_BWD_WAVES=4", "pems08", 4),
                                        ("DSTAGNN_GTU_GCONV=1", "pems08", 4), ("DSTAGNN_GTU_GCONV=1", "t24", 2),
                                        ("DSTAGNN_TAIL_CT24=0", "t24", 2), ("DSTAGNN_KSIG=0", "pems08", 4),
