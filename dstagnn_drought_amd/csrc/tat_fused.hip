@@ -38,7 +38,6 @@ constexpr int kTfLC = kTfHV + 4;        // ... of the ctx tile
 constexpr int kTfQT = kTfQW / 16;       // 18 column tiles of Q|K|V
 constexpr int kTfQTW = (kTfQT + 3) / 4; // 5 per GEMM wave (the last of waves 2, 3 is a discarded duplicate)
 constexpr int kTfNmax = 320;            // N <= 320 (LDS: <= 156 KB)
-constexpr int kTfRPW = kTfRows / 4;     // LayerNorm rows per wave
 constexpr int kTfDsMax = 2304;          // (48 / T) h T^2 at T = 16
 constexpr int kTfG1 = 16;               // workgroups per level-1 group of the gamma / beta ticket tree
 

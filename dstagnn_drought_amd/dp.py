@@ -83,6 +83,21 @@ class GradAllReducer:
             self.items.append((n, p, idx))
         self.bucket_elems = max(1, bucket_bytes // 4)
         self._inflight = []  # (flat gradient buffer, async work) started during the backward
+        self._avg = None     # RCCL averages in the collective itself (ncclAvg): no scale kernel
+
+    def _mean_op(self):
+        """(op, scale-after?) of a mean all-reduce: AVG on the nccl (RCCL) backend, SUM and a
+        division elsewhere (gloo has no AVG)."""
+        if self._avg is None:
+            self._avg = dist.get_backend(self.group) == "nccl"
+        return (dist.ReduceOp.AVG, False) if self._avg else (dist.ReduceOp.SUM, True)
+
+    def _mean(self, t, world, async_op=False):
+        op, scale = self._mean_op()
+        work = dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
+        if not async_op and scale and world > 1:
+            t.div_(world)
+        return work
 
     def attach(self, model):
         """Overlap the exchange with the backward: every DSTAGNN_block of `model` in
@@ -123,7 +138,7 @@ class GradAllReducer:
             return  # reduced by all_reduce() (masks as their support only on the large graphs)
         if any(f.data_ptr() == flat.data_ptr() for f, _ in self._inflight):
             return
-        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        work = self._mean(flat, dist.get_world_size(self.group), async_op=True)
         self._inflight.append((flat, work))
 
     def _payload(self, p, idx):
@@ -154,7 +169,8 @@ class GradAllReducer:
         done = set()
         for flat, work in self._inflight:  # started during the backward (attach)
             work.wait()
-            flat.div_(world)
+            if self._mean_op()[1] and world > 1:
+                flat.div_(world)
             done.add(flat.data_ptr())
         self._inflight.clear()
         live = [(n, p, idx) for n, p, idx in self.items if p.grad is not None]
@@ -162,8 +178,7 @@ class GradAllReducer:
         for b in bases:
             if b.data_ptr() in done:
                 continue
-            dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group)
-            b.div_(world)
+            self._mean(b, world)
         live = [it for it in live if id(it[1]) not in taken]
         buckets, cur, size = [], [], 0
         for it in live:
@@ -177,8 +192,7 @@ class GradAllReducer:
             buckets.append(cur)
         for b in buckets:
             flat = torch.cat([self._payload(p, idx) for _, p, idx in b])
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-            flat.div_(world)
+            self._mean(flat, world)
             off = 0
             for _, p, idx in b:
                 g = p.grad.view(-1)
