@@ -866,9 +866,12 @@ struct Fwd {
     params_forked = on_side;
     hipStream_t q = on_side ? ks.sd : st;
     ParamPrep pp;
+    bool full = false;
+    PrepSeg spare;  // (a segment past the capacity lands here; the call then fails below)
     auto add = [&](int kind, const float* src, float* dst, int64_t n, int p0 = 0, int p1 = 0, int p2 = 0,
                    int64_t off = 0) {
-      PrepSeg& g = pp.seg[pp.nseg++];
+      full = full || pp.nseg >= kPrepSegsHost;
+      PrepSeg& g = full ? spare : pp.seg[pp.nseg++];
       g.kind = kind; g.src = src; g.dst = dst; g.n = n; g.p0 = p0; g.p1 = p1; g.p2 = p2; g.dst_off = off;
     };
     add(0, p.tat_wq, s.Wqkv, m.HQ * m.N, 0, 0, 0, 0);
@@ -912,6 +915,10 @@ struct Fwd {
         add(6, p.mask[k], s.amt + (int64_t)k * m.NN, m.NN, m.N);
         pp.seg[pp.nseg - 1].src2 = gr.adj_pa;
       }
+    if (full) {
+      set_last_error("param_prep: more parameter re-layouts than kPrepSegsHost");
+      return DSTAGNN_E_ARG;
+    }
     DS_TRY(op_param_prep(pp, q));
     return 0;
   }

@@ -1744,7 +1744,7 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(PackRows a) {
 }
 
 // blockIdx.y = segment; grid-stride over the segment's source elements
-__global__ __launch_bounds__(256) void param_prep_kernel(ParamPrep a) {
+__global__ __launch_bounds__(256) void param_prep_kernel(ParamPrepK a) {
   const PrepSeg& g = a.seg[blockIdx.y];
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.n; i += (int64_t)gridDim.x * 256) {
     if (g.kind == 8) {  // DESTINATION-indexed: src (R, p0) -> dst (R, p1) rows zero-padded to p1 >= p0
@@ -2164,12 +2164,21 @@ int op_cheb_mask_grad(const ChebSm& a, hipStream_t st) {
 
 int op_param_prep(const ParamPrep& a, hipStream_t st) {
   if (a.nseg <= 0) return 0;
-  if (a.nseg > kPrepSegs) { set_last_error("param_prep: too many segments"); return DSTAGNN_E_ARG; }
-  int64_t mx = 1;
-  for (int q = 0; q < a.nseg; ++q) mx = std::max<int64_t>(mx, a.seg[q].n);
-  hipLaunchKernelGGL(param_prep_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(mx, 256), 256), (unsigned)a.nseg),
-                     dim3(256), 0, st, a);
-  DS_CHECK_LAUNCH();
+  if (a.nseg > kPrepSegsHost) { set_last_error("param_prep: too many segments"); return DSTAGNN_E_ARG; }
+  // chunks of kPrepSegs segments per launch (K >= 4 on the small-graph attention path needs
+  // more: 2 K mask re-layouts + K Theta blocks beside the fixed ones)
+  for (int q0 = 0; q0 < a.nseg; q0 += kPrepSegs) {
+    ParamPrepK k;
+    k.nseg = std::min(kPrepSegs, a.nseg - q0);
+    int64_t mx = 1;
+    for (int q = 0; q < k.nseg; ++q) {
+      k.seg[q] = a.seg[q0 + q];
+      mx = std::max<int64_t>(mx, k.seg[q].n);
+    }
+    hipLaunchKernelGGL(param_prep_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(mx, 256), 256), (unsigned)k.nseg),
+                       dim3(256), 0, st, k);
+    DS_CHECK_LAUNCH();
+  }
   return 0;
 }
 int op_pack_rows(const PackRows& a, hipStream_t st) {

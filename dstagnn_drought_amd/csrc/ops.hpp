@@ -93,10 +93,15 @@ struct PrepSeg {
   const float* src2 = nullptr;  // kind 5
   float* dst = nullptr;
 };
-constexpr int kPrepSegs = 32;
-struct ParamPrep {
+constexpr int kPrepSegs = 32;      // segments per launch (the kernel argument)
+constexpr int kPrepSegsHost = 96;  // segments per call (op_param_prep launches them in chunks)
+struct ParamPrepK {
   int nseg = 0;
   PrepSeg seg[kPrepSegs];
+};
+struct ParamPrep {
+  int nseg = 0;
+  PrepSeg seg[kPrepSegsHost];
 };
 
 // fused per-node GTU gates + fcmy + dropout + residual + LayerNorm (gtu_tail.hip)

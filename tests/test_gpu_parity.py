@@ -383,6 +383,10 @@ CONFIGS = {
     # an odd number of 32-node strips (5): the two-strip small-graph dQ'/dK' kernel's last pair
     # holds one strip (its second pair of waves idle), with N <= 192 so that kernel runs
     "n150": (150, 12, 3, 3, 64, 32, 32),
+    # Chebyshev orders 2 and 5 at T <= 16: the sample-pair aggregate-first kernels' other order
+    # templates (KM = 2: 8 dot products a batch; KM = 5: 20, reduced as 32)
+    "k2t12": (64, 12, 2, 3, 64, 32, 32),
+    "k5t8": (40, 8, 5, 3, 64, 32, 32),
 }
 RELU_EPS = 1e-5  # ReLU decisions may differ from the fp64 oracle's only where |z| <= RELU_EPS * max|z|
 
@@ -549,7 +553,8 @@ def _run_config_vs_oracle(name, first, B, seed=3, flash=None, tol=TOL, relu_eps=
     ("pems07", False, 2, False), ("pems08", False, 4, False), ("pems08", True, 2, False), ("pems04", False, 2, False),
     ("t24", False, 2, False), ("gambia", False, 1, False), ("t144k3", False, 2, None), ("t144k3", True, 1, None),
     ("t8", False, 3, None), ("t16", False, 2, None), ("t16", True, 2, None),
-    ("n150", False, 3, None), ("n150", True, 2, None)])
+    ("n150", False, 3, None), ("n150", True, 2, None), ("k2t12", False, 3, None), ("k2t12", True, 2, None),
+    ("k5t8", False, 3, None), ("k5t8", True, 2, None)])
 def test_block_vs_oracle_configs(name, first, B, flash):
     """Held against the oracle evaluated in float64 (pems08 at B=32: the bench configuration
     itself).  Bound per tensor: the stated 1e-4 (scaled by max(1, max|ref|)), or twice the
